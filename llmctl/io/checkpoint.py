@@ -1,0 +1,318 @@
+"""Sharded, asynchronous checkpointing with resharding on load.
+
+Reference layout (``engine.py:363-394``) is kept and extended::
+
+    <output_dir>/checkpoint-<step>/ | final/
+        model.safetensors                       (tp=pp=1)  or
+        model-0000r-of-0000N.safetensors + model.safetensors.index.json   (one per TP×PP shard)
+        config.json                             (model JSON; absent in the reference)
+        training_state.json                     {"global_step","epoch","config", + scheduler,
+                                                 consumed_samples, world_size, layout, data}
+        optimizer/rank_XXXXX.pt                 fp32 master + Adam moments (ZeRO shard)
+        rng/rank_XXXXX.pt
+        plan.toml                               (when a plan drove the run)
+    <output_dir>/latest                         name of the newest complete checkpoint
+
+Tensor names are layout-independent: ``layers.<global_idx>.<param>`` with full (unsharded)
+shapes recorded in the index, so a checkpoint written at TP=a/PP=b loads at TP=c/PP=d
+(:func:`consolidate_tp` / :func:`shard_tp`).  Writes are rank-parallel (each TP×PP shard
+owner at DP rank 0 writes its model file, every rank its optimizer shard), done on a
+background thread after a device→pinned-host copy, and committed by a barrier + ``latest``
+pointer update (``keep_latest`` GC as in the reference config ``checkpoint.keep_latest``).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import threading
+from pathlib import Path
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+# ----------------------------------------------------------------------------- TP (re)sharding
+# how each parameter is split across tensor-parallel ranks
+#   ("rows", parts)  - dim 0, each rank's block is the concat of `parts` sub-blocks
+#   ("cols", 1)      - dim 1
+#   None             - replicated
+
+
+def tp_split_rule(name: str, cfg) -> Optional[tuple]:
+    leaf = name.split(".")[-1]
+    if leaf in ("wqkv", "bqkv"):
+        return ("rows", (cfg.heads, cfg.kv_heads, cfg.kv_heads))
+    if leaf in ("w_up", "b_up"):
+        return ("rows", (1, 1) if cfg.gated_mlp else (1,))
+    if leaf in ("embed", "lm_head"):
+        return ("rows", (1,))
+    if leaf in ("wo", "w_down"):
+        return ("cols", None)
+    return None
+
+
+def consolidate_tp(name: str, shards: List[torch.Tensor], cfg) -> torch.Tensor:
+    rule = tp_split_rule(name, cfg)
+    if rule is None or len(shards) == 1:
+        return shards[0]
+    kind, parts = rule
+    if kind == "cols":
+        return torch.cat(shards, dim=1)
+    weights = parts
+    tot = sum(weights)
+    pieces: List[List[torch.Tensor]] = [[] for _ in weights]
+    for s in shards:
+        n = s.shape[0]
+        unit = n // tot
+        o = 0
+        for i, w in enumerate(weights):
+            pieces[i].append(s[o:o + unit * w])
+            o += unit * w
+    return torch.cat([torch.cat(p, 0) for p in pieces], 0)
+
+
+def shard_tp(name: str, full: torch.Tensor, tp: int, rank: int, cfg) -> torch.Tensor:
+    rule = tp_split_rule(name, cfg)
+    if rule is None or tp == 1:
+        return full
+    kind, parts = rule
+    if kind == "cols":
+        n = full.shape[1] // tp
+        return full[:, rank * n:(rank + 1) * n]
+    tot = sum(parts)
+    unit_full = full.shape[0] // tot
+    out, o = [], 0
+    for w in parts:
+        blk = full[o:o + unit_full * w]
+        n = blk.shape[0] // tp
+        out.append(blk[rank * n:(rank + 1) * n])
+        o += unit_full * w
+    return torch.cat(out, 0)
+
+
+def _global_name(name: str, layer_start: int) -> str:
+    # "layers.<local>.x" -> "layers.<global>.x"
+    if name.startswith("layers."):
+        parts = name.split(".")
+        parts[1] = str(int(parts[1]) + layer_start)
+        return ".".join(parts)
+    return name
+
+
+def _local_name(name: str, layer_start: int) -> str:
+    if name.startswith("layers."):
+        parts = name.split(".")
+        parts[1] = str(int(parts[1]) - layer_start)
+        return ".".join(parts)
+    return name
+
+
+# ----------------------------------------------------------------------------- manager
+class CheckpointManager:
+    def __init__(self, engine, output_dir: str):
+        self.engine = engine
+        self.root = Path(output_dir)
+        self._thread: Optional[threading.Thread] = None
+        self._error: Optional[BaseException] = None
+
+    # ------------------------------------------------------------------ save
+    def save(self, name: str, final: bool = False) -> Path:
+        e = self.engine
+        c = e.config
+        self.wait()
+        path = self.root / name
+        pg = e.pg
+        rank = pg.rank
+        world = pg.layout.world_size
+        if e.is_main:
+            path.mkdir(parents=True, exist_ok=True)
+        if dist.is_initialized():
+            dist.barrier()
+        path.mkdir(parents=True, exist_ok=True)
+        # ---- device -> host snapshot (synchronous, so training can continue right away)
+        shard_id = pg.pp_rank * pg.layout.tp + pg.tp_rank
+        n_shards = pg.layout.tp * pg.layout.pp
+        write_model = pg.dp_rank == 0
+        model_sd = {}
+        if write_model:
+            if getattr(e, "zero3", None) is not None:
+                named = e.zero3.full_named_parameters()
+            else:
+                named = list(e.model.named_parameters())
+            for n, p in named:
+                model_sd[_global_name(n, e.pc.layer_start)] = p.detach().to("cpu", copy=True).contiguous()
+        opt_sd = {k: (v.detach().to("cpu", copy=True) if torch.is_tensor(v) else v)
+                  for k, v in e.optimizer.state_dict().items()}
+        rng = {"cpu": torch.get_rng_state(), "cuda": torch.cuda.get_rng_state() if e.device.type == "cuda" else None}
+        state = {
+            "global_step": e.global_step, "epoch": e.epoch,
+            "config": {k: (list(v) if isinstance(v, tuple) else v) for k, v in vars(c).items()},
+            "scheduler": e.scheduler.state_dict(), "consumed_samples": e.consumed_samples,
+            "world_size": world, "layout": {"tp": pg.layout.tp, "pp": pg.layout.pp, "dp": pg.layout.dp},
+            "zero_stage": c.zero_stage,
+        }
+
+        def _write():
+            try:
+                from safetensors.torch import save_file
+
+                if write_model:
+                    fname = "model.safetensors" if n_shards == 1 else f"model-{shard_id + 1:05d}-of-{n_shards:05d}.safetensors"
+                    meta = {"tp_rank": str(pg.tp_rank), "tp": str(pg.layout.tp), "pp_rank": str(pg.pp_rank),
+                            "pp": str(pg.layout.pp), "format": "pt"}
+                    save_file(model_sd, str(path / fname), metadata=meta)
+                (path / "optimizer").mkdir(exist_ok=True)
+                torch.save(opt_sd, path / "optimizer" / f"rank_{rank:05d}.pt")
+                (path / "rng").mkdir(exist_ok=True)
+                torch.save(rng, path / "rng" / f"rank_{rank:05d}.pt")
+            except BaseException as ex:  # surfaced by wait()
+                self._error = ex
+
+        if c.async_checkpoint and not final:
+            self._thread = threading.Thread(target=_write, daemon=True)
+            self._thread.start()
+        else:
+            _write()
+        self._commit_after(path, state, n_shards)
+        return path
+
+    def _commit_after(self, path: Path, state: Dict[str, Any], n_shards: int) -> None:
+        """Metadata + barrier + latest pointer; runs after the shard writes complete."""
+        e = self.engine
+
+        def _finish():
+            if self._thread is not None:
+                self._thread.join()
+            if self._error is not None:
+                raise self._error
+
+        self._pending_commit = (path, state, n_shards, _finish)
+        if not (e.config.async_checkpoint and self._thread is not None):
+            self._do_commit()
+
+    def _do_commit(self):
+        pc = getattr(self, "_pending_commit", None)
+        if pc is None:
+            return
+        path, state, n_shards, finish = pc
+        self._pending_commit = None
+        finish()
+        e = self.engine
+        if dist.is_initialized():
+            dist.barrier()
+        if e.is_main:
+            (path / "config.json").write_text(json.dumps(e.model_config.to_dict(), indent=2))
+            (path / "training_state.json").write_text(json.dumps(state, indent=2, default=str))
+            if n_shards > 1:
+                weight_map = {}
+                for f in sorted(path.glob("model-*.safetensors")):
+                    from safetensors import safe_open
+
+                    with safe_open(str(f), "pt") as sf:
+                        for k in sf.keys():
+                            weight_map.setdefault(k, []).append(f.name)
+                (path / "model.safetensors.index.json").write_text(json.dumps(
+                    {"metadata": {"tp": state["layout"]["tp"], "pp": state["layout"]["pp"]},
+                     "weight_map": weight_map}, indent=2))
+            if e.config.plan_file and Path(e.config.plan_file).exists():
+                shutil.copy(e.config.plan_file, path / "plan.toml")
+            (self.root / "latest").write_text(path.name)
+            self._gc()
+
+    def wait(self) -> None:
+        if getattr(self, "_pending_commit", None) is not None:
+            self._do_commit()
+        self._thread = None
+
+    def _gc(self) -> None:
+        keep = self.engine.config.keep_latest or self.engine.config.save_total_limit
+        if not keep or keep <= 0:
+            return
+        ckpts = sorted((p for p in self.root.glob("checkpoint-*") if p.is_dir()),
+                       key=lambda p: int(p.name.split("-")[-1]))
+        for p in ckpts[:-keep]:
+            shutil.rmtree(p, ignore_errors=True)
+
+    # ------------------------------------------------------------------ load
+    def load(self, path: str) -> None:
+        e = self.engine
+        p = Path(path)
+        if p.is_dir() and (p / "latest").exists() and not (p / "training_state.json").exists():
+            p = p / (p / "latest").read_text().strip()
+        state = json.loads((p / "training_state.json").read_text())
+        full = load_full_state_dict(p, e.model_config)
+        # re-shard for this rank's layout
+        named = (e.zero3.full_named_parameters() if getattr(e, "zero3", None) is not None
+                 else list(e.model.named_parameters()))
+        with torch.no_grad():
+            for n, prm in named:
+                g = _global_name(n, e.pc.layer_start)
+                if g not in full:
+                    raise KeyError(f"checkpoint {p} lacks tensor {g}")
+                t = shard_tp(g, full[g], e.pg.layout.tp, e.pg.tp_rank, e.model_config)
+                prm.copy_(t.to(prm.dtype))
+        if getattr(e, "zero3", None) is not None:
+            e.zero3.reload_shards_from_full()
+        same_layout = (state.get("layout") == {"tp": e.pg.layout.tp, "pp": e.pg.layout.pp, "dp": e.pg.layout.dp}
+                       and state.get("zero_stage", 0) == e.config.zero_stage)
+        opt_file = p / "optimizer" / f"rank_{e.pg.rank:05d}.pt"
+        if same_layout and opt_file.exists():
+            e.optimizer.load_state_dict(torch.load(opt_file, map_location=e.device, weights_only=True))
+        else:
+            # layout changed: masters restart from the (resharded) bf16 weights
+            _reinit_master_from_params(e)
+            e.optimizer.step_count = int(state.get("global_step", 0))
+        rng_file = p / "rng" / f"rank_{e.pg.rank:05d}.pt"
+        if rng_file.exists():
+            rng = torch.load(rng_file, weights_only=True)
+            torch.set_rng_state(rng["cpu"])
+            if rng.get("cuda") is not None and e.device.type == "cuda":
+                torch.cuda.set_rng_state(rng["cuda"])
+        e.global_step = int(state["global_step"])
+        e.epoch = int(state.get("epoch", 0))
+        e.consumed_samples = int(state.get("consumed_samples", 0))
+
+
+def _reinit_master_from_params(e) -> None:
+    opt = e.optimizer
+    f = e.flat
+    with torch.no_grad():
+        if opt.zero_stage == 0:
+            opt.master.copy_(f.data.float())
+        else:
+            for b in f.buckets:
+                off, c = opt.shard_offsets[b.index]
+                s = b.start + opt.dp_rank * c
+                opt.master[off:off + c].copy_(f.data[s:s + c].float())
+        opt.exp_avg.zero_()
+        opt.exp_avg_sq.zero_()
+
+
+def load_full_state_dict(path, model_cfg) -> Dict[str, torch.Tensor]:
+    """Load a (possibly TP/PP-sharded) checkpoint directory into full, unsharded tensors."""
+    from safetensors import safe_open
+
+    p = Path(path)
+    single = p / "model.safetensors"
+    if single.exists():
+        out = {}
+        with safe_open(str(single), "pt") as sf:
+            for k in sf.keys():
+                out[k] = sf.get_tensor(k)
+        return out
+    files = sorted(p.glob("model-*.safetensors"))
+    if not files:
+        raise FileNotFoundError(f"no model weights in {p}")
+    by_name: Dict[str, Dict[int, torch.Tensor]] = {}
+    for f in files:
+        with safe_open(str(f), "pt") as sf:
+            meta = sf.metadata() or {}
+            tr = int(meta.get("tp_rank", 0))
+            for k in sf.keys():
+                by_name.setdefault(k, {})[tr] = sf.get_tensor(k)
+    out = {}
+    for k, shards in by_name.items():
+        out[k] = consolidate_tp(k, [shards[i] for i in sorted(shards)], model_cfg)
+    return out

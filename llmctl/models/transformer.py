@@ -1,0 +1,317 @@
+"""Decoder-only transformer (Llama-style and GPT-2-style) built on llmctl's fused ops.
+
+Replaces the reference's HF ``AutoModelForCausalLM`` (``llmctl/runtime/engine.py:119-140``):
+weights are random-initialised from the model JSON (no Hub access on the GPU box), and
+every non-GEMM op is a hand-written HIP kernel (``llmctl.ops``).  GEMMs go to hipBLASLt via
+``torch.nn.functional.linear`` on token-major ``[T, features]`` activations; fused weights
+(``wqkv``, ``w_gate_up``) keep the GEMM count at 4 per layer.
+
+Parallelism hooks (see ``llmctl.parallel``):
+* tensor parallel — ``wqkv``/``w_gate_up`` column-parallel, ``wo``/``w_down`` row-parallel,
+  vocab-parallel embedding / lm_head / cross-entropy;
+* sequence parallel — residual stream sharded on tokens inside the TP group;
+* pipeline parallel — a stage owns ``layers[lo:hi]`` plus optionally embed / head.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from llmctl import ops
+from llmctl.parallel import tensor_parallel as tp
+from .config import ModelConfig
+
+
+@dataclass
+class ParallelContext:
+    tp_group: Optional[object] = None
+    tp_size: int = 1
+    tp_rank: int = 0
+    sequence_parallel: bool = False
+    # pipeline stage description
+    layer_start: int = 0
+    layer_end: Optional[int] = None
+    has_embedding: bool = True
+    has_head: bool = True
+    # recompute policy: "none" | "selective" | "full"
+    activation_checkpoint: str = "none"
+
+
+def _init_linear(w: torch.Tensor, std: float) -> None:
+    with torch.no_grad():
+        w.normal_(0.0, std)
+
+
+class _SwiGLUDown(torch.autograd.Function):
+    """Selective recompute: ``down(swiglu(gu))`` saving only ``gu`` (the [T, ffn]
+    activation is recomputed by the swiglu kernel in backward — one extra memory-bound
+    pass in exchange for T*ffn*2 bytes per layer)."""
+
+    @staticmethod
+    def forward(ctx, gu, w_down):
+        from llmctl.ops._lib import native, use_native
+        from llmctl.ops import ref
+
+        act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
+        out = F.linear(act, w_down)
+        ctx.save_for_backward(gu, w_down)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        gu, w_down = ctx.saved_tensors
+        from llmctl.ops._lib import native, use_native
+        from llmctl.ops import ref
+
+        act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
+        dout2 = dout.reshape(-1, dout.shape[-1])
+        dw = dout2.t().matmul(act.reshape(-1, act.shape[-1]))
+        dact = dout.matmul(w_down)
+        dgu = native().swiglu_bwd(dact, gu) if use_native(gu) else ref.swiglu_bwd(dact, gu)
+        return dgu, dw
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, pc: ParallelContext, layer_idx: int, device=None, dtype=None):
+        super().__init__()
+        self.cfg, self.pc, self.idx = cfg, pc, layer_idx
+        t = pc.tp_size
+        if cfg.heads % t or cfg.kv_heads % t or cfg.ffn % t:
+            raise ValueError(f"heads/kv_heads/ffn must divide tp={t}")
+        self.nq, self.nkv, self.D = cfg.heads // t, cfg.kv_heads // t, cfg.head_dim
+        self.f = cfg.ffn // t
+        h = cfg.hidden
+        kw = dict(device=device, dtype=dtype)
+        ln = cfg.norm == "layernorm"
+        self.attn_norm_w = nn.Parameter(torch.ones(h, **kw))
+        self.mlp_norm_w = nn.Parameter(torch.ones(h, **kw))
+        self.attn_norm_b = nn.Parameter(torch.zeros(h, **kw)) if ln else None
+        self.mlp_norm_b = nn.Parameter(torch.zeros(h, **kw)) if ln else None
+        self.wqkv = nn.Parameter(torch.empty((self.nq + 2 * self.nkv) * self.D, h, **kw))
+        self.wo = nn.Parameter(torch.empty(h, self.nq * self.D, **kw))
+        gated = cfg.gated_mlp
+        self.w_up = nn.Parameter(torch.empty((2 if gated else 1) * self.f, h, **kw))
+        self.w_down = nn.Parameter(torch.empty(h, self.f, **kw))
+        if ln:  # GPT-2 style biases (row-parallel biases are replicated, added after the reduce)
+            self.bqkv = nn.Parameter(torch.zeros((self.nq + 2 * self.nkv) * self.D, **kw))
+            self.bo = nn.Parameter(torch.zeros(h, **kw))
+            self.b_up = nn.Parameter(torch.zeros((2 if gated else 1) * self.f, **kw))
+            self.b_down = nn.Parameter(torch.zeros(h, **kw))
+        else:
+            self.bqkv = self.bo = self.b_up = self.b_down = None
+        std = 0.02
+        _init_linear(self.wqkv, std)
+        _init_linear(self.w_up, std)
+        _init_linear(self.wo, std / math.sqrt(2 * cfg.layers))
+        _init_linear(self.w_down, std / math.sqrt(2 * cfg.layers))
+        for p in (self.attn_norm_w, self.mlp_norm_w, self.attn_norm_b, self.mlp_norm_b, self.bo, self.b_down):
+            if p is not None:
+                p.tp_replicated = True  # identical on every TP rank (partial grads under SP)
+
+    # -- norm helpers --------------------------------------------------------------
+    def _norm(self, x, w, b):
+        eps = self.cfg.layer_norm_eps
+        return ops.layernorm(x, w, b, eps) if b is not None else ops.rmsnorm(x, w, eps)
+
+    def _add_norm(self, x, res, w, b):
+        eps = self.cfg.layer_norm_eps
+        return ops.add_layernorm(x, res, w, b, eps) if b is not None else ops.add_rmsnorm(x, res, w, eps)
+
+    def _col_in(self, x):
+        pc = self.pc
+        if pc.tp_size == 1:
+            return x
+        return tp.gather_from_sp(x, pc.tp_group) if pc.sequence_parallel else tp.copy_to_tp(x, pc.tp_group)
+
+    def _row_out(self, x):
+        pc = self.pc
+        if pc.tp_size == 1:
+            return x
+        return tp.reduce_scatter_to_sp(x, pc.tp_group) if pc.sequence_parallel else tp.reduce_from_tp(x, pc.tp_group)
+
+    def attention(self, xn, B, S, rope, positions=None):
+        qkv = F.linear(self._col_in(xn), self.wqkv, self.bqkv)
+        if rope is not None:
+            q, k, v = ops.rope_qkv(qkv, rope[0], rope[1], self.nq, self.nkv, S, positions)
+        else:
+            T = qkv.shape[0]
+            x = qkv.view(T, self.nq + 2 * self.nkv, self.D)
+            q, k, v = x[:, :self.nq].contiguous(), x[:, self.nq:self.nq + self.nkv].contiguous(), \
+                x[:, self.nq + self.nkv:].contiguous()
+        q = q.view(B, S, self.nq, self.D)
+        k = k.view(B, S, self.nkv, self.D)
+        v = v.view(B, S, self.nkv, self.D)
+        o = ops.flash_attention(q, k, v, causal=True)
+        out = F.linear(o.view(B * S, self.nq * self.D), self.wo)
+        out = self._row_out(out)
+        if self.bo is not None:
+            out = out + self.bo
+        return out
+
+    def mlp(self, xn):
+        x = self._col_in(xn)
+        if self.cfg.gated_mlp:
+            gu = F.linear(x, self.w_up, self.b_up)
+            if self.pc.activation_checkpoint == "selective":
+                out = _SwiGLUDown.apply(gu, self.w_down)
+            else:
+                out = F.linear(ops.swiglu(gu), self.w_down)
+        else:
+            hdn = ops.gelu(F.linear(x, self.w_up, self.b_up))
+            out = F.linear(hdn, self.w_down)
+        out = self._row_out(out)
+        if self.b_down is not None:
+            out = out + self.b_down
+        return out
+
+    def forward(self, x, residual, B, S, rope, positions=None):
+        """Pre-norm block with fused residual-add + norm.
+
+        ``residual`` is the running residual stream (None for the first layer);
+        ``x`` is the previous block's output to be added into it.
+        Returns (block_output, residual) — the add of block_output is deferred into the
+        next layer's fused add+norm kernel."""
+        if residual is None:
+            residual = x
+            xn = self._norm(x, self.attn_norm_w, self.attn_norm_b)
+        else:
+            xn, residual = self._add_norm(x, residual, self.attn_norm_w, self.attn_norm_b)
+        a = self.attention(xn, B, S, rope, positions)
+        xn2, residual = self._add_norm(a, residual, self.mlp_norm_w, self.mlp_norm_b)
+        m = self.mlp(xn2)
+        return m, residual
+
+
+class DecoderLM(nn.Module):
+    """Causal LM.  ``forward(input_ids [B,S], labels [B,S]|None)`` -> mean loss or logits."""
+
+    def __init__(self, cfg: ModelConfig, pc: Optional[ParallelContext] = None, device=None,
+                 dtype: torch.dtype = torch.bfloat16):
+        super().__init__()
+        self.cfg = cfg
+        self.pc = pc = pc or ParallelContext()
+        end = pc.layer_end if pc.layer_end is not None else cfg.layers
+        kw = dict(device=device, dtype=dtype)
+        t = pc.tp_size
+        h = cfg.hidden
+        if cfg.vocab_size % t:
+            raise ValueError(f"vocab {cfg.vocab_size} not divisible by tp={t}")
+        self.vocab_local = cfg.vocab_size // t
+        self.vocab_start = pc.tp_rank * self.vocab_local
+        self.embed = None
+        self.pos_embed = None
+        if pc.has_embedding:
+            self.embed = nn.Parameter(torch.empty(self.vocab_local, h, **kw))
+            _init_linear(self.embed, 0.02)
+            if cfg.position == "learned":
+                self.pos_embed = nn.Parameter(torch.empty(cfg.max_position_embeddings, h, **kw))
+                _init_linear(self.pos_embed, 0.01)
+        self.layers = nn.ModuleList(
+            [DecoderLayer(cfg, pc, i, **kw) for i in range(pc.layer_start, end)]
+        )
+        self.final_norm_w = self.final_norm_b = self.lm_head = None
+        if pc.has_head:
+            self.final_norm_w = nn.Parameter(torch.ones(h, **kw))
+            if cfg.norm == "layernorm":
+                self.final_norm_b = nn.Parameter(torch.zeros(h, **kw))
+            if not (cfg.tie_word_embeddings and pc.has_embedding):
+                self.lm_head = nn.Parameter(torch.empty(self.vocab_local, h, **kw))
+                _init_linear(self.lm_head, 0.02)
+        for p in (self.pos_embed, self.final_norm_w, self.final_norm_b):
+            if p is not None:
+                p.tp_replicated = True
+        self._rope_cache = {}
+
+    # ------------------------------------------------------------------ helpers
+    def head_weight(self):
+        return self.lm_head if self.lm_head is not None else self.embed
+
+    def rope_tables(self, S: int, device):
+        if self.cfg.position != "rope":
+            return None
+        key = (max(S, 1), str(device))
+        if key not in self._rope_cache:
+            r = self.cfg.rope or {}
+            n = max(S, self.cfg.max_position_embeddings)
+            self._rope_cache[key] = ops.ref.rope_tables(
+                n, self.cfg.head_dim, base=float(r.get("base", 10000)), scaling=r.get("scaling", "linear"),
+                factor=float(r.get("factor", 1.0)), short_factor=r.get("short_factor"),
+                long_factor=r.get("long_factor"), original_max_position=r.get("original_max_position"),
+                device=device)
+        return self._rope_cache[key]
+
+    def embed_tokens(self, input_ids: torch.Tensor) -> torch.Tensor:
+        B, S = input_ids.shape
+        ids = input_ids.reshape(-1)
+        pc = self.pc
+        if pc.tp_size > 1:
+            x = tp.vocab_parallel_embedding(ids, self.embed, self.vocab_start, pc.tp_group, pc.sequence_parallel)
+        else:
+            x = F.embedding(ids, self.embed)
+        if self.pos_embed is not None:
+            pos = self.pos_embed[:S].repeat(B, 1)
+            if pc.tp_size > 1 and pc.sequence_parallel:
+                pos = tp._split_tokens(pos, pc.tp_group)
+            x = x + pos
+        return x
+
+    def run_layers(self, x, B, S, residual=None, positions=None):
+        rope = self.rope_tables(S, x.device)
+        ac = self.pc.activation_checkpoint
+        for layer in self.layers:
+            if ac == "full" and self.training and torch.is_grad_enabled():
+                if residual is None:
+                    x, residual = torch.utils.checkpoint.checkpoint(
+                        lambda a, l=layer: l(a, None, B, S, rope, positions), x, use_reentrant=False)
+                else:
+                    x, residual = torch.utils.checkpoint.checkpoint(
+                        lambda a, r, l=layer: l(a, r, B, S, rope, positions), x, residual, use_reentrant=False)
+            else:
+                x, residual = layer(x, residual, B, S, rope, positions)
+        return x, residual
+
+    def head(self, x, residual):
+        cfg = self.cfg
+        if residual is None:
+            xn = (ops.layernorm(x, self.final_norm_w, self.final_norm_b, cfg.layer_norm_eps)
+                  if self.final_norm_b is not None else ops.rmsnorm(x, self.final_norm_w, cfg.layer_norm_eps))
+        else:
+            xn, _ = (ops.add_layernorm(x, residual, self.final_norm_w, self.final_norm_b, cfg.layer_norm_eps)
+                     if self.final_norm_b is not None
+                     else ops.add_rmsnorm(x, residual, self.final_norm_w, cfg.layer_norm_eps))
+        pc = self.pc
+        if pc.tp_size > 1:
+            xn = tp.gather_from_sp(xn, pc.tp_group) if pc.sequence_parallel else tp.copy_to_tp(xn, pc.tp_group)
+        return F.linear(xn, self.head_weight())
+
+    def loss(self, logits, labels, denom: Optional[float] = None):
+        pc = self.pc
+        lab = labels.reshape(-1)
+        if denom is None:
+            denom = float(lab.numel())
+        if pc.tp_size > 1:
+            return tp.vocab_parallel_cross_entropy(logits, lab, self.vocab_start, pc.tp_group, denom)
+        return ops.cross_entropy(logits, lab, reduction_denom=denom)
+
+    def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
+                loss_denom: Optional[float] = None):
+        B, S = input_ids.shape
+        x = self.embed_tokens(input_ids)
+        x, residual = self.run_layers(x, B, S)
+        logits = self.head(x, residual)
+        if labels is None:
+            return logits
+        return self.loss(logits, labels, loss_denom)
+
+
+def build_model(cfg: ModelConfig, device=None, dtype=torch.bfloat16, pc: Optional[ParallelContext] = None,
+                seed: Optional[int] = None) -> DecoderLM:
+    if seed is not None:
+        torch.manual_seed(seed)
+    return DecoderLM(cfg, pc=pc, device=device, dtype=dtype)

@@ -1,0 +1,31 @@
+"""Hand-written CDNA4 (gfx950) HIP kernels for the hot ops + their autograd wrappers.
+
+Kernel sources live in ``llmctl/ops/csrc/*.hip`` and build in-tree into
+``llmctl/ops/_llmctl_hip.so`` (``python -m llmctl.ops.build``).  See ``functional.py`` for
+the op surface and ``ref.py`` for the fp32 oracles.
+"""
+
+from . import ref
+from ._lib import available as native_available
+from .functional import (
+    adamw_step_,
+    add_layernorm,
+    add_rmsnorm,
+    cross_entropy,
+    flash_attention,
+    gelu,
+    kv_cache_write,
+    l2norm_sq,
+    layernorm,
+    paged_attention_decode,
+    rmsnorm,
+    rope_qkv,
+    sample,
+    swiglu,
+)
+
+__all__ = [
+    "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy",
+    "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
+    "rmsnorm", "rope_qkv", "sample", "swiglu",
+]

@@ -1,0 +1,325 @@
+"""Autograd-facing fused ops.  GPU tensors run the hand-written CDNA4 HIP kernels in
+``csrc/`` (``torch.ops.llmctl.*``); CPU tensors run the fp32 oracle in :mod:`.ref`.
+
+Every op keeps the layouts the GEMMs (hipBLASLt) produce/consume so no transposes or
+copies are needed between kernels:
+
+* activations are token-major ``[T, features]`` (T = batch*seq);
+* attention takes ``q [B,S,Hq,D]``, ``k/v [B,S,Hkv,D]`` (GQA), returns ``o [B,S,Hq,D]``
+  which *is* the ``[T, Hq*D]`` input of the output projection;
+* RoPE is fused with the QKV split: ``[T,(Hq+2Hkv)D] -> q,k (rotated), v``.
+"""
+
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import ref
+from ._lib import native, use_native
+
+
+# =============================================================================== norms
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        x2 = x.reshape(-1, x.shape[-1])
+        if use_native(x):
+            y, rstd = native().rmsnorm_fwd(x2, w, eps)
+        else:
+            y, rstd = ref.rmsnorm_fwd(x2, w, eps)
+        ctx.save_for_backward(x2, w, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, rstd = ctx.saved_tensors
+        dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
+        if use_native(dy):
+            dx, dw = native().rmsnorm_bwd(dy2, x2, w, rstd, None)
+        else:
+            dx, dw = ref.rmsnorm_bwd(dy2, x2, w, rstd)
+        return dx.view(ctx.shape), dw, None
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """res_out = x + residual ; y = rmsnorm(res_out) * w.  One HBM pass for both."""
+
+    @staticmethod
+    def forward(ctx, x, residual, w, eps):
+        H = x.shape[-1]
+        x2, r2 = x.reshape(-1, H), residual.reshape(-1, H)
+        if use_native(x):
+            y, res_out, rstd = native().add_rmsnorm_fwd(x2, r2, w, eps)
+        else:
+            res_out = (x2.float() + r2.float()).to(x.dtype)
+            y, rstd = ref.rmsnorm_fwd(res_out, w, eps)
+        ctx.save_for_backward(res_out, w, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape), res_out.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        res_out, w, rstd = ctx.saved_tensors
+        H = res_out.shape[-1]
+        dy2 = dy.reshape(-1, H).contiguous()
+        dres2 = dres.reshape(-1, H).contiguous() if dres is not None else None
+        if use_native(dy):
+            dx, dw = native().rmsnorm_bwd(dy2, res_out, w, rstd, dres2)
+        else:
+            dx, dw = ref.rmsnorm_bwd(dy2, res_out, w, rstd, dres2)
+        dx = dx.view(ctx.shape)
+        return dx, dx, dw, None
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        x2 = x.reshape(-1, x.shape[-1])
+        if use_native(x):
+            y, mu, rstd = native().layernorm_fwd(x2, w, b, eps)
+        else:
+            y, mu, rstd = ref.layernorm_fwd(x2, w, b, eps)
+        ctx.save_for_backward(x2, w, mu, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mu, rstd = ctx.saved_tensors
+        dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
+        if use_native(dy):
+            dx, dw, db = native().layernorm_bwd(dy2, x2, w, mu, rstd, None)
+        else:
+            dx, dw, db = ref.layernorm_bwd(dy2, x2, w, mu, rstd)
+        return dx.view(ctx.shape), dw, db, None
+
+
+class _AddLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, w, b, eps):
+        H = x.shape[-1]
+        x2, r2 = x.reshape(-1, H), residual.reshape(-1, H)
+        if use_native(x):
+            y, res_out, mu, rstd = native().add_layernorm_fwd(x2, r2, w, b, eps)
+        else:
+            res_out = (x2.float() + r2.float()).to(x.dtype)
+            y, mu, rstd = ref.layernorm_fwd(res_out, w, b, eps)
+        ctx.save_for_backward(res_out, w, mu, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape), res_out.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        res_out, w, mu, rstd = ctx.saved_tensors
+        H = res_out.shape[-1]
+        dy2 = dy.reshape(-1, H).contiguous()
+        dres2 = dres.reshape(-1, H).contiguous() if dres is not None else None
+        if use_native(dy):
+            dx, dw, db = native().layernorm_bwd(dy2, res_out, w, mu, rstd, dres2)
+        else:
+            dx, dw, db = ref.layernorm_bwd(dy2, res_out, w, mu, rstd, dres2)
+        dx = dx.view(ctx.shape)
+        return dx, dx, dw, db, None
+
+
+def rmsnorm(x, w, eps: float = 1e-5):
+    return _RMSNorm.apply(x, w, eps)
+
+
+def add_rmsnorm(x, residual, w, eps: float = 1e-5):
+    return _AddRMSNorm.apply(x, residual, w, eps)
+
+
+def layernorm(x, w, b, eps: float = 1e-5):
+    return _LayerNorm.apply(x, w, b, eps)
+
+
+def add_layernorm(x, residual, w, b, eps: float = 1e-5):
+    return _AddLayerNorm.apply(x, residual, w, b, eps)
+
+
+# =============================================================================== rope
+class _RopeQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, nq, nkv, seq_len, positions):
+        if use_native(qkv):
+            q, k, v = native().rope_qkv_fwd(qkv, cos, sin, nq, nkv, seq_len, positions)
+        else:
+            q, k, v = ref.rope_qkv_fwd(qkv, cos, sin, nq, nkv, seq_len, positions)
+        ctx.save_for_backward(cos, sin, positions if positions is not None else torch.empty(0))
+        ctx.has_pos = positions is not None
+        ctx.seq_len = seq_len
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin, pos = ctx.saved_tensors
+        pos = pos if ctx.has_pos else None
+        dq, dk, dv = dq.contiguous(), dk.contiguous(), dv.contiguous()
+        if use_native(dq):
+            dqkv = native().rope_qkv_bwd(dq, dk, dv, cos, sin, ctx.seq_len, pos)
+        else:
+            dqkv = ref.rope_qkv_bwd(dq, dk, dv, cos, sin, ctx.seq_len, pos)
+        return dqkv, None, None, None, None, None, None
+
+
+def rope_qkv(qkv, cos, sin, nq: int, nkv: int, seq_len: int, positions: Optional[torch.Tensor] = None):
+    """``qkv [T,(nq+2nkv)*D]`` -> ``q [T,nq,D], k [T,nkv,D], v [T,nkv,D]`` with RoPE on q,k."""
+    return _RopeQKV.apply(qkv, cos, sin, nq, nkv, seq_len, positions)
+
+
+# =============================================================================== attention
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale, causal):
+        if use_native(q):
+            o, lse = native().flash_attn_fwd(q, k, v, scale, causal)
+        else:
+            o, lse = ref.attention_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.scale, ctx.causal = scale, causal
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        if use_native(do):
+            dq, dk, dv = native().flash_attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
+        else:
+            dq, dk, dv = ref.attention_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
+        return dq, dk, dv, None, None
+
+
+def flash_attention(q, k, v, causal: bool = True, softmax_scale: Optional[float] = None):
+    """Causal flash attention.  q ``[B,S,Hq,D]``, k/v ``[B,S,Hkv,D]`` (Hq % Hkv == 0)."""
+    scale = softmax_scale if softmax_scale is not None else q.shape[-1] ** -0.5
+    return _FlashAttn.apply(q, k, v, scale, causal)
+
+
+# =============================================================================== MLP
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        ctx.save_for_backward(gu)
+        return native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dact):
+        (gu,) = ctx.saved_tensors
+        dact = dact.contiguous()
+        return native().swiglu_bwd(dact, gu) if use_native(dact) else ref.swiglu_bwd(dact, gu)
+
+
+class _GELU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return native().gelu_fwd(x) if use_native(x) else ref.gelu_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        return native().gelu_bwd(dy, x) if use_native(dy) else ref.gelu_bwd(dy, x)
+
+
+def swiglu(gu):
+    """``gu [..., 2F]`` laid out ``[gate | up]`` -> ``silu(gate) * up``."""
+    return _SwiGLU.apply(gu)
+
+
+def gelu(x):
+    return _GELU.apply(x)
+
+
+# =============================================================================== loss
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index, denom):
+        if use_native(logits):
+            loss, lse = native().cross_entropy_fwd(logits, labels, ignore_index)
+        else:
+            loss, lse = ref.cross_entropy_fwd(logits, labels, ignore_index)
+        ctx.save_for_backward(logits, lse, labels)
+        ctx.ignore_index, ctx.denom = ignore_index, denom
+        return loss.sum() / denom
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, lse, labels = ctx.saved_tensors
+        dloss = (g / ctx.denom).float().expand(labels.shape).contiguous()
+        if use_native(logits):
+            # logits are dead after this: write dlogits in place (saves a [T,V] buffer)
+            dl = native().cross_entropy_bwd(dloss, logits, lse, labels, ctx.ignore_index, True)
+        else:
+            dl = ref.cross_entropy_bwd(dloss, logits, lse, labels, ctx.ignore_index)
+        return dl, None, None, None
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100, reduction_denom: Optional[float] = None):
+    """Mean token cross-entropy over non-ignored labels; logits ``[T,V]`` bf16/fp32."""
+    if reduction_denom is None:
+        reduction_denom = float(max(int((labels != ignore_index).sum()), 1)) if not labels.is_cuda else None
+    if reduction_denom is None:
+        # avoid a host sync on GPU: callers that know the count pass it; default = all tokens
+        reduction_denom = float(labels.numel())
+    return _CrossEntropy.apply(logits, labels, ignore_index, reduction_denom)
+
+
+# =============================================================================== optimizer
+def adamw_step_(param, master, grad, exp_avg, exp_avg_sq, *, lr: float, beta1: float, beta2: float,
+                eps: float, weight_decay: float, step: int, grad_scale: Optional[torch.Tensor] = None):
+    """One fused AdamW update over flat buffers (bf16 param, fp32 master/m/v, bf16|fp32 grad).
+    ``grad_scale`` is a 1-element fp32 device tensor (e.g. the clip coefficient) so clipping
+    needs no host sync."""
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    if use_native(param):
+        native().adamw_step_(param, master, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                             bc1, bc2, grad_scale)
+    else:
+        gs = float(grad_scale) if grad_scale is not None else 1.0
+        ref.adamw_step_(param, master, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, gs)
+
+
+def l2norm_sq(t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum of squares of ``t`` accumulated (fp32) into ``out`` (allocated if None)."""
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=t.device)
+    if use_native(t):
+        native().l2norm_sq_(t, out)
+    else:
+        out += ref.l2norm_sq(t)
+    return out
+
+
+# =============================================================================== serving
+def kv_cache_write(k, v, k_cache, v_cache, slot_mapping):
+    if use_native(k):
+        native().kv_cache_write(k, v, k_cache, v_cache, slot_mapping)
+    else:
+        ref.kv_cache_write(k, v, k_cache, v_cache, slot_mapping)
+
+
+def paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale: Optional[float] = None):
+    scale = scale if scale is not None else q.shape[-1] ** -0.5
+    if use_native(q):
+        return native().paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale)
+    return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale)
+
+
+def sample(logits, temperature, top_k, top_p, uniform):
+    if use_native(logits):
+        return native().sample(logits, temperature, top_k, top_p, uniform)
+    return ref.sample(logits, temperature, top_k, top_p, uniform)
+
+
+__all__ = [
+    "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "swiglu",
+    "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
+    "sample",
+]
