@@ -25,7 +25,7 @@ import time
 
 # Measured reference-equivalent stack on one MI355X (HF LlamaForCausalLM eager + torch
 # AdamW, same GPT-7B config/seq/bf16) — see BASELINE.md §3.  None until measured.
-REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU = None
+REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU = 14732.2  # gpurun_out 2026-10-15: HF+SDPA, mb=4
 
 
 def parse():

@@ -182,7 +182,7 @@ MODEL_TEMPLATES: Dict[str, Dict[str, Dict[str, Any]]] = {
     },
     "tiny": {
         "test": {
-            "name": "tiny-test", "arch": "decoder-only", "layers": 2, "hidden": 128, "ffn": 352,
+            "name": "tiny-test", "arch": "decoder-only", "layers": 2, "hidden": 256, "ffn": 704,
             "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
             "rope": {"base": 10000, "scaling": "linear"},
         },

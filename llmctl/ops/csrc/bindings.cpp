@@ -1,0 +1,36 @@
+// Operator schemas for torch.ops.llmctl.*  (implementations: TORCH_LIBRARY_IMPL(llmctl, CUDA)
+// blocks in the individual .hip files; CUDA dispatch key == HIP on ROCm builds of PyTorch).
+#include <torch/library.h>
+
+TORCH_LIBRARY(llmctl, m) {
+  // norms (norm.hip)
+  m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
+  m.def("add_rmsnorm_fwd(Tensor x, Tensor residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres) -> (Tensor, Tensor)");
+  m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("add_layernorm_fwd(Tensor x, Tensor residual, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mu, Tensor rstd, Tensor? dres) -> (Tensor, Tensor, Tensor)");
+  // elementwise (elementwise.hip)
+  m.def("rope_qkv_fwd(Tensor qkv, Tensor cos, Tensor sin, int nq, int nkv, int seq_len, Tensor? positions) -> (Tensor, Tensor, Tensor)");
+  m.def("rope_qkv_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cos, Tensor sin, int seq_len, Tensor? positions) -> Tensor");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor dact, Tensor gu) -> Tensor");
+  m.def("gelu_fwd(Tensor x) -> Tensor");
+  m.def("gelu_bwd(Tensor dy, Tensor x) -> Tensor");
+  // loss (loss.hip)
+  m.def("cross_entropy_fwd(Tensor logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");
+  m.def("cross_entropy_bwd(Tensor dloss, Tensor logits, Tensor lse, Tensor labels, int ignore_index, bool inplace) -> Tensor");
+  // optimizer (optim.hip)
+  m.def("adamw_step_(Tensor(a!) param, Tensor(b!) master, Tensor grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, Tensor? grad_scale) -> ()");
+  m.def("l2norm_sq_(Tensor x, Tensor(a!) out) -> ()");
+  // attention (flash_attn_fwd.hip / flash_attn_bwd.hip)
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal) -> (Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal) -> (Tensor, Tensor, Tensor)");
+  // serving (paged_attn.hip, sampling.hip)
+  m.def("kv_cache_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot_mapping) -> ()");
+  m.def("paged_attention_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, float scale) -> Tensor");
+  m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor uniform) -> Tensor");
+  // benchmarks / tuning (gemm_bf16.hip, hbm_stream.hip)
+  m.def("gemm_bf16(Tensor a, Tensor b) -> Tensor");
+  m.def("hbm_copy(Tensor src, Tensor(a!) dst) -> ()");
+}

@@ -1,0 +1,106 @@
+// Shared helpers for llmctl's CDNA4 (gfx950) HIP kernels.
+//
+// Conventions
+//   * wave64: every warp-level idiom here is written for 64 lanes (shfl_xor offsets up to 32).
+//   * bf16 tensors are moved as 16-byte vectors (8 x bf16 per lane) — hipcc does not
+//     auto-vectorise bf16 (CDNA guide, Guideline 13).
+//   * f32 -> bf16 uses the compiler's RNE cast (lowers to v_cvt_pk_bf16_f32, NaN-safe).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include <cstdint>
+
+#define LLMCTL_CHECK(cond, ...) TORCH_CHECK(cond, "llmctl: ", __VA_ARGS__)
+#define LLMCTL_CHECK_CUDA(t) LLMCTL_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define LLMCTL_CHECK_CONTIG(t) LLMCTL_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define LLMCTL_CHECK_BF16(t) LLMCTL_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define LLMCTL_HIP_CHECK(expr)                                                      \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    TORCH_CHECK(_e == hipSuccess, "llmctl HIP error: ", hipGetErrorString(_e));     \
+  } while (0)
+
+namespace llmctl {
+
+using bf16x8 = __attribute__((ext_vector_type(8))) unsigned short;  // 16 B
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(((unsigned)u) << 16); }
+
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return __bfloat16_as_ushort(b);
+}
+
+__device__ __forceinline__ void load8(const unsigned short* p, float* out) {
+  bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = bf2f(v[j]);
+}
+
+__device__ __forceinline__ void store8(unsigned short* p, const float* in) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(in[j]);
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// block-wide sum for blockDim.x = NW*64 (result valid in every thread)
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* smem) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) smem[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r += smem[i];
+  __syncthreads();
+  return r;
+}
+
+// torch on ROCm "masquerades" HIP as the CUDA device type: use the masquerading stream so
+// kernels honour torch.cuda.stream(...) contexts and hipGraph capture.
+inline hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+inline int num_cus() {
+  static int n = -1;
+  if (n < 0) {
+    hipDeviceProp_t p;
+    int dev = 0;
+    LLMCTL_HIP_CHECK(hipGetDevice(&dev));
+    LLMCTL_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    n = p.multiProcessorCount;
+  }
+  return n;
+}
+
+template <typename T>
+inline const unsigned short* bf_ptr(const T& t) {
+  return reinterpret_cast<const unsigned short*>(t.data_ptr());
+}
+template <typename T>
+inline unsigned short* bf_mut(T& t) {
+  return reinterpret_cast<unsigned short*>(t.data_ptr());
+}
+
+}  // namespace llmctl

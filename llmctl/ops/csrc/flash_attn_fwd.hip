@@ -1,0 +1,253 @@
+// Flash-attention forward (causal / full, GQA) for gfx950 — MFMA 32x32x16 bf16.
+//
+// Structure (CDNA guide App. B "Fused attention prefill"):
+//   * workgroup = 4 waves = 128 query rows of one (batch, q-head); each wave owns 32 rows;
+//   * Q fragments live in registers for the whole kernel (HD/16 x bf16x8 per lane);
+//   * K/V tiles of 64 keys are staged global -> registers -> LDS (async-STAGE split, T14:
+//     the next tile's global loads are issued before this tile's MFMAs and written to LDS
+//     after the next barrier);
+//   * "swapped" QK^T: S^T = K Q^T puts the key index in registers and the query on the
+//     lane, so the online-softmax row max/sum are in-lane + one xor-32 shuffle, and P^T
+//     is directly the B operand of O^T += V^T P^T (no P round-trip through LDS);
+//   * K is read with ds_read_b128 from an XOR-swizzled row image (T2), V with
+//     ds_read_b64_tr_b16 from a swizzled tr image (T10) — both bank-conflict free;
+//   * exp2-domain softmax with the 1/sqrt(d)*log2(e) scale folded into one multiply;
+//   * causal: tiles wholly above a wave's diagonal are skipped, the mask is applied only
+//     on diagonal tiles; the heaviest q-blocks are dispatched first;
+//   * blocks that share a K/V head are B*Hq apart in dispatch order, i.e. on one XCD (L2
+//     reuse of the K/V stream) when B*Hq % 8 == 0.
+// Outputs O [B,S,Hq,HD] bf16 and LSE [B,Hq,S] fp32 (natural log) for the backward pass.
+#include "attn_common.h"
+
+namespace llmctl {
+using namespace attn;
+namespace {
+
+constexpr int QB = 128;  // query rows per workgroup
+constexpr int KB = 64;   // keys per tile
+
+struct FwdArgs {
+  const unsigned short* q;
+  const unsigned short* k;
+  const unsigned short* v;
+  unsigned short* o;
+  float* lse;
+  int B, S, Hq, Hkv;
+  long q_sb, q_ss, q_sh;  // element strides (batch, seq, head); d is contiguous
+  long k_sb, k_ss, k_sh;
+  long v_sb, v_ss, v_sh;
+  long o_sb, o_ss, o_sh;
+  float scale_log2;  // softmax_scale * log2(e)
+};
+
+template <int HD, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
+  constexpr int NKS = HD / 16;  // k-steps of QK^T
+  constexpr int NDB = HD / 32;  // 32-wide d blocks of O
+  constexpr int ROWB = HD * 2;  // bytes per LDS row
+  constexpr int CPR = HD / 8;   // 16-B chunks per row
+  constexpr int LD_ITERS = KB * CPR / 256;  // 16-B chunks per thread per tile (4 for HD=128)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * KB * ROWB];
+  unsigned char* Ks = smem;
+  unsigned char* Vs = smem + KB * ROWB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = (a.S + QB - 1) / QB;
+  const int BH = a.B * a.Hq;
+  const int bh = blockIdx.x % BH;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (largest causal span) first
+  const int b = bh / a.Hq, hq = bh % a.Hq;
+  const int hk = hq / (a.Hq / a.Hkv);
+  const int q_row0 = qblk * QB + wave * 32;
+  const int my_q = q_row0 + r;
+
+  const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh;
+  const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh;
+  const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh;
+
+  // ---- Q fragments (B operand of S^T = K Q^T): Q[my_q][16ks + 8hh + j]
+  bf16x8_t qf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (my_q < a.S) u = gload16(Qp + (long)my_q * a.q_ss + ks * 16 + 8 * hh);
+    qf[ks] = __builtin_bit_cast(bf16x8_t, u);
+  }
+
+  f32x16 o[NDB];
+#pragma unroll
+  for (int d = 0; d < NDB; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;
+
+  const int kv_end = CAUSAL ? min(a.S, qblk * QB + QB) : a.S;
+  const int ntiles = (kv_end + KB - 1) / KB;
+
+  // ---- staging registers for one K and one V tile
+  uint4 kst[LD_ITERS], vst[LD_ITERS];
+  auto issue = [&](int t) {
+#pragma unroll
+    for (int it = 0; it < LD_ITERS; ++it) {
+      const int c = tid + 256 * it;
+      const int row = c / CPR, ch = c % CPR;
+      const int key = t * KB + row;
+      if (key < a.S) {
+        kst[it] = gload16(Kp + (long)key * a.k_ss + ch * 8);
+        vst[it] = gload16(Vp + (long)key * a.v_ss + ch * 8);
+      } else {
+        kst[it] = make_uint4(0, 0, 0, 0);
+        vst[it] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int it = 0; it < LD_ITERS; ++it) {
+      const int c = tid + 256 * it;
+      const int row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<uint4*>(Ks + row_off<HD>(row, ch)) = kst[it];
+      *reinterpret_cast<uint4*>(Vs + tr_off<HD>(row, ch)) = vst[it];
+    }
+  };
+
+  issue(0);
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();  // all waves finished reading the previous tile
+    commit();
+    __syncthreads();
+    if (t + 1 < ntiles) issue(t + 1);  // overlaps the MFMAs below
+    const int kv0 = t * KB;
+    if (CAUSAL && kv0 > q_row0 + 31) continue;  // tile entirely above this wave's diagonal
+
+    // ---- S^T = K Q^T  (two 32-key blocks)
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8_t kf = lds_read_b128(Ks, row_off<HD>(kb * 32 + r, 2 * ks + hh));
+        s[kb] = mfma32(kf, qf[ks], s[kb]);
+      }
+    }
+    // ---- scale, mask, online softmax (exp2 domain)
+    const bool need_mask = (CAUSAL && kv0 + KB - 1 > q_row0) || (kv0 + KB > a.S);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float x = s[kb][i] * a.scale_log2;
+        if (need_mask) {
+          const int key = kv0 + kb * 32 + acc_row(i, hh);
+          if ((CAUSAL && key > my_q) || key >= a.S) x = -INFINITY;
+        }
+        s[kb][i] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_i, mx);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = fast_exp2(m_i - m_use);
+    float rs = 0.f;
+    bf16x8_t pb[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float p[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        p[i] = fast_exp2(s[kb][i] - m_use);
+        rs += p[i];
+      }
+      pb[kb][0] = to_bf16x8(p);
+      pb[kb][1] = to_bf16x8(p + 8);
+    }
+    rs += __shfl_xor(rs, 32);
+    l_i = l_i * alpha + rs;
+    m_i = m_new;
+#pragma unroll
+    for (int d = 0; d < NDB; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) {
+          const bf16x8_t vf = tr_frag<HD>(Vs, kb * 32 + 16 * st, d * 32, lane);
+          o[d] = mfma32(vf, pb[kb][st], o[d]);
+        }
+  }
+
+  // ---- epilogue: O = O^T^T / l ; LSE
+  if (my_q < a.S) {
+    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+    unsigned short* Op = a.o + b * a.o_sb + (long)my_q * a.o_ss + hq * a.o_sh;
+#pragma unroll
+    for (int d = 0; d < NDB; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = d * 32 + 8 * g + 4 * hh;
+        unsigned short w4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w4[j] = f2bf(o[d][4 * g + j] * inv);
+        *reinterpret_cast<uint2*>(Op + col) =
+            make_uint2((unsigned)w4[0] | ((unsigned)w4[1] << 16), (unsigned)w4[2] | ((unsigned)w4[3] << 16));
+      }
+    if (hh == 0) {
+      const float lse = (l_i > 0.f) ? (m_i + __log2f(l_i)) * 0.69314718055994531f : -INFINITY;
+      a.lse[((long)b * a.Hq + hq) * a.S + my_q] = lse;
+    }
+  }
+}
+
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                  double scale, bool causal) {
+  LLMCTL_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "flash_attn_fwd: GPU tensors");
+  LLMCTL_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 &&
+                   v.scalar_type() == at::kBFloat16,
+               "flash_attn_fwd: bf16");
+  LLMCTL_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "q/k/v must be [B,S,H,D]");
+  const int B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int Hkv = k.size(2);
+  LLMCTL_CHECK(k.size(0) == B && k.size(1) == S && v.sizes() == k.sizes() && k.size(3) == D,
+               "k/v shape must be [B,S,Hkv,D] matching q");
+  LLMCTL_CHECK(Hq % Hkv == 0, "Hq must be a multiple of Hkv");
+  LLMCTL_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128, got ", D);
+  LLMCTL_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1, "head_dim must be contiguous");
+  for (const at::Tensor* t : {&q, &k, &v})
+    LLMCTL_CHECK(t->stride(0) % 8 == 0 && t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0 &&
+                     (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                 "q/k/v strides must be multiples of 8 elements and 16-B aligned");
+  const c10::DeviceGuard g(q.device());
+  auto o = at::empty({B, S, Hq, D}, q.options());
+  auto lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  if (B * S * Hq == 0) return {o, lse};
+  FwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_mut(o), lse.data_ptr<float>(), B, S, Hq, Hkv,
+            q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+            v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
+            (float)(scale * 1.4426950408889634)};
+  const int nqb = (S + QB - 1) / QB;
+  dim3 grid((unsigned)(B * Hq * nqb)), block(256);
+  auto s = stream();
+  if (D == 128) {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<128, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<128, false>), grid, block, 0, s, a);
+  } else {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<64, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<64, false>), grid, block, 0, s, a);
+  }
+  return {o, lse};
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("flash_attn_fwd", &flash_attn_fwd); }
+
+}  // namespace llmctl

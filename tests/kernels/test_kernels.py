@@ -1,0 +1,200 @@
+"""HIP kernel numerics vs the fp32 PyTorch oracles in llmctl/ops/ref.py (GPU only)."""
+
+import math
+
+import pytest
+import torch
+
+from llmctl.ops import ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-12)
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=DEV) * scale).to(torch.bfloat16)
+
+
+# ----------------------------------------------------------------------------- norms
+@pytest.mark.parametrize("T,H", [(7, 128), (300, 4096), (64, 768), (33, 8192), (5, 5120)])
+def test_rmsnorm(native_lib, T, H):
+    x, w = _bf(T, H, seed=1), _bf(H, seed=2, scale=0.5)
+    y, rstd = native_lib.rmsnorm_fwd(x, w, 1e-5)
+    yr, rr = ref.rmsnorm_fwd(x, w, 1e-5)
+    assert _rel(y, yr) < 1e-2 and _rel(rstd, rr) < 1e-5
+    dy = _bf(T, H, seed=3)
+    dres = _bf(T, H, seed=4)
+    dx, dw = native_lib.rmsnorm_bwd(dy, x, w, rstd, dres)
+    dxr, dwr = ref.rmsnorm_bwd(dy, x, w, rr, dres)
+    assert _rel(dx, dxr) < 1e-2 and _rel(dw, dwr) < 1e-2
+
+
+@pytest.mark.parametrize("T,H", [(300, 4096), (17, 768)])
+def test_add_rmsnorm(native_lib, T, H):
+    x, res, w = _bf(T, H, seed=1), _bf(T, H, seed=5), _bf(H, seed=2)
+    y, ro, rstd = native_lib.add_rmsnorm_fwd(x, res, w, 1e-5)
+    ro_r = (x.float() + res.float()).to(torch.bfloat16)
+    yr, rr = ref.rmsnorm_fwd(ro_r, w, 1e-5)
+    assert torch.equal(ro, ro_r)
+    assert _rel(y, yr) < 1e-2
+
+
+@pytest.mark.parametrize("T,H", [(100, 768), (9, 4096)])
+def test_layernorm(native_lib, T, H):
+    x, w, b = _bf(T, H, seed=1, scale=2.0), _bf(H, seed=2), _bf(H, seed=3)
+    y, mu, rstd = native_lib.layernorm_fwd(x, w, b, 1e-5)
+    yr, mr, rr = ref.layernorm_fwd(x, w, b, 1e-5)
+    assert _rel(y, yr) < 1e-2 and _rel(mu, mr) < 1e-4 and _rel(rstd, rr) < 1e-4
+    dy = _bf(T, H, seed=4)
+    dx, dw, db = native_lib.layernorm_bwd(dy, x, w, mu, rstd, None)
+    dxr, dwr, dbr = ref.layernorm_bwd(dy, x, w, mr, rr)
+    assert _rel(dx, dxr) < 1e-2 and _rel(dw, dwr) < 1e-2 and _rel(db, dbr) < 1e-2
+
+
+# ----------------------------------------------------------------------------- rope / mlp
+@pytest.mark.parametrize("nq,nkv,D,S", [(32, 32, 128, 64), (8, 2, 64, 48), (4, 1, 128, 16)])
+@pytest.mark.parametrize("with_pos", [False, True])
+def test_rope_qkv(native_lib, nq, nkv, D, S, with_pos):
+    B = 3
+    T = B * S
+    qkv = _bf(T, (nq + 2 * nkv) * D, seed=7)
+    cos, sin = ref.rope_tables(S + 5, D, base=10000.0, device=DEV)
+    pos = torch.randint(0, S + 5, (T,), device=DEV, dtype=torch.int32) if with_pos else None
+    q, k, v = native_lib.rope_qkv_fwd(qkv, cos, sin, nq, nkv, S, pos)
+    qr, kr, vr = ref.rope_qkv_fwd(qkv, cos, sin, nq, nkv, S, pos)
+    assert _rel(q, qr) < 1e-2 and _rel(k, kr) < 1e-2 and torch.equal(v, vr)
+    dq, dk, dv = _bf(T, nq, D, seed=8), _bf(T, nkv, D, seed=9), _bf(T, nkv, D, seed=10)
+    d = native_lib.rope_qkv_bwd(dq, dk, dv, cos, sin, S, pos)
+    dr = ref.rope_qkv_bwd(dq, dk, dv, cos, sin, S, pos)
+    assert _rel(d, dr) < 1e-2
+
+
+@pytest.mark.parametrize("T,F", [(33, 11008), (128, 1376), (8, 64)])
+def test_swiglu(native_lib, T, F):
+    gu = _bf(T, 2 * F, seed=11, scale=2.0)
+    a = native_lib.swiglu_fwd(gu)
+    assert _rel(a, ref.swiglu_fwd(gu)) < 1e-2
+    d = _bf(T, F, seed=12)
+    assert _rel(native_lib.swiglu_bwd(d, gu), ref.swiglu_bwd(d, gu)) < 1e-2
+
+
+def test_gelu(native_lib):
+    x = _bf(64, 3072, seed=13, scale=2.0)
+    assert _rel(native_lib.gelu_fwd(x), ref.gelu_fwd(x)) < 1e-2
+    d = _bf(64, 3072, seed=14)
+    assert _rel(native_lib.gelu_bwd(d, x), ref.gelu_bwd(d, x)) < 1e-2
+
+
+# ----------------------------------------------------------------------------- loss
+@pytest.mark.parametrize("T,V", [(37, 32000), (8, 50304), (4, 1003)])
+def test_cross_entropy(native_lib, T, V):
+    logits = _bf(T, V, seed=15, scale=3.0)
+    labels = torch.randint(0, V, (T,), device=DEV)
+    labels[1] = -100
+    loss, lse = native_lib.cross_entropy_fwd(logits, labels, -100)
+    lr, lser = ref.cross_entropy_fwd(logits, labels, -100)
+    assert torch.allclose(loss, lr, atol=2e-3, rtol=1e-3) and torch.allclose(lse, lser, atol=2e-3, rtol=1e-4)
+    dloss = torch.rand(T, device=DEV)
+    g = native_lib.cross_entropy_bwd(dloss, logits, lse, labels, -100, False)
+    gr = ref.cross_entropy_bwd(dloss, logits, lser, labels, -100)
+    assert _rel(g, gr) < 1e-2
+    g2 = native_lib.cross_entropy_bwd(dloss, logits.clone(), lse, labels, -100, True)
+    assert torch.equal(g, g2)
+
+
+# ----------------------------------------------------------------------------- optimizer
+@pytest.mark.parametrize("n", [1000, 4096 * 64 + 3])
+@pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
+def test_adamw(native_lib, n, gdt):
+    torch.manual_seed(0)
+    master = torch.randn(n, device=DEV)
+    p = master.to(torch.bfloat16)
+    g = torch.randn(n, device=DEV).to(gdt)
+    m, v = torch.randn(n, device=DEV) * 0.1, torch.rand(n, device=DEV) * 0.1
+    M2, m2, v2, p2 = master.clone(), m.clone(), v.clone(), p.clone()
+    gs = torch.tensor([0.5], device=DEV)
+    step = 3
+    b1, b2 = 0.9, 0.95
+    native_lib.adamw_step_(p, master, g, m, v, 1e-3, b1, b2, 1e-8, 0.1, 1 - b1 ** step, 1 - b2 ** step, gs)
+    ref.adamw_step_(p2, M2, g, m2, v2, 1e-3, b1, b2, 1e-8, 0.1, step, 0.5)
+    assert torch.allclose(master, M2, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(m, m2, atol=1e-6) and torch.allclose(v, v2, atol=1e-6)
+    assert torch.equal(p, master.to(torch.bfloat16))
+
+
+def test_l2norm(native_lib):
+    x = _bf(1 << 20, seed=3)
+    out = torch.zeros(1, device=DEV)
+    native_lib.l2norm_sq_(x, out)
+    assert abs(out.item() - x.float().pow(2).sum().item()) / out.item() < 1e-4
+
+
+# ----------------------------------------------------------------------------- attention
+ATTN_CASES = [
+    (2, 128, 4, 4, 128, True),
+    (1, 200, 4, 2, 128, True),
+    (2, 256, 2, 1, 64, True),
+    (1, 192, 4, 4, 128, False),
+    (1, 100, 2, 2, 64, False),
+    (1, 1024, 2, 1, 128, True),
+]
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal", ATTN_CASES)
+def test_flash_attn(native_lib, B, S, Hq, Hkv, D, causal):
+    q, k, v = _bf(B, S, Hq, D, seed=21), _bf(B, S, Hkv, D, seed=22), _bf(B, S, Hkv, D, seed=23)
+    scale = D ** -0.5
+    o, lse = native_lib.flash_attn_fwd(q, k, v, scale, causal)
+    orf, lser = ref.attention_fwd(q, k, v, scale, causal)
+    assert _rel(o, orf) < 2e-2, _rel(o, orf)
+    assert torch.allclose(lse, lser, atol=2e-2, rtol=1e-3)
+    do = _bf(B, S, Hq, D, seed=24)
+    dq, dk, dv = native_lib.flash_attn_bwd(do, q, k, v, o, lse, scale, causal)
+    dqr, dkr, dvr = ref.attention_bwd(do, q, k, v, o, lse, scale, causal)
+    assert _rel(dv, dvr) < 3e-2, _rel(dv, dvr)
+    assert _rel(dk, dkr) < 3e-2, _rel(dk, dkr)
+    assert _rel(dq, dqr) < 3e-2, _rel(dq, dqr)
+
+
+def test_flash_attn_forced_rescale(native_lib):
+    """Spike one key so the running max jumps mid-sequence (guide rule 26)."""
+    B, S, H, D = 1, 512, 2, 128
+    q, k, v = _bf(B, S, H, D, seed=31), _bf(B, S, H, D, seed=32), _bf(B, S, H, D, seed=33)
+    k[0, 300] = (q[0, 310] * 6).to(torch.bfloat16)
+    o, lse = native_lib.flash_attn_fwd(q, k, v, D ** -0.5, True)
+    orf, _ = ref.attention_fwd(q, k, v, D ** -0.5, True)
+    assert _rel(o, orf) < 2e-2
+
+
+def test_functional_autograd_matches_ref(native_lib):
+    """Whole-model forward/backward through the HIP path vs the fp32 oracle path."""
+    import os
+    from llmctl.models import get_model_config, build_model
+
+    cfg = get_model_config("tiny")
+    torch.manual_seed(0)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, cfg.vocab_size, (2, 128), device=DEV)
+    loss = m(ids, ids)
+    loss.backward()
+    g1 = [p.grad.float().clone() for p in m.parameters()]
+    l1 = loss.item()
+    for p in m.parameters():
+        p.grad = None
+    os.environ["LLMCTL_FORCE_REF"] = "1"
+    try:
+        loss2 = m(ids, ids)
+        loss2.backward()
+    finally:
+        del os.environ["LLMCTL_FORCE_REF"]
+    assert abs(l1 - loss2.item()) < 2e-2
+    for a, p in zip(g1, m.parameters()):
+        assert _rel(a, p.grad) < 5e-2
