@@ -112,7 +112,7 @@ def main():
     par = f"dp{dp}" + (f"-tp{args.tp}" if args.tp > 1 else "") + (f"-pp{args.pp}" if args.pp > 1 else "") + \
         (f"-zero{zero}" if zero else "") + ("-sp" if args.sequence_parallel else "")
     vs = None
-    if REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU:
+    if REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU and mc.name == "gpt-7b" and args.seq_len == 2048 and dev.type == "cuda":
         vs = tps / (REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU * world)
     res = {
         "metric": "tokens/sec (node) GPT-7B train",

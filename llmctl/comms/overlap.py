@@ -52,6 +52,9 @@ class GradSyncEngine:
         for b in flat.buckets:
             for p in b.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        sink = getattr(flat, "sink", None)
+        if sink is not None:  # GEMM-written grads (llmctl.exec.linear) signal readiness here
+            sink.callbacks.append(self._on_grad)
         self._expected = {b.index: len(b.params) for b in flat.buckets}
 
     # ------------------------------------------------------------------ hooks

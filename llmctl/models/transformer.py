@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from llmctl import ops
+from llmctl.exec.linear import linear, weight_grad
 from llmctl.parallel import tensor_parallel as tp
 from .config import ModelConfig
 
@@ -71,7 +72,7 @@ class _SwiGLUDown(torch.autograd.Function):
 
         act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
         dout2 = dout.reshape(-1, dout.shape[-1])
-        dw = dout2.t().matmul(act.reshape(-1, act.shape[-1]))
+        dw = weight_grad(w_down, dout2, act.reshape(-1, act.shape[-1]))
         dact = dout.matmul(w_down)
         dgu = native().swiglu_bwd(dact, gu) if use_native(gu) else ref.swiglu_bwd(dact, gu)
         return dgu, dw
@@ -136,7 +137,7 @@ class DecoderLayer(nn.Module):
         return tp.reduce_scatter_to_sp(x, pc.tp_group) if pc.sequence_parallel else tp.reduce_from_tp(x, pc.tp_group)
 
     def attention(self, xn, B, S, rope, positions=None):
-        qkv = F.linear(self._col_in(xn), self.wqkv, self.bqkv)
+        qkv = linear(self._col_in(xn), self.wqkv, self.bqkv)
         if rope is not None:
             q, k, v = ops.rope_qkv(qkv, rope[0], rope[1], self.nq, self.nkv, S, positions)
         else:
@@ -148,7 +149,7 @@ class DecoderLayer(nn.Module):
         k = k.view(B, S, self.nkv, self.D)
         v = v.view(B, S, self.nkv, self.D)
         o = ops.flash_attention(q, k, v, causal=True)
-        out = F.linear(o.view(B * S, self.nq * self.D), self.wo)
+        out = linear(o.view(B * S, self.nq * self.D), self.wo)
         out = self._row_out(out)
         if self.bo is not None:
             out = out + self.bo
@@ -157,14 +158,14 @@ class DecoderLayer(nn.Module):
     def mlp(self, xn):
         x = self._col_in(xn)
         if self.cfg.gated_mlp:
-            gu = F.linear(x, self.w_up, self.b_up)
+            gu = linear(x, self.w_up, self.b_up)
             if self.pc.activation_checkpoint == "selective":
                 out = _SwiGLUDown.apply(gu, self.w_down)
             else:
-                out = F.linear(ops.swiglu(gu), self.w_down)
+                out = linear(ops.swiglu(gu), self.w_down)
         else:
-            hdn = ops.gelu(F.linear(x, self.w_up, self.b_up))
-            out = F.linear(hdn, self.w_down)
+            hdn = ops.gelu(linear(x, self.w_up, self.b_up))
+            out = linear(hdn, self.w_down)
         out = self._row_out(out)
         if self.b_down is not None:
             out = out + self.b_down
@@ -288,7 +289,7 @@ class DecoderLM(nn.Module):
         pc = self.pc
         if pc.tp_size > 1:
             xn = tp.gather_from_sp(xn, pc.tp_group) if pc.sequence_parallel else tp.copy_to_tp(xn, pc.tp_group)
-        return F.linear(xn, self.head_weight())
+        return linear(xn, self.head_weight())
 
     def loss(self, logits, labels, denom: Optional[float] = None):
         pc = self.pc

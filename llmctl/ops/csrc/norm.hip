@@ -192,14 +192,27 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const unsigned short* __r
   }
 }
 
-// sum partial rows [P, H] -> out[H] (bf16)
+// sum partial rows [P, H] -> out[H] (bf16).  Block = 64 columns x 4 waves; wave w sums rows
+// w, w+4, ... (4 independent loads in flight per lane), then the 4 waves combine via LDS.
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ part, int P, int H,
                                                           unsigned short* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= H) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * H + c];
-  out[c] = f2bf(s);
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < H) {
+    int p = w;
+    for (; p + 12 < P; p += 16) {
+      s0 += part[(size_t)p * H + c];
+      s1 += part[(size_t)(p + 4) * H + c];
+      s2 += part[(size_t)(p + 8) * H + c];
+      s3 += part[(size_t)(p + 12) * H + c];
+    }
+    for (; p < P; p += 4) s0 += part[(size_t)p * H + c];
+  }
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && c < H) out[c] = f2bf(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
 int fwd_grid(int T) {
@@ -239,7 +252,7 @@ void launch_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, 
                 at::Tensor* db) {
   const int T = x.size(0), H = x.size(1);
   const int nv = (H + 511) / 512;
-  const int grid = std::max(1, std::min((T + kWaves - 1) / kWaves, 2 * num_cus()));
+  const int grid = std::max(1, std::min((T + kWaves - 1) / kWaves, num_cus()));
   auto opts = x.options().dtype(at::kFloat);
   at::Tensor dw_part = at::empty({grid, H}, opts);
   at::Tensor db_part = LN ? at::empty({grid, H}, opts) : at::Tensor();
@@ -266,10 +279,10 @@ void launch_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, 
     default: LAUNCH(16); break;
   }
 #undef LAUNCH
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 255) / 256), dim3(256), 0, s, dw_part.data_ptr<float>(), grid, H,
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), dim3(256), 0, s, dw_part.data_ptr<float>(), grid, H,
                      bf_mut(dw));
   if (LN)
-    hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 255) / 256), dim3(256), 0, s, db_part.data_ptr<float>(), grid, H,
+    hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), dim3(256), 0, s, db_part.data_ptr<float>(), grid, H,
                        bf_mut(*db));
 }
 

@@ -162,6 +162,12 @@ class TrainingEngine:
         else:
             self.zero3 = None
             self.flat = FlatParameters(list(self.model.named_parameters()), bucket_numel=bucket_numel, align=align)
+            # GEMM-written weight gradients (no AccumulateGrad pass); tied embeddings excluded
+            from llmctl.exec.linear import GradSink
+
+            tied = mc.tie_word_embeddings
+            leafs = ("wqkv", "wo", "w_up", "w_down") + (() if tied else ("lm_head",))
+            self.flat.install_sinks(GradSink(), lambda n, p: n.split(".")[-1] in leafs)
         norm_group = pg.pp_group if pp > 1 else None
         self.optimizer = FlatAdamW(self.flat, lr=c.learning_rate, betas=tuple(c.betas), eps=c.eps,
                                    weight_decay=c.weight_decay, max_grad_norm=c.gradient_clipping,

@@ -128,15 +128,34 @@ class FlatParameters:
                 p.grad = self.grad[off:off + p.numel()].view_as(p)
 
     # ------------------------------------------------------------------ helpers
+    def install_sinks(self, sink, predicate) -> int:
+        """Attach a :class:`llmctl.exec.linear.GradSink` to every parameter for which
+        ``predicate(name, p)`` holds; their gradients are then written (beta=0 first) by
+        the backward GEMM, so ``zero_grad`` skips them."""
+        n = 0
+        for p in self.params:
+            if predicate(self.names[id(p)], p):
+                sink.attach(p)
+                n += 1
+        self.sink = sink
+        return n
+
     def zero_grad(self) -> None:
         if self.grad is None:
             return
-        self.grad.zero_()
+        sink = getattr(self, "sink", None)
+        if sink is None:
+            self.grad.zero_()
         for p in self.params:
             off = self.offsets[id(p)]
             g = p.grad
             if g is None or g.data_ptr() != self.grad[off:].data_ptr():
-                p.grad = self.grad[off:off + p.numel()].view_as(p)
+                p.grad = g = self.grad[off:off + p.numel()].view_as(p)
+            if sink is not None:
+                if getattr(p, "_llmctl_grad_sink", None) is sink:
+                    sink.reset(p)
+                else:
+                    g.zero_()
 
     def view(self, start: int, end: int, which: str = "grad") -> torch.Tensor:
         buf = self.grad if which == "grad" else self.data
