@@ -47,6 +47,9 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
+        # keep the Parameter object itself: tensors coming back from saved_tensors can be
+        # aliases (e.g. under activation checkpointing) that do not carry the sink
+        ctx.wparam = w
         ctx.has_b = b is not None
         return F.linear(x, w, b)
 
@@ -57,9 +60,9 @@ class _Linear(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         dw = None
         if ctx.needs_input_grad[1]:
-            sink: Optional[GradSink] = getattr(w, "_llmctl_grad_sink", None)
+            sink: Optional[GradSink] = getattr(ctx.wparam, "_llmctl_grad_sink", None)
             if sink is not None:
-                sink.write(w, dy2, x2)  # weight grad first: lets its bucket's comm start earlier
+                sink.write(ctx.wparam, dy2, x2)  # weight grad first: lets its bucket's comm start earlier
             else:
                 dw = dy2.t().matmul(x2)
         dx = dy.matmul(w) if ctx.needs_input_grad[0] else None

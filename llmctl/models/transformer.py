@@ -62,6 +62,7 @@ class _SwiGLUDown(torch.autograd.Function):
         act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
         out = F.linear(act, w_down)
         ctx.save_for_backward(gu, w_down)
+        ctx.wparam = w_down  # the Parameter (carries the grad sink)
         return out
 
     @staticmethod
@@ -72,7 +73,7 @@ class _SwiGLUDown(torch.autograd.Function):
 
         act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
         dout2 = dout.reshape(-1, dout.shape[-1])
-        dw = weight_grad(w_down, dout2, act.reshape(-1, act.shape[-1]))
+        dw = weight_grad(ctx.wparam, dout2, act.reshape(-1, act.shape[-1]))
         dact = dout.matmul(w_down)
         dgu = native().swiglu_bwd(dact, gu) if use_native(gu) else ref.swiglu_bwd(dact, gu)
         return dgu, dw

@@ -310,6 +310,40 @@ class TrainingEngine:
         ckpt.wait()
         return {"final_loss": last_loss, "steps": self.global_step, "history": history}
 
+    # ------------------------------------------------------------------ state (layout-independent)
+    def load_full_state_dict(self, full: Dict[str, torch.Tensor]) -> None:
+        """Load unsharded tensors (names ``layers.<global>.<p>``) into this rank's shards and
+        restart the optimizer masters from them."""
+        from llmctl.io.checkpoint import _global_name, _reinit_master_from_params, shard_tp
+
+        named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
+        with torch.no_grad():
+            for n, p in named:
+                g = _global_name(n, self.pc.layer_start)
+                t = shard_tp(g, full[g], self.pg.layout.tp, self.pg.tp_rank, self.model_config)
+                p.copy_(t.to(p.dtype))
+        if self.zero3 is not None:
+            self.zero3.reload_shards_from_full()
+        _reinit_master_from_params(self)
+
+    def gather_full_state_dict(self) -> Dict[str, torch.Tensor]:
+        """Collective: every rank returns the full unsharded model (CPU tensors)."""
+        from llmctl.io.checkpoint import _global_name, consolidate_tp
+
+        named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
+        local = {_global_name(n, self.pc.layer_start): p.detach().float().cpu() for n, p in named}
+        if not dist.is_initialized():
+            return local
+        parts: List[Dict[str, torch.Tensor]] = [None] * dist.get_world_size()  # type: ignore
+        dist.all_gather_object(parts, (self.pg.tp_rank, self.pg.dp_rank, local))
+        by_name: Dict[str, Dict[int, torch.Tensor]] = {}
+        for tp_rank, dp_rank, sd in parts:
+            if dp_rank != 0:
+                continue
+            for k, v in sd.items():
+                by_name.setdefault(k, {})[tp_rank] = v
+        return {k: consolidate_tp(k, [s[i] for i in sorted(s)], self.model_config) for k, s in by_name.items()}
+
     def _peak_flops(self) -> float:
         if self.device.type == "cuda":
             from llmctl.metrics.flops import device_peak_flops

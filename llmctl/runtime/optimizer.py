@@ -72,7 +72,7 @@ class FlatAdamW:
         self.step_count = 0
         dev = flat.device
         if self.zero_stage == 0:
-            self.master = flat.data.float()
+            self.master = flat.data.float().clone()
             self.exp_avg = torch.zeros_like(self.master)
             self.exp_avg_sq = torch.zeros_like(self.master)
             self.grad_shard = None

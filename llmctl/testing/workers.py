@@ -1,0 +1,93 @@
+"""Rank workers for the parallel-equivalence tests (CPU / gloo, fp32).
+
+Every parallel layout is checked against a single-process run that sees the same global
+batch: the DP ranks' micro-batches become gradient-accumulation micro-steps of the
+reference, TP/SP/PP/ZeRO must not change the math at all.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+
+def make_batch(vocab: int, seq: int, mb: int, step: int, dp_rank: int, micro: int = 0):
+    g = torch.Generator()
+    g.manual_seed(10007 * step + 101 * dp_rank + micro)
+    t = torch.randint(0, vocab, (mb, seq + 1), generator=g)
+    return t[:, :-1].contiguous(), t[:, 1:].contiguous()
+
+
+def reference_state(model: str = "tiny", seed: int = 0) -> Dict[str, torch.Tensor]:
+    from llmctl.models import build_model, get_model_config
+
+    cfg = get_model_config(model)
+    torch.manual_seed(seed)
+    m = build_model(cfg, dtype=torch.float32)
+    return {n: p.detach().clone() for n, p in m.named_parameters()}
+
+
+def _config(**kw):
+    from llmctl.runtime.engine import TrainingConfig
+
+    base = dict(model_name_or_path="tiny", device="cpu", mixed_precision="fp32", learning_rate=1e-3,
+                weight_decay=0.1, warmup_steps=0, scheduler="constant", gradient_clipping=1.0, seq_len=32,
+                batch_size=2, log_level="error", bucket_mb=0.05, seed=0)
+    base.update(kw)
+    return TrainingConfig(**base)
+
+
+def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "tiny",
+                 micro_per_rank: int = 1) -> dict:
+    """Run ``steps`` optimizer steps under ``layout`` (tp/pp/zero/sp/...) and return the
+    gathered full state + losses (rank 0 meaningful)."""
+    from llmctl.runtime.engine import TrainingEngine
+
+    cfg = _config(model_name_or_path=model, tensor_parallel=layout.get("tp", 1),
+                  pipeline_parallel=layout.get("pp", 1), zero_stage=layout.get("zero", 0),
+                  sequence_parallel=layout.get("sp", False),
+                  activation_checkpoint=layout.get("ac", "none"),
+                  num_microbatches=layout.get("microbatches", 0))
+    eng = TrainingEngine(cfg)
+    eng.load_full_state_dict(reference_state(model))
+    vocab = eng.model_config.vocab_size
+    losses = []
+    dp_rank = eng.pg.dp_rank
+    nmb = eng.pipeline.num_microbatches if eng.pipeline is not None else micro_per_rank
+    for s in range(steps):
+        batches = [make_batch(vocab, cfg.seq_len, cfg.batch_size, s, dp_rank, i) for i in range(nmb)]
+        out = eng.train_step(batches)
+        loss = out["loss"]
+        if eng.pipeline is not None:
+            losses.append(eng.pipeline.broadcast_loss(loss))
+        else:
+            # DP mean of the per-rank losses
+            lt = loss.detach().clone().reshape(1)
+            if eng.pg.dp_group is not None:
+                torch.distributed.all_reduce(lt, group=eng.pg.dp_group)
+                lt /= eng.pg.layout.dp
+            losses.append(float(lt))
+    full = eng.gather_full_state_dict()
+    return {"losses": losses, "state": full if rank == 0 else None}
+
+
+def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: int = 1) -> dict:
+    """Single process; the DP ranks' batches are accumulation micro-steps."""
+    import os
+
+    from llmctl.runtime.engine import TrainingEngine
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    cfg = _config(model_name_or_path=model)
+    eng = TrainingEngine(cfg)
+    eng.load_full_state_dict(reference_state(model))
+    vocab = eng.model_config.vocab_size
+    losses = []
+    for s in range(steps):
+        batches = [make_batch(vocab, cfg.seq_len, cfg.batch_size, s, r, i) for r in range(dp)
+                   for i in range(micro_per_rank)]
+        out = eng.train_step(batches)
+        losses.append(float(out["loss"]))  # already the mean over all micro-batches
+    return {"losses": losses, "state": eng.gather_full_state_dict()}
