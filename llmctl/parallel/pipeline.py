@@ -1,0 +1,199 @@
+"""Pipeline parallelism: non-interleaved 1F1B schedule over RCCL point-to-point.
+
+The reference only models PP in its planner (``plan.py:92-93,116-118,140``); nothing runs.
+Here a stage owns a contiguous slice of decoder layers (``partition.shard_map.split_layers``)
+plus the embedding (first stage) and final norm + lm_head + loss (last stage).  Between
+stages the residual stream ``[tokens, hidden]`` travels as one bf16 tensor (the deferred
+residual add is materialised at the stage boundary), ``batch_isend_irecv`` pairs every send
+with the opposite recv so the schedule is deadlock-free, and DP gradient sync is enabled
+only for the last micro-batch's backward (so the overlap engine still hides it under the
+cool-down backwards of earlier stages).
+
+Schedule per stage s of P with M micro-batches (Megatron 1F1B):
+  warm-up   min(P-s-1, M) forwards
+  steady    M - warmup  (forward, backward) pairs
+  cool-down warmup backwards
+Activation memory is bounded by P in-flight micro-batches on stage 0.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+class PipelineSchedule:
+    def __init__(self, engine, num_microbatches: int):
+        self.e = engine
+        pg = engine.pg
+        self.P = pg.layout.pp
+        self.s = pg.pp_rank
+        self.ranks = pg.pp_ranks
+        self.num_microbatches = max(int(num_microbatches), 1)
+        self.prev = self.ranks[self.s - 1] if self.s > 0 else None
+        self.next = self.ranks[self.s + 1] if self.s < self.P - 1 else None
+        if engine.model_config.tie_word_embeddings and self.P > 1:
+            raise NotImplementedError("tied word embeddings across pipeline stages are not supported; untie them")
+        self.last_loss: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def is_first(self):
+        return self.s == 0
+
+    @property
+    def is_last(self):
+        return self.s == self.P - 1
+
+    def _act_shape(self, B: int, S: int) -> Tuple[int, int]:
+        pc = self.e.pc
+        T = B * S
+        if pc.sequence_parallel and pc.tp_size > 1:
+            T //= pc.tp_size
+        return (T, self.e.model_config.hidden)
+
+    def _p2p(self, send: Optional[Tuple[torch.Tensor, int]] = None,
+             recv: Optional[Tuple[torch.Tensor, int]] = None) -> None:
+        ops = []
+        if send is not None:
+            ops.append(dist.P2POp(dist.isend, send[0].contiguous(), send[1]))
+        if recv is not None:
+            ops.append(dist.P2POp(dist.irecv, recv[0], recv[1]))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+
+    def _empty(self, B, S):
+        return torch.empty(self._act_shape(B, S), dtype=self.e.config.dtype, device=self.e.device)
+
+    # ------------------------------------------------------------------ stage compute
+    def _forward(self, x_in: Optional[torch.Tensor], ids: torch.Tensor, labels: torch.Tensor, denom: float):
+        m = self.e.model
+        B, S = ids.shape
+        x = m.embed_tokens(ids) if self.is_first else x_in
+        x, res = m.run_layers(x, B, S)
+        if self.is_last:
+            logits = m.head(x, res)
+            return m.loss(logits, labels, denom)
+        return x + res if res is not None else x
+
+    def _set_sync(self, enabled: bool):
+        e = self.e
+        if e.zero3 is not None:
+            e.zero3.set_sync(enabled)
+        elif e.sync is not None:
+            e.sync.enabled = enabled
+
+    # ------------------------------------------------------------------ 1F1B
+    def run(self, batches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        M = len(batches)
+        P, s = self.P, self.s
+        B, S = batches[0][0].shape
+        denom = float(batches[0][1].numel() * M)
+        warm = min(P - s - 1, M)
+        inputs: List[Optional[torch.Tensor]] = []
+        outputs: List[torch.Tensor] = []
+        losses: List[torch.Tensor] = []
+        fwd_i = 0
+        bwd_i = 0
+
+        def do_forward(x_in):
+            nonlocal fwd_i
+            ids, labels = batches[fwd_i]
+            if x_in is not None:
+                x_in.requires_grad_(True)
+            out = self._forward(x_in, ids, labels, denom)
+            inputs.append(x_in)
+            outputs.append(out)
+            if self.is_last:
+                losses.append(out.detach())
+            fwd_i += 1
+            return out
+
+        def do_backward(grad_out):
+            nonlocal bwd_i
+            self._set_sync(bwd_i == M - 1)
+            out = outputs[bwd_i]
+            if self.is_last:
+                out.backward()
+            else:
+                torch.autograd.backward(out, grad_out)
+            x_in = inputs[bwd_i]
+            g = x_in.grad if x_in is not None else None
+            outputs[bwd_i] = None  # free activations
+            inputs[bwd_i] = None
+            bwd_i += 1
+            return g
+
+        # warm-up forwards
+        for _ in range(warm):
+            x_in = None
+            if not self.is_first:
+                x_in = self._empty(B, S)
+                self._p2p(recv=(x_in, self.prev))
+            out = do_forward(x_in)
+            if not self.is_last:
+                self._p2p(send=(out.detach(), self.next))
+        remaining = M - warm
+        x_in = None
+        if remaining > 0 and not self.is_first:
+            x_in = self._empty(B, S)
+            self._p2p(recv=(x_in, self.prev))
+        for i in range(remaining):
+            out = do_forward(x_in)
+            grad_out = None
+            if not self.is_last:
+                grad_out = self._empty(B, S)
+                self._p2p(send=(out.detach(), self.next), recv=(grad_out, self.next))
+            g = do_backward(grad_out)
+            last_iter = i == remaining - 1
+            if not self.is_first:
+                if not last_iter:
+                    x_in = self._empty(B, S)
+                    self._p2p(send=(g, self.prev), recv=(x_in, self.prev))
+                else:
+                    self._p2p(send=(g, self.prev))
+        # cool-down backwards
+        for _ in range(warm):
+            grad_out = None
+            if not self.is_last:
+                grad_out = self._empty(B, S)
+                self._p2p(recv=(grad_out, self.next))
+            g = do_backward(grad_out)
+            if not self.is_first:
+                self._p2p(send=(g, self.prev))
+        self._set_sync(True)
+        if self.is_last:
+            loss = torch.stack(losses).sum()
+        else:
+            loss = torch.zeros((), device=self.e.device)
+        self.last_loss = loss
+        return loss
+
+    # ------------------------------------------------------------------ loss / eval
+    def broadcast_loss(self, loss: torch.Tensor) -> float:
+        t = loss.detach().float().reshape(1).clone()
+        if not self.is_last:
+            t.zero_()
+        dist.all_reduce(t, group=self.e.pg.pp_group)
+        if self.e.pg.dp_group is not None:
+            dist.all_reduce(t, group=self.e.pg.dp_group)
+            t /= self.e.pg.layout.dp
+        return float(t)
+
+    @torch.no_grad()
+    def eval_loss(self, ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        B, S = ids.shape
+        x_in = None
+        if not self.is_first:
+            x_in = self._empty(B, S)
+            self._p2p(recv=(x_in, self.prev))
+        out = self._forward(x_in, ids, labels, float(labels.numel()))
+        if not self.is_last:
+            self._p2p(send=(out, self.next))
+            out = torch.zeros((), device=self.e.device)
+        t = out.float().reshape(1).clone()
+        dist.all_reduce(t, group=self.e.pg.pp_group)
+        return t[0]
