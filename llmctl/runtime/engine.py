@@ -211,6 +211,8 @@ class TrainingEngine:
         self.model.train()
         c = self.config
         self.flat.zero_grad()
+        if self.zero3 is not None:
+            self.zero3.begin_step()
         if self.pipeline is not None:
             loss = self.pipeline.run(batches)
         else:
@@ -332,6 +334,8 @@ class TrainingEngine:
 
         named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
         local = {_global_name(n, self.pc.layer_start): p.detach().float().cpu() for n, p in named}
+        if self.zero3 is not None:
+            self.zero3.release_all()
         if not dist.is_initialized():
             return local
         parts: List[Dict[str, torch.Tensor]] = [None] * dist.get_world_size()  # type: ignore

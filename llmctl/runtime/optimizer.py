@@ -69,6 +69,7 @@ class FlatAdamW:
         self.tp = dist.get_world_size(tp_group) if tp_group is not None else 1
         self.tp_rank = dist.get_rank(tp_group) if self.tp > 1 else 0
         self.norm_group = norm_group  # extra group (e.g. pipeline) for the global norm
+        self.dp_sharded = False  # set by ZeRO-3: every rank holds a disjoint parameter shard
         self.step_count = 0
         dev = flat.device
         if self.zero_stage == 0:
@@ -125,7 +126,7 @@ class FlatAdamW:
             if region == "replicated" and self.tp > 1 and self.tp_rank != 0:
                 continue  # counted once per TP group
             ops.l2norm_sq(g, buf)
-        if self.zero_stage > 0:
+        if self.zero_stage > 0 or self.dp_sharded:
             dist.all_reduce(buf, group=self.dp_group)
         if self.tp > 1:
             dist.all_reduce(buf, group=self.tp_group)
