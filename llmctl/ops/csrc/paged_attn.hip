@@ -1,0 +1,185 @@
+// Paged KV cache: write kernel + decode attention over block tables (gfx950).
+//
+// KV layout: k_cache/v_cache [num_blocks, block_size, Hkv, D] bf16 — one token's K row is
+// contiguous (D*2 bytes), a block holds block_size consecutive tokens of one sequence.
+//
+// Decode (one new token per sequence) is HBM-bound: every cached K/V byte is read once.
+// Workgroup = one (sequence, kv-head) pair = 4 waves; the `group = Hq/Hkv` query heads that
+// share the kv head are handled together so GQA reads K/V once per group.  Inside a wave,
+// 16 lanes cooperate on one token (8 contiguous bf16 of D=128 per lane: 16-B loads), so a
+// wave-instruction covers 4 tokens; q·k is reduced over the 16 lanes with xor-shuffles.  Each
+// wave streams a contiguous slice of the context with an online softmax; the 4 waves (and
+// the 4 token groups within each wave) are merged through LDS at the end.
+#include "common.h"
+
+namespace llmctl {
+namespace {
+
+__global__ __launch_bounds__(256) void kv_write_kernel(const unsigned short* __restrict__ k,
+                                                        const unsigned short* __restrict__ v,
+                                                        unsigned short* __restrict__ kc,
+                                                        unsigned short* __restrict__ vc,
+                                                        const int64_t* __restrict__ slots, int N, int row8) {
+  // row8 = Hkv*D/8 vectors per token
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * row8) return;
+  const int t = i / row8, c = i % row8;
+  const long slot = slots[t];
+  if (slot < 0) return;
+  reinterpret_cast<uint4*>(kc)[slot * row8 + c] = reinterpret_cast<const uint4*>(k)[(long)t * row8 + c];
+  reinterpret_cast<uint4*>(vc)[slot * row8 + c] = reinterpret_cast<const uint4*>(v)[(long)t * row8 + c];
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short* __restrict__ q,
+                                                            const unsigned short* __restrict__ kc,
+                                                            const unsigned short* __restrict__ vc,
+                                                            const int* __restrict__ block_tables,
+                                                            const int* __restrict__ ctx_lens,
+                                                            unsigned short* __restrict__ out, int Hq, int Hkv,
+                                                            int block_size, int max_blocks, float scale_log2) {
+  constexpr int LPT = D / 8;          // lanes per token (16 for D=128, 8 for D=64)
+  constexpr int TPW = 64 / LPT;       // tokens per wave-instruction
+  __shared__ float sm_m[4 * TPW][G], sm_l[4 * TPW][G];
+  __shared__ float sm_o[4 * TPW][G][D];
+  const int seq = blockIdx.x / Hkv, hk = blockIdx.x % Hkv;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane % LPT;         // which 8-element slice of D
+  const int tg = lane / LPT;          // token group inside the wave
+  const int L = ctx_lens[seq];
+  const int* bt = block_tables + (long)seq * max_blocks;
+  // q slices for the group's heads
+  float qv[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) load8(q + ((long)seq * Hq + hk * G + g) * D + sub * 8, qv[g]);
+  float m[G], l[G], o[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+  }
+  // contiguous token slice per wave
+  const int per_wave = (L + 3) / 4;
+  const int t0 = wave * per_wave, t1 = min(L, t0 + per_wave);
+  const long kv_row = (long)Hkv * D;
+  for (int t = t0 + tg; t < t1; t += TPW) {
+    const int blk = bt[t / block_size];
+    const long base = ((long)blk * block_size + (t % block_size)) * kv_row + (long)hk * D + sub * 8;
+    float kf[8], vf[8];
+    load8(kc + base, kf);
+    load8(vc + base, vf);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += qv[g][j] * kf[j];
+#pragma unroll
+      for (int off = LPT / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
+      s *= scale_log2;
+      const float mn = fmaxf(m[g], s);
+      const float a = exp2f(m[g] - mn), p = exp2f(s - mn);
+      l[g] = l[g] * a + p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + p * vf[j];
+      m[g] = mn;
+    }
+  }
+  // publish per (wave, token-group) partials
+  const int slot = wave * TPW + tg;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (sub == 0) {
+      sm_m[slot][g] = m[g];
+      sm_l[slot][g] = l[g];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sm_o[slot][g][sub * 8 + j] = o[g][j];
+  }
+  __syncthreads();
+  // combine 4*TPW partials: thread -> (g, d)
+  for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    const int g = idx / D, d = idx % D;
+    float M = -INFINITY;
+    for (int s = 0; s < 4 * TPW; ++s) M = fmaxf(M, sm_m[s][g]);
+    float Ls = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+      for (int s = 0; s < 4 * TPW; ++s) {
+        const float w = exp2f(sm_m[s][g] - M);
+        Ls += sm_l[s][g] * w;
+        O += sm_o[s][g][d] * w;
+      }
+    }
+    out[((long)seq * Hq + hk * G + g) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+  }
+}
+
+}  // namespace
+
+void kv_cache_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at::Tensor& v_cache,
+                    const at::Tensor& slot_mapping) {
+  LLMCTL_CHECK(k.is_contiguous() && v.is_contiguous() && k_cache.is_contiguous() && v_cache.is_contiguous(),
+               "kv_cache_write: contiguous tensors");
+  LLMCTL_CHECK(k.scalar_type() == at::kBFloat16 && k_cache.scalar_type() == at::kBFloat16, "kv_cache_write: bf16");
+  LLMCTL_CHECK(slot_mapping.scalar_type() == at::kLong && slot_mapping.numel() == k.size(0),
+               "slot_mapping: int64 [N]");
+  const int N = k.size(0);
+  const long row = k.numel() / std::max(N, 1);
+  LLMCTL_CHECK(row % 8 == 0 && k_cache.size(2) * k_cache.size(3) == row, "kv row size mismatch");
+  if (N == 0) return;
+  const c10::DeviceGuard g(k.device());
+  const int row8 = row / 8;
+  const long total = (long)N * row8;
+  hipLaunchKernelGGL(kv_write_kernel, dim3((total + 255) / 256), dim3(256), 0, stream(), bf_ptr(k), bf_ptr(v),
+                     bf_mut(k_cache), bf_mut(v_cache), slot_mapping.data_ptr<int64_t>(), N, row8);
+}
+
+at::Tensor paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                                  const at::Tensor& block_tables, const at::Tensor& context_lens, double scale) {
+  LLMCTL_CHECK(q.dim() == 3 && q.is_contiguous() && q.scalar_type() == at::kBFloat16, "q: [N, Hq, D] bf16");
+  LLMCTL_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.sizes() == k_cache.sizes(),
+               "caches: [blocks, block_size, Hkv, D]");
+  LLMCTL_CHECK(block_tables.scalar_type() == at::kInt && block_tables.is_contiguous() &&
+                   context_lens.scalar_type() == at::kInt && context_lens.is_contiguous(),
+               "block_tables / context_lens must be contiguous int32");
+  const int N = q.size(0), Hq = q.size(1), D = q.size(2);
+  const int bs = k_cache.size(1), Hkv = k_cache.size(2);
+  LLMCTL_CHECK(k_cache.size(3) == D && Hq % Hkv == 0, "head shape mismatch");
+  const int G = Hq / Hkv;
+  const int max_blocks = block_tables.size(1);
+  const c10::DeviceGuard g(q.device());
+  auto out = at::empty_like(q);
+  if (N == 0) return out;
+  const float sl2 = (float)(scale * 1.4426950408889634);
+  dim3 grid(N * Hkv), block(256);
+  auto s = stream();
+#define LAUNCH(DD, GG)                                                                                            \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, GG>), grid, block, 0, s, bf_ptr(q), bf_ptr(k_cache), bf_ptr(v_cache), \
+                     block_tables.data_ptr<int>(), context_lens.data_ptr<int>(), bf_mut(out), Hq, Hkv, bs,         \
+                     max_blocks, sl2)
+  if (D == 128) {
+    if (G == 1) LAUNCH(128, 1);
+    else if (G == 2) LAUNCH(128, 2);
+    else if (G == 4) LAUNCH(128, 4);
+    else if (G == 8) LAUNCH(128, 8);
+    else LLMCTL_CHECK(false, "GQA group must be 1/2/4/8");
+  } else if (D == 64) {
+    if (G == 1) LAUNCH(64, 1);
+    else if (G == 2) LAUNCH(64, 2);
+    else if (G == 4) LAUNCH(64, 4);
+    else if (G == 8) LAUNCH(64, 8);
+    else LLMCTL_CHECK(false, "GQA group must be 1/2/4/8");
+  } else {
+    LLMCTL_CHECK(false, "head_dim must be 64 or 128");
+  }
+#undef LAUNCH
+  return out;
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("kv_cache_write", &kv_cache_write);
+  m.impl("paged_attention_decode", &paged_attention_decode);
+}
+
+}  // namespace llmctl

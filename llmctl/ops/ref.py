@@ -278,7 +278,12 @@ def l2norm_sq(t: torch.Tensor) -> torch.Tensor:
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor,
            uniform: torch.Tensor) -> torch.Tensor:
     """Batched temperature / top-k / top-p sampling driven by caller-supplied uniforms
-    (so the kernel and this oracle pick identical tokens).  temperature<=0 => greedy."""
+    (so the kernel and this oracle pick the same token).  temperature<=0 => greedy.
+
+    Semantics (shared with ``csrc/sampling.hip``): x = logits / T; the kept set is
+    {x >= max(T_k, T_p)} where T_k is the k-th largest x and T_p the smallest value of the
+    minimal descending prefix whose softmax mass reaches top_p; the token is drawn by
+    inverse CDF over the kept tokens *in vocabulary order* with r = u * kept_mass."""
     N, V = logits.shape
     out = torch.empty(N, dtype=torch.long, device=logits.device)
     for i in range(N):
@@ -287,22 +292,22 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
         if t <= 0:
             out[i] = int(torch.argmax(l))
             continue
-        p = torch.softmax(l / t, dim=-1)
-        sp, si = torch.sort(p, descending=True, stable=True)
+        x = l / t
+        e = torch.exp(x - x.max())
+        thr = -float("inf")
         k = int(top_k[i])
-        keep = torch.ones(V, dtype=torch.bool, device=l.device)
         if 0 < k < V:
-            keep[k:] = False
+            thr = float(torch.topk(x, k).values[-1])
         tp = float(top_p[i])
         if tp < 1.0:
-            cum = torch.cumsum(sp, 0)
-            keep &= (cum - sp) < tp
-        sp = torch.where(keep, sp, torch.zeros_like(sp))
-        cum = torch.cumsum(sp, 0)
+            sx, si = torch.sort(x, descending=True)
+            cum = torch.cumsum(e[si], 0)
+            n = int(torch.searchsorted(cum, torch.tensor([tp * float(e.sum())], device=cum.device), right=False)[0])
+            thr = max(thr, float(sx[min(n, V - 1)]))
+        keep = x >= thr
+        w = torch.where(keep, e, torch.zeros_like(e))
+        cum = torch.cumsum(w, 0)
         r = float(uniform[i]) * float(cum[-1])
         j = int(torch.searchsorted(cum, torch.tensor([r], device=cum.device, dtype=cum.dtype), right=True)[0])
-        j = min(j, V - 1)
-        while j > 0 and not keep[j]:
-            j -= 1
-        out[i] = si[j]
+        out[i] = min(j, V - 1)
     return out

@@ -1,0 +1,301 @@
+"""Inference engine: batched prefill + paged-KV decode on llmctl's HIP kernels, with
+hipGraph-captured decode steps.
+
+Reference ``InferenceEngine`` (``server.py:127-251``) re-ran a full-prefix HF forward for
+every generated token with ``use_cache=True`` but discarded the cache, right-padded
+batches and read the logits of the padded last position (wrong tokens for shorter
+prompts), and sampled with a host sync per request per token.  Here:
+
+* prefill: prompts are right-padded into one ``[B, S]`` batch (causal attention makes the
+  padding invisible to real tokens) through the flash-attention kernel; K/V of the real
+  tokens are scattered into the paged cache by ``kv_cache_write``; logits are taken at
+  each sequence's own last position;
+* decode: one token per running sequence; per layer ``rope_qkv`` (explicit positions) ->
+  ``kv_cache_write`` -> ``paged_attention_decode`` (block tables, GQA) -> o-proj -> MLP;
+  the whole decode step (embedding .. lm_head) is captured once per batch-size bucket in
+  a HIP graph and replayed with static input buffers (no per-layer launch overhead);
+* sampling: one batched kernel (temperature / top-k / top-p / greedy) with uniforms drawn
+  once per step; the only host sync per step is reading the sampled ids.
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+import time
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from llmctl import ops
+from llmctl.io.artifact import load_model
+from llmctl.models import DecoderLM
+
+from .block_manager import PagedKVCache, make_kv_manager
+from .scheduler import ContinuousBatchScheduler, SamplingParams, Sequence
+from .tokenizer import load_tokenizer
+
+log = logging.getLogger("llmctl.serve")
+
+
+class InferenceEngine:
+    def __init__(self, model_path: str = "tiny", device: str = "auto", dtype=torch.bfloat16, max_batch_size: int = 8,
+                 max_batch_tokens: int = 8192, max_model_len: Optional[int] = None, kv_cache_fraction: float = 0.85,
+                 block_size: int = 16, num_kv_blocks: Optional[int] = None, scheduler: str = "dynamic",
+                 use_graphs: bool = True, seed: int = 0):
+        if device == "auto":
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        if self.device.type == "cpu" and dtype == torch.bfloat16:
+            dtype = torch.float32  # the CPU oracle path
+        self.dtype = dtype
+        self.model_path = model_path
+        self.model: DecoderLM
+        self.model, self.cfg, self.ckpt = load_model(model_path, device=self.device, dtype=dtype, seed=seed)
+        self.model.eval()
+        self.tokenizer = load_tokenizer(str(self.ckpt) if self.ckpt else None)
+        cfg = self.cfg
+        self.max_model_len = max_model_len or cfg.max_position_embeddings
+        self.block_size = block_size
+        self.max_blocks_per_seq = (self.max_model_len + block_size - 1) // block_size
+        if num_kv_blocks is None:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+                free, _ = torch.cuda.mem_get_info(self.device)
+                budget = free * kv_cache_fraction
+            else:
+                budget = 256 * 2 ** 20
+            num_kv_blocks = PagedKVCache.blocks_for_memory(budget, cfg.layers, block_size, cfg.kv_heads, cfg.head_dim,
+                                                           torch.tensor([], dtype=dtype).element_size())
+            num_kv_blocks = min(num_kv_blocks, 1 << 20)
+        self.kv_cache = PagedKVCache(cfg.layers, num_kv_blocks, block_size, cfg.kv_heads, cfg.head_dim, dtype,
+                                     self.device)
+        self.kv = make_kv_manager(num_kv_blocks, block_size)
+        self.scheduler = ContinuousBatchScheduler(self.kv, max_batch_size, max_batch_tokens, self.max_model_len,
+                                                  scheduler, block_size)
+        self.max_batch_size = max_batch_size
+        self.rope = self.model.rope_tables(self.max_model_len, self.device)
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self._graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, Dict[str, torch.Tensor]]] = {}
+        self._rng = torch.Generator(device=self.device)
+        self._rng.manual_seed(seed)
+        self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "graph_replays": 0}
+        log.info("engine: %s on %s, %d KV blocks x %d tokens (%.1f GB)", cfg.name, self.device, num_kv_blocks,
+                 block_size, self.kv_cache.nbytes / 1e9)
+
+    # ------------------------------------------------------------------ model pieces
+    def _embed(self, ids: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        x = F.embedding(ids, m.embed)
+        if m.pos_embed is not None:
+            x = x + m.pos_embed[positions]
+        return x
+
+    def _norm(self, layer, x, res, which: str):
+        w = layer.attn_norm_w if which == "attn" else layer.mlp_norm_w
+        b = layer.attn_norm_b if which == "attn" else layer.mlp_norm_b
+        eps = self.cfg.layer_norm_eps
+        if res is None:
+            return (ops.layernorm(x, w, b, eps) if b is not None else ops.rmsnorm(x, w, eps)), x
+        return ops.add_layernorm(x, res, w, b, eps) if b is not None else ops.add_rmsnorm(x, res, w, eps)
+
+    def _qkv(self, layer, xn, positions, seq_len):
+        qkv = F.linear(xn, layer.wqkv, layer.bqkv)
+        if self.rope is not None:
+            return ops.rope_qkv(qkv, self.rope[0], self.rope[1], layer.nq, layer.nkv, seq_len, positions)
+        T = qkv.shape[0]
+        x = qkv.view(T, layer.nq + 2 * layer.nkv, layer.D)
+        return (x[:, :layer.nq].contiguous(), x[:, layer.nq:layer.nq + layer.nkv].contiguous(),
+                x[:, layer.nq + layer.nkv:].contiguous())
+
+    def _mlp(self, layer, xn):
+        if self.cfg.gated_mlp:
+            out = F.linear(ops.swiglu(F.linear(xn, layer.w_up, layer.b_up)), layer.w_down)
+        else:
+            out = F.linear(ops.gelu(F.linear(xn, layer.w_up, layer.b_up)), layer.w_down)
+        if layer.b_down is not None:
+            out = out + layer.b_down
+        return out
+
+    def _final(self, x, res):
+        m = self.model
+        eps = self.cfg.layer_norm_eps
+        if m.final_norm_b is not None:
+            xn, _ = ops.add_layernorm(x, res, m.final_norm_w, m.final_norm_b, eps)
+        else:
+            xn, _ = ops.add_rmsnorm(x, res, m.final_norm_w, eps)
+        return F.linear(xn, m.head_weight())
+
+    # ------------------------------------------------------------------ prefill
+    @torch.inference_mode()
+    def prefill(self, seqs: List[Sequence]) -> torch.Tensor:
+        """Run the prompts (all known tokens) of ``seqs``; returns last-position logits [n, V]."""
+        lens = [s.num_tokens for s in seqs]
+        B, S = len(seqs), max(lens)
+        ids = torch.zeros(B, S, dtype=torch.long)
+        slots = torch.full((B, S), -1, dtype=torch.long)
+        for i, s in enumerate(seqs):
+            toks = s.all_ids
+            ids[i, :len(toks)] = torch.tensor(toks)
+            slots[i, :len(toks)] = torch.from_numpy(np.asarray(self.kv.slots(s.seq_id, 0, len(toks)), dtype=np.int64))
+        ids = ids.to(self.device, non_blocking=True)
+        slots = slots.to(self.device, non_blocking=True).view(-1)
+        pos = torch.arange(S, device=self.device).repeat(B)
+        x = self._embed(ids.view(-1), pos)
+        res = None
+        kc, vc = self.kv_cache.k, self.kv_cache.v
+        for li, layer in enumerate(self.model.layers):
+            xn, res = self._norm(layer, x, res, "attn")
+            q, k, v = self._qkv(layer, xn, None, S)
+            ops.kv_cache_write(k, v, kc[li], vc[li], slots)
+            o = ops.flash_attention(q.view(B, S, layer.nq, layer.D), k.view(B, S, layer.nkv, layer.D),
+                                    v.view(B, S, layer.nkv, layer.D), causal=True)
+            a = F.linear(o.view(B * S, -1), layer.wo)
+            if layer.bo is not None:
+                a = a + layer.bo
+            xn, res = self._norm(layer, a, res, "mlp")
+            x = self._mlp(layer, xn)
+        last = torch.tensor([i * S + n - 1 for i, n in enumerate(lens)], device=self.device)
+        x_last, res_last = x.index_select(0, last), res.index_select(0, last)
+        self.stats["prefill_tokens"] += sum(lens)
+        return self._final(x_last, res_last)
+
+    # ------------------------------------------------------------------ decode
+    def _decode_body(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
+        x = self._embed(ids, positions)
+        res = None
+        kc, vc = self.kv_cache.k, self.kv_cache.v
+        for li, layer in enumerate(self.model.layers):
+            xn, res = self._norm(layer, x, res, "attn")
+            q, k, v = self._qkv(layer, xn, positions, self.max_model_len)
+            ops.kv_cache_write(k, v, kc[li], vc[li], slots)
+            o = ops.paged_attention_decode(q, kc[li], vc[li], block_tables, ctx_lens)
+            a = F.linear(o.view(o.shape[0], -1), layer.wo)
+            if layer.bo is not None:
+                a = a + layer.bo
+            xn, res = self._norm(layer, a, res, "mlp")
+            x = self._mlp(layer, xn)
+        return self._final(x, res)
+
+    def _bucket(self, n: int) -> int:
+        b = 1
+        while b < n:
+            b *= 2
+        return min(b, max(self.max_batch_size, n))
+
+    def _static(self, nb: int) -> Dict[str, torch.Tensor]:
+        d = self.device
+        return {"ids": torch.zeros(nb, dtype=torch.long, device=d),
+                "positions": torch.zeros(nb, dtype=torch.int32, device=d),
+                "slots": torch.full((nb,), -1, dtype=torch.long, device=d),
+                "block_tables": torch.zeros(nb, self.max_blocks_per_seq, dtype=torch.int32, device=d),
+                "ctx_lens": torch.ones(nb, dtype=torch.int32, device=d)}
+
+    def _capture(self, nb: int):
+        bufs = self._static(nb)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up (allocator / lazy init) outside the graph
+                self._decode_body(bufs["ids"], bufs["positions"], bufs["slots"], bufs["block_tables"],
+                                  bufs["ctx_lens"])
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            bufs["logits"] = self._decode_body(bufs["ids"], bufs["positions"], bufs["slots"], bufs["block_tables"],
+                                               bufs["ctx_lens"])
+        self._graphs[nb] = (g, bufs)
+
+    @torch.inference_mode()
+    def decode(self, seqs: List[Sequence]) -> torch.Tensor:
+        n = len(seqs)
+        ids = [s.all_ids[-1] for s in seqs]
+        positions = [s.num_tokens - 1 for s in seqs]
+        slots = [s._decode_slot for s in seqs]
+        ctx = [self.kv.num_tokens(s.seq_id) for s in seqs]
+        bt = np.asarray(self.kv.block_tables([s.seq_id for s in seqs], self.max_blocks_per_seq))
+        self.stats["decode_tokens"] += n
+        if self.use_graphs:
+            nb = self._bucket(n)
+            if nb not in self._graphs:
+                self._capture(nb)
+            g, b = self._graphs[nb]
+            b["ids"][:n].copy_(torch.tensor(ids), non_blocking=True)
+            b["positions"][:n].copy_(torch.tensor(positions, dtype=torch.int32), non_blocking=True)
+            b["slots"].fill_(-1)
+            b["slots"][:n].copy_(torch.tensor(slots), non_blocking=True)
+            b["block_tables"][:n].copy_(torch.from_numpy(bt), non_blocking=True)
+            b["ctx_lens"].fill_(1)
+            b["ctx_lens"][:n].copy_(torch.tensor(ctx, dtype=torch.int32), non_blocking=True)
+            g.replay()
+            self.stats["graph_replays"] += 1
+            return b["logits"][:n]
+        d = self.device
+        return self._decode_body(torch.tensor(ids, device=d), torch.tensor(positions, dtype=torch.int32, device=d),
+                                 torch.tensor(slots, device=d), torch.from_numpy(bt).to(d),
+                                 torch.tensor(ctx, dtype=torch.int32, device=d))
+
+    # ------------------------------------------------------------------ sampling
+    def sample(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[int]:
+        n = len(seqs)
+        d = self.device
+        temp = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32, device=d)
+        topk = torch.tensor([s.params.top_k if s.params.top_k and s.params.top_k > 0 else 0 for s in seqs],
+                            dtype=torch.int32, device=d)
+        topp = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32, device=d)
+        u = torch.rand(n, generator=self._rng, device=d)
+        toks = ops.sample(logits.contiguous(), temp, topk, topp, u)
+        return toks.tolist()
+
+    # ------------------------------------------------------------------ step loop
+    def add_request(self, prompt_ids: List[int], params: SamplingParams, request_id: str = "", on_token=None,
+                    on_finish=None) -> Sequence:
+        seq = Sequence(prompt_ids=list(prompt_ids), params=params, request_id=request_id, on_token=on_token,
+                       on_finish=on_finish)
+        self.scheduler.add(seq)
+        return seq
+
+    def _append(self, seq: Sequence, tok: int) -> None:
+        now = time.time()
+        if seq.first_token_time is None:
+            seq.first_token_time = now
+        seq.output_ids.append(tok)
+        if seq.on_token:
+            seq.on_token(seq, tok)
+        eos = getattr(self.tokenizer, "eos_token_id", None)
+        if not seq.params.ignore_eos and eos is not None and tok == eos:
+            self.scheduler.finish(seq, "stop")
+        elif len(seq.output_ids) >= seq.params.max_tokens:
+            self.scheduler.finish(seq, "length")
+        elif seq.num_tokens >= self.max_model_len:
+            self.scheduler.finish(seq, "length")
+        elif seq.params.stop:
+            text = self.tokenizer.decode(seq.output_ids)
+            if any(st and st in text for st in seq.params.stop):
+                self.scheduler.finish(seq, "stop")
+
+    def step(self) -> int:
+        """One scheduling iteration; returns the number of tokens produced."""
+        out = self.scheduler.schedule()
+        produced = 0
+        if out.decode:
+            logits = self.decode(out.decode)
+            for seq, tok in zip(out.decode, self.sample(logits, out.decode)):
+                self._append(seq, tok)
+                produced += 1
+        if out.prefill:
+            # cap the padded prefill batch by the token budget (padding is real compute)
+            logits = self.prefill(out.prefill)
+            for seq, tok in zip(out.prefill, self.sample(logits, out.prefill)):
+                self._append(seq, tok)
+                produced += 1
+        self.stats["steps"] += 1
+        return produced
+
+    def generate(self, prompts: List[List[int]], params: SamplingParams) -> List[Sequence]:
+        seqs = [self.add_request(p, params) for p in prompts]
+        while any(s.status != "finished" for s in seqs):
+            self.step()
+        return seqs

@@ -1,0 +1,185 @@
+"""Continuous-batching scheduler (and a static batcher for comparison).
+
+Reference ``DynamicBatchScheduler`` (``server.py:89-125``): FIFO admission up to 8 requests
+/ 8192 tokens, head-of-line blocking, and — the fatal bug — unfinished requests were never
+re-queued, so any ``max_tokens > 1`` request hung.
+
+Here (``scheduler="dynamic"``), every engine step:
+1. all RUNNING sequences decode one token (up to ``max_batch_size``); each first gets a KV
+   slot — if the pool is exhausted the most recently admitted sequence is preempted (its
+   blocks freed, it returns to the front of the queue and is recomputed later);
+2. WAITING sequences are admitted FIFO for prefill while the step's token budget
+   (``max_batch_tokens`` minus the decode tokens), the batch-size cap and the free KV
+   blocks (prompt + one block headroom) allow.
+``scheduler="static"`` admits a new group only when the running group has fully finished.
+"""
+
+from __future__ import annotations
+
+import itertools
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Any, Callable, Deque, List, Optional, Tuple
+
+
+@dataclass
+class SamplingParams:
+    max_tokens: int = 100
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = -1
+    stop: List[str] = field(default_factory=list)
+    ignore_eos: bool = False
+    seed: Optional[int] = None
+
+
+_ids = itertools.count(1)
+
+
+@dataclass
+class Sequence:
+    prompt_ids: List[int]
+    params: SamplingParams
+    request_id: str = ""
+    seq_id: int = field(default_factory=lambda: next(_ids))
+    output_ids: List[int] = field(default_factory=list)
+    status: str = "waiting"  # waiting | running | finished
+    finish_reason: Optional[str] = None
+    arrival_time: float = field(default_factory=time.time)
+    first_token_time: Optional[float] = None
+    finish_time: Optional[float] = None
+    preemptions: int = 0
+    on_token: Optional[Callable[["Sequence", int], None]] = None
+    on_finish: Optional[Callable[["Sequence"], None]] = None
+
+    @property
+    def all_ids(self) -> List[int]:
+        return self.prompt_ids + self.output_ids
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.prompt_ids) + len(self.output_ids)
+
+
+@dataclass
+class SchedulerOutput:
+    prefill: List[Sequence]
+    decode: List[Sequence]
+    preempted: List[Sequence]
+
+
+class ContinuousBatchScheduler:
+    def __init__(self, kv, max_batch_size: int = 8, max_batch_tokens: int = 8192, max_model_len: int = 4096,
+                 policy: str = "dynamic", block_size: int = 16):
+        self.kv = kv
+        self.block_size = block_size
+        self.max_batch_size = max_batch_size
+        self.max_batch_tokens = max_batch_tokens
+        self.max_model_len = max_model_len
+        self.policy = policy
+        self.waiting: Deque[Sequence] = deque()
+        self.running: List[Sequence] = []
+
+    # ------------------------------------------------------------------ queue
+    def add(self, seq: Sequence) -> None:
+        if len(seq.prompt_ids) == 0:
+            raise ValueError("empty prompt")
+        if len(seq.prompt_ids) >= self.max_model_len:
+            raise ValueError(f"prompt of {len(seq.prompt_ids)} tokens exceeds max_model_len {self.max_model_len}")
+        self.waiting.append(seq)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    @property
+    def num_waiting(self) -> int:
+        return len(self.waiting)
+
+    @property
+    def num_running(self) -> int:
+        return len(self.running)
+
+    # ------------------------------------------------------------------ step
+    def schedule(self) -> SchedulerOutput:
+        preempted: List[Sequence] = []
+        decode: List[Sequence] = []
+        # 1) decodes for running sequences (each needs one more KV slot)
+        for seq in list(self.running):
+            if len(decode) >= self.max_batch_size:
+                break
+            if seq.status != "running":  # preempted earlier in this loop
+                continue
+            slot = self.kv.append_token(seq.seq_id)
+            while slot < 0:
+                victim = self._preempt_newest(exclude=seq)
+                if victim is None:
+                    break
+                preempted.append(victim)
+                slot = self.kv.append_token(seq.seq_id)
+            if slot < 0:  # cannot even fit this one: preempt it
+                self._preempt(seq)
+                preempted.append(seq)
+                continue
+            seq._decode_slot = slot
+            decode.append(seq)
+        # 2) admissions (prefill)
+        prefill: List[Sequence] = []
+        if self.policy == "static" and self.running:
+            return SchedulerOutput(prefill, decode, preempted)
+        budget = self.max_batch_tokens - len(decode)
+        while self.waiting and len(self.running) + len(prefill) < self.max_batch_size:
+            seq = self.waiting[0]
+            n = seq.num_tokens  # recompute generated tokens after a preemption
+            if n > budget and (prefill or decode):
+                break
+            if not self.kv.can_allocate(n + self.kv_block_size()):
+                break
+            self.waiting.popleft()
+            ok = self.kv.add_sequence(seq.seq_id, n)
+            if not ok:
+                self.waiting.appendleft(seq)
+                break
+            seq.status = "running"
+            prefill.append(seq)
+            budget -= n
+        self.running.extend(prefill)
+        return SchedulerOutput(prefill, decode, preempted)
+
+    def kv_block_size(self) -> int:
+        return self.block_size
+
+    def _preempt_newest(self, exclude: Sequence) -> Optional[Sequence]:
+        for seq in reversed(self.running):
+            if seq is not exclude:
+                self._preempt(seq)
+                return seq
+        return None
+
+    def _preempt(self, seq: Sequence) -> None:
+        self.kv.free_sequence(seq.seq_id)
+        if seq in self.running:
+            self.running.remove(seq)
+        seq.status = "waiting"
+        seq.preemptions += 1
+        self.waiting.appendleft(seq)
+
+    def finish(self, seq: Sequence, reason: str) -> None:
+        seq.status = "finished"
+        seq.finish_reason = reason
+        seq.finish_time = time.time()
+        self.kv.free_sequence(seq.seq_id)
+        if seq in self.running:
+            self.running.remove(seq)
+        if seq.on_finish:
+            seq.on_finish(seq)
+
+    def abort(self, request_id: str) -> None:
+        for seq in list(self.running) + list(self.waiting):
+            if seq.request_id == request_id:
+                if seq in self.waiting:
+                    self.waiting.remove(seq)
+                    seq.status = "finished"
+                    seq.finish_reason = "abort"
+                else:
+                    self.finish(seq, "abort")

@@ -198,3 +198,57 @@ def test_functional_autograd_matches_ref(native_lib):
     assert abs(l1 - loss2.item()) < 2e-2
     for a, p in zip(g1, m.parameters()):
         assert _rel(a, p.grad) < 5e-2
+
+
+# ----------------------------------------------------------------------------- serving kernels
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 32, 128), (8, 2, 128), (4, 4, 64), (16, 2, 64)])
+def test_paged_attention_decode(native_lib, Hq, Hkv, D):
+    torch.manual_seed(0)
+    nb, bs, N = 64, 16, 5
+    kc = _bf(nb, bs, Hkv, D, seed=41)
+    vc = _bf(nb, bs, Hkv, D, seed=42)
+    lens = torch.tensor([1, 17, 100, 250, 33], dtype=torch.int32, device=DEV)
+    maxb = 16
+    bt = torch.randperm(nb, device=DEV)[: N * maxb].view(N, maxb).to(torch.int32).contiguous()
+    q = _bf(N, Hq, D, seed=43)
+    o = native_lib.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+    orf = ref.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+    assert _rel(o, orf) < 2e-2, _rel(o, orf)
+
+
+def test_kv_cache_write(native_lib):
+    nb, bs, H, D = 8, 16, 4, 128
+    kc = torch.zeros(nb, bs, H, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    k, v = _bf(10, H, D, seed=51), _bf(10, H, D, seed=52)
+    slots = torch.tensor([0, 5, 17, 33, 127, 64, 65, 66, -1, 100], device=DEV)
+    native_lib.kv_cache_write(k, v, kc, vc, slots)
+    kr, vr = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.kv_cache_write(k, v, kr, vr, slots)
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)
+
+
+def test_sampling(native_lib):
+    torch.manual_seed(0)
+    N, V = 64, 32000
+    logits = (torch.randn(N, V, device=DEV) * 3).to(torch.bfloat16)
+    temp = torch.rand(N, device=DEV) + 0.3
+    temp[:8] = 0.0  # greedy rows
+    topk = torch.randint(0, 100, (N,), device=DEV, dtype=torch.int32)
+    topp = torch.rand(N, device=DEV) * 0.6 + 0.4
+    topp[::3] = 1.0
+    u = torch.rand(N, device=DEV)
+    got = native_lib.sample(logits, temp, topk, topp, u)
+    exp = ref.sample(logits, temp, topk, topp, u)
+    assert torch.equal(got[:8], exp[:8])
+    assert (got != exp).sum().item() <= 2  # float summation order at an inverse-CDF boundary
+
+
+def test_gemm_and_copy(native_lib):
+    a, b = _bf(256, 512, seed=61), _bf(384, 512, seed=62)
+    c = native_lib.gemm_bf16(a, b)
+    assert _rel(c, a.float() @ b.float().t()) < 1e-2
+    src = _bf(1 << 16, seed=63)
+    dst = torch.empty_like(src)
+    native_lib.hbm_copy(src, dst)
+    assert torch.equal(src, dst)

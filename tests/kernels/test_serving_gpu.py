@@ -1,0 +1,43 @@
+"""Serving engine on the GPU: HIP kernels + hipGraph decode must match the eager path."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_graph_decode_matches_eager_and_forward(native_lib):
+    from llmctl.serve.engine import InferenceEngine
+    from llmctl.serve.scheduler import SamplingParams
+
+    prompts = [[1, 2, 3, 4, 5], [9] * 37, [7, 7], [3] * 70]
+    p = SamplingParams(max_tokens=12, temperature=0.0)
+    eg = InferenceEngine("tiny", device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16,
+                         max_model_len=512, use_graphs=True)
+    ee = InferenceEngine("tiny", device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16,
+                         max_model_len=512, use_graphs=False)
+    a = eg.generate(prompts, p)
+    b = ee.generate(prompts, p)
+    assert eg.stats["graph_replays"] > 0
+    assert [s.output_ids for s in a] == [s.output_ids for s in b]
+    # bf16 rounding differs between paged decode and the full prefill forward; require
+    # the first generated token (pure prefill) to match and most later ones
+    m = eg.model
+    agree = total = 0
+    for s in a:
+        logits = m(torch.tensor([s.all_ids[:-1]], device="cuda"))
+        ref_next = logits.view(-1, logits.shape[-1]).argmax(-1)[len(s.prompt_ids) - 1:].tolist()
+        assert ref_next[0] == s.output_ids[0]
+        agree += sum(int(x == y) for x, y in zip(ref_next, s.output_ids))
+        total += len(s.output_ids)
+    assert agree / total > 0.9
+
+
+def test_sampling_params_respected(native_lib):
+    from llmctl.serve.engine import InferenceEngine
+    from llmctl.serve.scheduler import SamplingParams
+
+    e = InferenceEngine("tiny", device="cuda", max_batch_size=8, num_kv_blocks=64, block_size=16, max_model_len=256)
+    seqs = e.generate([[5, 6, 7]] * 8, SamplingParams(max_tokens=6, temperature=1.0, top_k=1))
+    outs = {tuple(s.output_ids) for s in seqs}
+    assert len(outs) == 1  # top_k=1 is greedy regardless of temperature
