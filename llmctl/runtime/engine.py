@@ -116,6 +116,8 @@ class TrainingEngine:
             self.device = torch.device("cuda", self.env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
         else:
             self.device = torch.device(c.device)
+            if self.device.type == "cuda" and self.device.index is None:
+                self.device = torch.device("cuda", self.env.local_rank)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         backend = c.distributed_backend

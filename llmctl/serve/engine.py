@@ -48,6 +48,8 @@ class InferenceEngine:
         if device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         if self.device.type == "cpu" and dtype == torch.bfloat16:
             dtype = torch.float32  # the CPU oracle path
         self.dtype = dtype

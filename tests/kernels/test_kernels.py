@@ -204,7 +204,7 @@ def test_functional_autograd_matches_ref(native_lib):
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 32, 128), (8, 2, 128), (4, 4, 64), (16, 2, 64)])
 def test_paged_attention_decode(native_lib, Hq, Hkv, D):
     torch.manual_seed(0)
-    nb, bs, N = 64, 16, 5
+    nb, bs, N = 96, 16, 5
     kc = _bf(nb, bs, Hkv, D, seed=41)
     vc = _bf(nb, bs, Hkv, D, seed=42)
     lens = torch.tensor([1, 17, 100, 250, 33], dtype=torch.int32, device=DEV)
