@@ -151,9 +151,9 @@ class PlanParallelism(_Open):
     zero_stage: int
     micro_batch_size: int
     global_batch_size: int
-    estimated_memory_gb: float
-    estimated_comm_gb: float
-    estimated_flops: float
+    estimated_memory_gb: Optional[float] = None  # written by `plan compute`; optional in hand-written plans
+    estimated_comm_gb: Optional[float] = None
+    estimated_flops: Optional[float] = None
     sequence_parallel: bool = False
     activation_checkpoint: str = "none"
     grad_accum: int = 1

@@ -105,7 +105,9 @@ def tokenize_to_bin(src: str, dst: str, vocab_size: int = 256) -> int:
     out = []
     with open(src_p, "r", encoding="utf-8", errors="replace") as f:
         for line in f:
-            text = line
+            text = line.rstrip("\n")
+            if not text:
+                continue  # same document split as the native indexer: one non-empty line per doc
             if src_p.suffix == ".jsonl":
                 try:
                     text = json.loads(line).get("text", "")

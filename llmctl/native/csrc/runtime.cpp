@@ -335,7 +335,32 @@ py::tuple index_bytes(const std::string& text_path, const std::string& bin_path,
         char c = doc[i];
         if (c == '\\' && i + 1 < doc.size()) {
           char n = doc[++i];
-          out.push_back(n == 'n' ? '\n' : n == 't' ? '\t' : n);
+          if (n == 'u' && i + 4 < doc.size()) {
+            uint32_t cp = std::stoul(doc.substr(i + 1, 4), nullptr, 16);
+            i += 4;
+            if (cp >= 0xD800 && cp < 0xDC00 && i + 6 < doc.size() && doc[i + 1] == '\\' && doc[i + 2] == 'u') {
+              uint32_t lo = std::stoul(doc.substr(i + 3, 4), nullptr, 16);
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+              i += 6;
+            }
+            if (cp < 0x80) {
+              out.push_back(char(cp));
+            } else if (cp < 0x800) {
+              out.push_back(char(0xC0 | (cp >> 6)));
+              out.push_back(char(0x80 | (cp & 0x3F)));
+            } else if (cp < 0x10000) {
+              out.push_back(char(0xE0 | (cp >> 12)));
+              out.push_back(char(0x80 | ((cp >> 6) & 0x3F)));
+              out.push_back(char(0x80 | (cp & 0x3F)));
+            } else {
+              out.push_back(char(0xF0 | (cp >> 18)));
+              out.push_back(char(0x80 | ((cp >> 12) & 0x3F)));
+              out.push_back(char(0x80 | ((cp >> 6) & 0x3F)));
+              out.push_back(char(0x80 | (cp & 0x3F)));
+            }
+          } else {
+            out.push_back(n == 'n' ? '\n' : n == 't' ? '\t' : n == 'r' ? '\r' : n == 'b' ? '\b' : n == 'f' ? '\f' : n);
+          }
         } else if (c == '"') {
           break;
         } else {

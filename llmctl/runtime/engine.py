@@ -261,6 +261,7 @@ class TrainingEngine:
     # ------------------------------------------------------------------ loop
     def train(self, data_iter: Optional[Iterator] = None) -> Dict[str, float]:
         from llmctl.io.checkpoint import CheckpointManager
+        from llmctl.runtime.replay import write_manifest
 
         c = self.config
         data = data_iter if data_iter is not None else iter(self.make_data())
@@ -310,8 +311,10 @@ class TrainingEngine:
                     log.info("step %d eval loss %.4f", s, vl)
             if c.save_steps and s % c.save_steps == 0:
                 ckpt.save(f"checkpoint-{s}")
+                write_manifest(self, history)
         ckpt.save("final", final=True)
         ckpt.wait()
+        write_manifest(self, history, status="complete")
         return {"final_loss": last_loss, "steps": self.global_step, "history": history}
 
     # ------------------------------------------------------------------ state (layout-independent)

@@ -1,0 +1,127 @@
+"""Planner golden values, the MI355X cost model, TOML round-trip, schemas."""
+
+import json
+from pathlib import Path
+
+import pytest
+
+from llmctl.config.schemas import resolve_training_config, validate
+from llmctl.config.toml_io import dumps_toml, load_toml, loads_toml
+from llmctl.models.config import get_model_config
+from llmctl.partition.planner import ParallelismPlanner, ReferenceCompatPlanner
+from llmctl.partition.shard_map import build_shard_map, split_layers
+
+ROOT = Path(__file__).resolve().parents[2]
+LLAMA7B = json.loads((ROOT / "configs/models/llama-7b.json").read_text())
+HW8 = {"gpu": {"count": 8}}
+
+
+# ---------------------------------------------------------------- reference-compatible planner (golden)
+def test_reference_param_and_memory_formulas():
+    p = ReferenceCompatPlanner(LLAMA7B, HW8)
+    assert p.estimate_parameters() == 5_164_761_088
+    assert abs(p.estimate_model_memory() - 57.72) < 0.01
+    assert abs(p.estimate_activation_memory(1, 2048) - 0.75) < 1e-9
+
+
+def test_reference_search_golden_plan():
+    best = ReferenceCompatPlanner(LLAMA7B, HW8).search_optimal_plan(1e14, 40, 100)
+    assert (best["tensor_parallel"], best["pipeline_parallel"], best["data_parallel"], best["zero_stage"],
+            best["micro_batch_size"], best["global_batch_size"]) == (8, 1, 1, 0, 1, 4)
+    assert abs(best["estimated_memory_gb"] - 7.97) < 0.01
+
+
+def test_reference_manual_golden_plan():
+    m = ReferenceCompatPlanner(LLAMA7B, HW8).manual_plan(2, 2, 3)
+    assert abs(m["estimated_memory_gb"] - 5.57) < 0.01
+    assert abs(m["estimated_comm_gb"] - 9.62) < 0.01
+    assert abs(m["estimated_flops"] - 1.69e14) / 1.69e14 < 0.01
+
+
+def test_reference_70b_like():
+    d = dict(hidden=8192, layers=80, ffn=28672, vocab_size=128256, heads=64)
+    p = ReferenceCompatPlanner(d, HW8)
+    assert abs(p.estimate_parameters() / 1e9 - 60.1) < 0.05
+    assert abs(p.estimate_model_memory() - 671.8) < 0.5
+    assert p.search_optimal_plan(1e15, 1000, 100)["tensor_parallel"] == 8
+
+
+# ---------------------------------------------------------------- MI355X planner
+def test_exact_param_count_matches_reference_config():
+    cfg = get_model_config(str(ROOT / "configs/models/llama-7b.json"))
+    assert cfg.num_parameters() == 6_738_415_616  # the reference's own estimated_params
+
+
+def _mi355x(n):
+    from llmctl.cli.commands.hw import mi355x_preset
+
+    return mi355x_preset(n)
+
+
+def test_mi355x_plan_7b_single_node_prefers_dp():
+    pl = ParallelismPlanner(LLAMA7B, _mi355x(8))
+    best = pl.search_optimal_plan(max_memory=259)
+    assert best["tensor_parallel"] * best["pipeline_parallel"] * best["data_parallel"] == 8
+    # 7B fits one 288 GB GPU with ZeRO: no model parallelism is needed on xGMI
+    assert best["tensor_parallel"] == 1 and best["pipeline_parallel"] == 1
+    assert best["estimated_memory_gb"] <= 259
+
+
+def test_mi355x_plan_70b_needs_sharding():
+    d = json.loads((ROOT / "configs/models/llama-70b.json").read_text())
+    pl = ParallelismPlanner(d, _mi355x(8))
+    best = pl.search_optimal_plan(max_memory=259)
+    assert best["estimated_memory_gb"] <= 259
+    assert best["tensor_parallel"] > 1 or best["pipeline_parallel"] > 1 or best["zero_stage"] >= 1
+
+
+def test_memory_monotone_in_sharding():
+    pl = ParallelismPlanner(LLAMA7B, _mi355x(8))
+    m0 = pl.compute_memory_requirement(1, 1, 8, 0, 1)
+    m1 = pl.compute_memory_requirement(1, 1, 8, 1, 1)
+    m3 = pl.compute_memory_requirement(1, 1, 8, 3, 1)
+    mt = pl.compute_memory_requirement(8, 1, 1, 0, 1)
+    assert m0 > m1 > m3
+    assert mt < m0
+
+
+def test_shard_map():
+    assert split_layers(32, 4) == [(0, 8), (8, 16), (16, 24), (24, 32)]
+    sm = build_shard_map(LLAMA7B, tp=2, pp=2, dp=2, zero_stage=1)
+    assert sm is not None
+
+
+# ---------------------------------------------------------------- TOML + schemas
+def test_toml_roundtrip_nested():
+    d = {"a": 1, "b": {"c": [1, 2, 3], "d": {"e": "x\"y", "f": 1.5e-5, "g": True}},
+         "devs": [{"id": 0, "name": "MI355X"}, {"id": 1, "name": "MI355X"}]}
+    back = loads_toml(dumps_toml(d))
+    assert back == d
+
+
+def test_reference_presets_parse_and_validate():
+    ref = Path("/root/reference/configs/presets")
+    files = sorted(ref.glob("*.toml")) if ref.exists() else []
+    files += sorted((ROOT / "configs/presets").glob("*.toml"))
+    assert files
+    for f in files:
+        d = load_toml(f)
+        kind = "hardware" if "gpu" in d and "system" in d else "train"
+        validate(kind, d)
+
+
+def test_resolve_precedence():
+    t = load_toml(ROOT / "configs/presets/llama-7b-mi355x8.toml")
+    plan = {"parallelism": {"tensor_parallel": 2, "pipeline_parallel": 1, "data_parallel": 4, "zero_stage": 2,
+                            "micro_batch_size": 4, "global_batch_size": 64}}
+    out = resolve_training_config(t, plan, {"batch_size": 3, "learning_rate": None})
+    assert out["tensor_parallel"] == 2 and out["zero_stage"] == 2
+    assert out["batch_size"] == 3  # CLI beats plan
+    assert out["learning_rate"] == pytest.approx(2e-4)  # None CLI value does not override the file
+
+
+def test_model_json_configs_load():
+    for f in sorted((ROOT / "configs/models").glob("*.json")):
+        cfg = get_model_config(str(f))
+        d = json.loads(f.read_text())
+        assert cfg.num_parameters() == d["estimated_params"], f.name

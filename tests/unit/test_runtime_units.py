@@ -1,0 +1,143 @@
+"""CPU unit tests: launchers (argv/env, no exec), LR schedules, native data loader, quantizers,
+plugin registry, health thresholds, autotuner, TP shard/consolidate round-trip."""
+
+import json
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from llmctl.runtime.launcher import LaunchConfig, create_launcher
+
+
+# ---------------------------------------------------------------- launchers
+def test_local_launcher_argv_env():
+    c = LaunchConfig(nodes=1, gpus_per_node=8, master_port=29611, deterministic=True, seed=7)
+    L = create_launcher(c)
+    cmd = L.build_command("llmctl.runtime.worker", ["--max-steps", "2"])
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc_per_node=8" in cmd and "--master_addr=127.0.0.1" in cmd and "--master_port=29611" in cmd
+    assert cmd[-4:] == ["-m", "llmctl.runtime.worker", "--max-steps", "2"]
+    env = L.get_environment()
+    assert env["WORLD_SIZE"] == "8" and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert env["PYTHONHASHSEED"] == "7" and env["LLMCTL_DETERMINISTIC"] == "1"
+
+
+def test_slurm_mpi_k8s_launchers():
+    c = LaunchConfig(nodes=2, gpus_per_node=8, launcher="slurm")
+    s = create_launcher(c).create_slurm_script("llmctl.runtime.worker", ["--seed", "1"])
+    assert "#SBATCH --nodes=2" in s and "#SBATCH --ntasks-per-node=8" in s and "-m llmctl.runtime.worker" in s
+    m = create_launcher(LaunchConfig(nodes=2, gpus_per_node=8, launcher="mpi")).build_command("train.py", [])
+    assert m[:3] == ["mpirun", "-np", "16"]
+    k = create_launcher(LaunchConfig(nodes=4, gpus_per_node=8, launcher="k8s")).render_manifest("x.py", ["--a"])
+    assert "completions: 4" in k and "amd.com/gpu: 8" in k
+
+
+# ---------------------------------------------------------------- LR schedules
+def test_lr_schedules():
+    from llmctl.runtime.optimizer import LRSchedule
+
+    lin = LRSchedule(1.0, "linear", warmup_steps=10, total_steps=110)
+    assert lin(5) == pytest.approx(0.5) and lin(10) == pytest.approx(1.0) and lin(110) == pytest.approx(0.0)
+    cos = LRSchedule(1.0, "cosine", warmup_steps=0, total_steps=100, min_lr_ratio=0.1)
+    assert cos(0) == pytest.approx(1.0) and cos(100) == pytest.approx(0.1) and cos(50) == pytest.approx(0.55)
+    assert LRSchedule(3e-4, "constant")(1000) == 3e-4
+
+
+# ---------------------------------------------------------------- data loader
+@pytest.fixture()
+def token_file(tmp_path):
+    arr = np.arange(64 * 33 + 1, dtype=np.uint16) % 50000
+    p = tmp_path / "tok.bin"
+    arr.tofile(p)
+    return p
+
+
+def test_memmap_tokens_dp_partition_and_resume(token_file):
+    from llmctl.io.dataset import MemmapTokens
+
+    S, B = 32, 4
+    seen = []
+    for r in range(2):
+        ds = MemmapTokens(str(token_file), S, B, dp_rank=r, dp_size=2, seed=3)
+        starts = set()
+        for _ in range(8):  # 8 batches x 4 = 32 samples = one epoch per rank
+            x, y = ds.next_batch()
+            assert x.shape == (B, S) and torch.equal(x[:, 1:], y[:, :-1])
+            starts.update(int(v) // S for v in x[:, 0])
+        seen.append(starts)
+    assert not (seen[0] & seen[1]), "DP ranks must read disjoint samples"
+    assert len(seen[0] | seen[1]) == 64
+    a = MemmapTokens(str(token_file), S, B, seed=3)
+    for _ in range(3):
+        a.next_batch()
+    st = a.state_dict()
+    want = a.next_batch()[0]
+    b = MemmapTokens(str(token_file), S, B, seed=3)
+    b.load_state_dict(st)
+    assert torch.equal(b.next_batch()[0], want)
+
+
+# ---------------------------------------------------------------- quantizers + registry
+@pytest.mark.parametrize("name,tol", [("int8", 0.01), ("int4", 0.15), ("fp8", 0.07)])
+def test_quantizers_roundtrip(name, tol):
+    from llmctl.plugins.quantizers import QUANTIZERS, dequantize
+
+    torch.manual_seed(0)
+    w = torch.randn(64, 129)
+    q = QUANTIZERS[name](w)
+    back = dequantize(name, q, tuple(w.shape))
+    rel = (back - w).norm() / w.norm()
+    assert rel < tol, rel
+
+
+def test_plugin_registry():
+    from llmctl.plugins.registry import registry
+
+    assert {"int8", "int4", "fp8", "int8-awq", "int4-gptq"} <= set(registry.names("quantizers"))
+    assert {"safetensors", "hf"} <= set(registry.names("exporters"))
+    assert "flash_attention_v3" in registry.names("kernels")
+    sched = registry.get("schedulers", "lr-cosine")(1.0, total_steps=10)
+    assert sched(10) == pytest.approx(0.1)
+    with pytest.raises(KeyError):
+        registry.get("exporters", "nope")
+
+
+# ---------------------------------------------------------------- health
+def test_training_health_thresholds():
+    from llmctl.metrics.health import HealthStatus, TrainingHealthMonitor
+
+    m = TrainingHealthMonitor()
+    m.update_training_metrics(loss=2.0, grad_norm=1.0, throughput=1000.0)
+    assert m.get_health_report().status == HealthStatus.HEALTHY
+    m.update_training_metrics(loss=float("nan"), grad_norm=1.0, throughput=1000.0)
+    assert m.get_health_report().status != HealthStatus.HEALTHY
+
+
+# ---------------------------------------------------------------- autotuner
+def test_autotuner_cpu_cache(tmp_path):
+    from llmctl.plugins.autotuning import TuningConfig, create_auto_tuner
+
+    t = create_auto_tuner(TuningConfig(max_iterations=4, warmup_iterations=1, measurement_iterations=2, timeout=30))
+    r = t.tune_matmul((64, 64, 64), device="cpu")
+    assert r.best_config and r.best_performance > 0
+    f = tmp_path / "cache.json"
+    t.save_results(str(f))
+    t2 = create_auto_tuner()
+    t2.load_results(str(f))
+    assert json.loads(f.read_text())
+
+
+# ---------------------------------------------------------------- TP shard/consolidate (checkpoint reshard)
+@pytest.mark.parametrize("tp", [2, 4])
+def test_tp_shard_consolidate_roundtrip(tp):
+    from llmctl.io.checkpoint import consolidate_tp, shard_tp
+    from llmctl.models import build_model, get_model_config
+
+    cfg = get_model_config("tiny")
+    m = build_model(cfg, dtype=torch.float32)
+    for n, p in m.named_parameters():
+        shards = [shard_tp(n, p.detach(), tp, r, cfg) for r in range(tp)]
+        back = consolidate_tp(n, shards, cfg)
+        assert torch.equal(back, p.detach()), n
