@@ -19,6 +19,39 @@ import torch
 import torch.nn.functional as F
 
 
+def _gemm_ex_ok(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Shapes/layouts the hand-written MFMA wgrad kernel (llmctl/ops/csrc/gemm_bf16.hip) takes:
+    M = out and N = in multiples of 256, K = tokens a multiple of 32, bf16, unit inner stride."""
+    if not (g.is_cuda and g.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
+        return False
+    from llmctl.ops._lib import use_native
+
+    if not use_native(g):
+        return False
+    M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
+    if M % 256 or N % 256 or K % 32 or K == 0:
+        return False
+    for t in (g, dy2, x2):
+        if t.stride(1) != 1 or t.stride(0) % 8 or t.data_ptr() % 16:
+            return False
+    # 32-bit buffer offsets inside the kernel
+    return dy2.stride(0) * K * 2 < 2**31 and x2.stride(0) * K * 2 < 2**31
+
+
+def wgrad_into(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> None:
+    """``g (+)= dy2^T @ x2``: the MFMA kernel reads both K-major operands through
+    ds_read_b64_tr_b16 (+12-26 % over hipBLASLt on the GPT-7B shapes, profiles/gemm_bench_r1.json);
+    other shapes go to hipBLASLt."""
+    if _gemm_ex_ok(g, dy2, x2):
+        from llmctl.ops._lib import native
+
+        native().gemm_ex(dy2, x2, g, True, True, accumulate)
+    elif accumulate:
+        g.addmm_(dy2.t(), x2)
+    else:
+        torch.mm(dy2.t(), x2, out=g)
+
+
 class GradSink:
     def __init__(self):
         self.callbacks: List[Callable[[torch.nn.Parameter], None]] = []
@@ -34,11 +67,8 @@ class GradSink:
         g = p.grad
         if g is None:
             raise RuntimeError("grad sink parameter has no flat .grad view")
-        if p._llmctl_fresh:
-            torch.mm(dy2.t(), x2, out=g)
-            p._llmctl_fresh = False
-        else:
-            g.addmm_(dy2.t(), x2)
+        wgrad_into(g, dy2, x2, accumulate=not p._llmctl_fresh)
+        p._llmctl_fresh = False
         for cb in self.callbacks:
             cb(p)
 

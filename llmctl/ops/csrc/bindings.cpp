@@ -32,5 +32,6 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor uniform) -> Tensor");
   // benchmarks / tuning (gemm_bf16.hip, hbm_stream.hip)
   m.def("gemm_bf16(Tensor a, Tensor b) -> Tensor");
+  m.def("gemm_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int variant=-1) -> ()");
   m.def("hbm_copy(Tensor src, Tensor(a!) dst) -> ()");
 }

@@ -245,10 +245,41 @@ def test_sampling(native_lib):
 
 
 def test_gemm_and_copy(native_lib):
-    a, b = _bf(256, 512, seed=61), _bf(384, 512, seed=62)
+    a, b = _bf(256, 512, seed=61), _bf(512, 512, seed=62)
     c = native_lib.gemm_bf16(a, b)
     assert _rel(c, a.float() @ b.float().t()) < 1e-2
     src = _bf(1 << 16, seed=63)
     dst = torch.empty_like(src)
     native_lib.hbm_copy(src, dst)
     assert torch.equal(src, dst)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (768, 512, 1024), (2304, 1280, 192)])
+@pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_gemm_ex(native_lib, M, N, K, at, bt, acc):
+    """C (+)= A(m,k) B(n,k) for every operand storage order (fwd / dgrad / wgrad layouts)."""
+    A = _bf(M, K, seed=71)
+    B = _bf(N, K, seed=72)
+    a = A.t().contiguous() if at else A
+    b = B.t().contiguous() if bt else B
+    c0 = _bf(M, N, seed=73)
+    out = c0.clone() if acc else torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    native_lib.gemm_ex(a, b, out, at, bt, acc)
+    want = A.float() @ B.float().t() + (c0.float() if acc else 0.0)
+    assert torch.isfinite(out.float()).all()
+    assert _rel(out, want) < 8e-3
+
+
+def test_gemm_ex_strided_views(native_lib):
+    """Row-strided operand / output views (flat-buffer gradient views, column slices)."""
+    big = _bf(1024, 640, seed=81)
+    a = big[:, 64:576]          # [1024, 512] with row stride 640
+    b = _bf(1024, 512, seed=82)  # K-major B: [K=1024][N=512]
+    out_buf = torch.zeros(512, 768, device=DEV, dtype=torch.bfloat16)
+    out = out_buf[:, 256:768]    # [512, 512] with row stride 768
+    # A K-major: A(m,k) = a[k][m] -> M = 512, K = 1024
+    native_lib.gemm_ex(a, b, out, True, True, False)
+    want = a.float().t() @ b.float()
+    assert _rel(out, want) < 8e-3
+    assert (out_buf[:, :256] == 0).all()
