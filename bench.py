@@ -25,7 +25,7 @@ import time
 
 # Measured reference-equivalent stack on one MI355X (HF LlamaForCausalLM eager + torch
 # AdamW, same GPT-7B config/seq/bf16) — see BASELINE.md §3.  None until measured.
-REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU = 14732.2  # gpurun_out 2026-10-15: HF+SDPA, mb=4
+REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU = 17348.3  # best of mb 4/8/12/16 (mb=16), profiles/reference_stack_hf_sdpa_mb_sweep.jsonl
 
 
 def parse():
@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt-7b")
     ap.add_argument("--seq-len", type=int, default=2048)
-    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("LLMCTL_BENCH_MB", "8")))
+    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("LLMCTL_BENCH_MB", "12")))
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
@@ -131,6 +131,7 @@ def main():
                    "parallelism": par, "micro_batch": args.micro_batch, "grad_accum": accum,
                    "activation_checkpoint": args.activation_checkpoint},
         "mfu": round(mfu, 4) if mfu is not None else None,
+        "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
         "final_loss": round(loss, 4),
     }
     if eng.is_main:

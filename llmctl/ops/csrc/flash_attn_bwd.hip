@@ -83,20 +83,19 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
   constexpr int KV_ITERS = KBLK * CPR / 256;  // 8 for HD=128
   constexpr int Q_ITERS = QT * CPR / 256;     // 2 for HD=128
   constexpr int DST_ROWB = QT * 2;            // dS^T rows: 32 q * 2 B = 64 B
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * KBLK * ROWB + 2 * QT * ROWB + KBLK * DST_ROWB +
-                                                             2 * QT * 4];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * KBLK * ROWB + 4 * QT * ROWB + KBLK * DST_ROWB +
+                                                             4 * QT * 4];
   unsigned char* Ks = smem;
   unsigned char* Vs = Ks + KBLK * ROWB;
-  unsigned char* Qs = Vs + KBLK * ROWB;
-  unsigned char* Ds = Qs + QT * ROWB;  // dO
-  unsigned char* St = Ds + QT * ROWB;  // dS^T [key][q]
-  float* lse_s = reinterpret_cast<float*>(St + KBLK * DST_ROWB);
-  float* del_s = lse_s + QT;
+  unsigned char* Qbuf = Vs + KBLK * ROWB;       // [2][QT][HD] double-buffered Q tiles
+  unsigned char* Dbuf = Qbuf + 2 * QT * ROWB;   // [2][QT][HD] double-buffered dO tiles
+  unsigned char* St = Dbuf + 2 * QT * ROWB;     // dS^T [key][q]
+  float* lse_buf = reinterpret_cast<float*>(St + KBLK * DST_ROWB);  // [2][QT]
+  float* del_buf = lse_buf + 2 * QT;                                 // [2][QT]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int nkb = (a.S + KBLK - 1) / KBLK;
   const int BH = a.B * a.Hkv;
   const int bh = blockIdx.x % BH;
   const int kblk = blockIdx.x / BH;  // small kblk = most query tiles under causal: dispatched first
@@ -130,129 +129,169 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[d][i] = dv[d][i] = 0.f;
 
+  // flattened (q-head of the GQA group, query tile) sequence; the next tile's Q / dO / lse /
+  // delta are prefetched into registers while the current one is computed (register staging,
+  // guide T14) and written to the other LDS buffer after it
   const int q_start = CAUSAL ? (k0 / QT) * QT : 0;
-  for (int g = 0; g < group; ++g) {
+  const int nq = (a.S - q_start + QT - 1) / QT;
+  const int ntiles = group * nq;
+  uint4 pq[Q_ITERS], pd[Q_ITERS];
+  float pl = 0.f, pdl = 0.f;
+  auto fetch = [&](int t) {
+    const int g = t / nq;
+    const int q0 = q_start + (t - g * nq) * QT;
     const int hq = hk * group + g;
     const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh;
     const unsigned short* Dp = a.dout + b * a.do_sb + hq * a.do_sh;
-    const float* lse_p = a.lse + ((long)b * a.Hq + hq) * a.S;
-    const float* del_p = a.delta + ((long)b * a.Hq + hq) * a.S;
-    float* dq_p = a.dq_acc + (long)b * a.S * a.Hq * HD + (long)hq * HD;
-    for (int q0 = q_start; q0 < a.S; q0 += QT) {
-      __syncthreads();  // previous iteration's readers of Qs/Ds/St are done
 #pragma unroll
-      for (int it = 0; it < Q_ITERS; ++it) {
-        const int c = tid + 256 * it;
-        const int row = c / CPR, ch = c % CPR;
-        const int qq = q0 + row;
-        uint4 qv = make_uint4(0, 0, 0, 0), dv4 = make_uint4(0, 0, 0, 0);
-        if (qq < a.S) {
-          qv = gload16(Qp + (long)qq * a.q_ss + ch * 8);
-          dv4 = gload16(Dp + (long)qq * a.do_ss + ch * 8);
-        }
-        *reinterpret_cast<uint4*>(Qs + tr_off<HD>(row, ch)) = qv;
-        *reinterpret_cast<uint4*>(Ds + tr_off<HD>(row, ch)) = dv4;
+    for (int it = 0; it < Q_ITERS; ++it) {
+      const int c = tid + 256 * it;
+      const int row = c / CPR, ch = c % CPR;
+      const int qq = q0 + row;
+      pq[it] = make_uint4(0, 0, 0, 0);
+      pd[it] = make_uint4(0, 0, 0, 0);
+      if (qq < a.S) {
+        pq[it] = gload16(Qp + (long)qq * a.q_ss + ch * 8);
+        pd[it] = gload16(Dp + (long)qq * a.do_ss + ch * 8);
       }
-      if (tid < QT) {
-        const int qq = q0 + tid;
-        lse_s[tid] = qq < a.S ? lse_p[qq] * 1.4426950408889634f : 0.f;
-        del_s[tid] = qq < a.S ? del_p[qq] : 0.f;
-      }
-      __syncthreads();
+    }
+    if (tid < QT) {
+      const int qq = q0 + tid;
+      const long base = ((long)b * a.Hq + hq) * a.S;
+      pl = qq < a.S ? a.lse[base + qq] * 1.4426950408889634f : 0.f;
+      pdl = qq < a.S ? a.delta[base + qq] : 0.f;
+    }
+  };
+  auto commit = [&](int buf) {
+    unsigned char* Qs = Qbuf + buf * QT * ROWB;
+    unsigned char* Ds = Dbuf + buf * QT * ROWB;
+#pragma unroll
+    for (int it = 0; it < Q_ITERS; ++it) {
+      const int c = tid + 256 * it;
+      const int row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<uint4*>(Qs + tr_off<HD>(row, ch)) = pq[it];
+      *reinterpret_cast<uint4*>(Ds + tr_off<HD>(row, ch)) = pd[it];
+    }
+    if (tid < QT) {
+      lse_buf[buf * QT + tid] = pl;
+      del_buf[buf * QT + tid] = pdl;
+    }
+  };
+  if (ntiles > 0) {
+    fetch(0);
+    commit(0);
+  }
+  __syncthreads();
 
-      const bool active = !(CAUSAL && wkey0 > q0 + QT - 1) && wkey0 < a.S;
-      float pbuf[16], dsbuf[16];
-      if (active) {
-        // ---- S = Q K^T and dP = dO V^T   (q on regs, key on lane)
-        f32x16 s, dp;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const int g = t / nq;
+    const int q0 = q_start + (t - g * nq) * QT;
+    const int hq = hk * group + g;
+    float* dq_p = a.dq_acc + (long)b * a.S * a.Hq * HD + (long)hq * HD;
+    const unsigned char* Qs = Qbuf + buf * QT * ROWB;
+    const unsigned char* Ds = Dbuf + buf * QT * ROWB;
+    const float* lse_s = lse_buf + buf * QT;
+    const float* del_s = del_buf + buf * QT;
+    if (t + 1 < ntiles) fetch(t + 1);  // in flight during this tile's MFMAs
+
+    const bool active = !(CAUSAL && wkey0 > q0 + QT - 1) && wkey0 < a.S;
+    float pbuf[16], dsbuf[16];
+    if (active) {
+      // ---- S = Q K^T and dP = dO V^T   (q on regs, key on lane)
+      f32x16 s, dp;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
+      for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8_t qa = lds_read_b128(Qs, tr_off<HD>(r, 2 * ks + hh));
-          const bf16x8_t kb = lds_read_b128(Ks, tr_off<HD>(wave * 32 + r, 2 * ks + hh));
-          s = mfma32(qa, kb, s);
-          const bf16x8_t da = lds_read_b128(Ds, tr_off<HD>(r, 2 * ks + hh));
-          const bf16x8_t vb = lds_read_b128(Vs, tr_off<HD>(wave * 32 + r, 2 * ks + hh));
-          dp = mfma32(da, vb, dp);
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8_t qa = lds_read_b128(Qs, tr_off<HD>(r, 2 * ks + hh));
+        const bf16x8_t kb = lds_read_b128(Ks, tr_off<HD>(wave * 32 + r, 2 * ks + hh));
+        s = mfma32(qa, kb, s);
+        const bf16x8_t da = lds_read_b128(Ds, tr_off<HD>(r, 2 * ks + hh));
+        const bf16x8_t vb = lds_read_b128(Vs, tr_off<HD>(wave * 32 + r, 2 * ks + hh));
+        dp = mfma32(da, vb, dp);
+      }
+      const bool need_mask = (CAUSAL && wkey0 + 31 > q0) || (q0 + QT > a.S) || (wkey0 + 32 > a.S);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = acc_row(i, hh);
+        float p = fast_exp2(s[i] * a.scale_log2 - lse_s[qi]);
+        if (need_mask) {
+          const int qq = q0 + qi;
+          if ((CAUSAL && my_key > qq) || qq >= a.S || my_key >= a.S) p = 0.f;
         }
-        const bool need_mask = (CAUSAL && wkey0 + 31 > q0) || (q0 + QT > a.S) || (wkey0 + 32 > a.S);
+        pbuf[i] = p;
+        dsbuf[i] = p * (dp[i] - del_s[qi]) * a.scale;
+      }
+      // ---- dV^T += dO^T P ; dK^T += Q^T dS
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8_t pb = to_bf16x8(pbuf + 8 * st);
+        const bf16x8_t sb = to_bf16x8(dsbuf + 8 * st);
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) {
+          const bf16x8_t da = tr_frag<HD>(Ds, 16 * st, d * 32, lane);
+          dv[d] = mfma32(da, pb, dv[d]);
+          const bf16x8_t qa = tr_frag<HD>(Qs, 16 * st, d * 32, lane);
+          dk[d] = mfma32(qa, sb, dk[d]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dsbuf[i] = 0.f;
+    }
+    // ---- dS^T -> LDS [key][q] (64-B rows): lane = key, 4 groups of 4 contiguous q
+    {
+      unsigned char* rowp = St + (wave * 32 + r) * DST_ROWB;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int qc = 8 * gq + 4 * hh;
+        unsigned short w4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w4[j] = f2bf(dsbuf[4 * gq + j]);
+        *reinterpret_cast<uint2*>(rowp + qc * 2) =
+            make_uint2((unsigned)w4[0] | ((unsigned)w4[1] << 16), (unsigned)w4[2] | ((unsigned)w4[3] << 16));
+      }
+    }
+    __syncthreads();
+    // ---- dQ[q][d] += dS K over this block's 128 keys; waves split the d-blocks
+    {
+      constexpr int WPD = 4 / NDB;  // waves per d-block (1 for HD=128, 2 for HD=64)
+      const int d = wave / WPD;
+      const int kpart = wave % WPD;
+      constexpr int KSTEPS = KBLK / 16 / WPD;
+      // skip if every key of this block is above this q tile's diagonal (all dS zero)
+      if (!(CAUSAL && k0 > q0 + QT - 1)) {
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks) {
+          const int key0 = (kpart * KSTEPS + ks) * 16;
+          // A = dS[q][key]: from dS^T image X[key][q] (64-B rows, plain layout)
+          const int i16 = lane & 15, qq4 = i16 >> 2, p = i16 & 3;
+          const int col = 16 * ((lane >> 4) & 1) + 4 * p;  // q column
+          const int r1 = key0 + 8 * hh + qq4;
+          s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(St + r1 * DST_ROWB + col * 2));
+          s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(St + (r1 + 4) * DST_ROWB + col * 2));
+          s8_t av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8_t af = __builtin_bit_cast(bf16x8_t, av);
+          // B = K[key][d] with d on the lane
+          const bf16x8_t bf = tr_frag_nat<HD>(Ks, key0, d * 32, lane);
+          acc = mfma32(af, bf, acc);
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int qi = acc_row(i, hh);
-          float p = fast_exp2(s[i] * a.scale_log2 - lse_s[qi]);
-          if (need_mask) {
-            const int qq = q0 + qi;
-            if ((CAUSAL && my_key > qq) || qq >= a.S || my_key >= a.S) p = 0.f;
-          }
-          pbuf[i] = p;
-          dsbuf[i] = p * (dp[i] - del_s[qi]) * a.scale;
-        }
-        // ---- dV^T += dO^T P ; dK^T += Q^T dS
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8_t pb = to_bf16x8(pbuf + 8 * st);
-          const bf16x8_t sb = to_bf16x8(dsbuf + 8 * st);
-#pragma unroll
-          for (int d = 0; d < NDB; ++d) {
-            const bf16x8_t da = tr_frag<HD>(Ds, 16 * st, d * 32, lane);
-            dv[d] = mfma32(da, pb, dv[d]);
-            const bf16x8_t qa = tr_frag<HD>(Qs, 16 * st, d * 32, lane);
-            dk[d] = mfma32(qa, sb, dk[d]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dsbuf[i] = 0.f;
-      }
-      // ---- dS^T -> LDS [key][q] (64-B rows): lane = key, 4 groups of 4 contiguous q
-      {
-        unsigned char* rowp = St + (wave * 32 + r) * DST_ROWB;
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int qc = 8 * gq + 4 * hh;
-          unsigned short w4[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) w4[j] = f2bf(dsbuf[4 * gq + j]);
-          *reinterpret_cast<uint2*>(rowp + qc * 2) =
-              make_uint2((unsigned)w4[0] | ((unsigned)w4[1] << 16), (unsigned)w4[2] | ((unsigned)w4[3] << 16));
-        }
-      }
-      __syncthreads();
-      // ---- dQ[q][d] += dS K over this block's 128 keys; waves split the d-blocks
-      {
-        constexpr int WPD = 4 / NDB;  // waves per d-block (1 for HD=128, 2 for HD=64)
-        const int d = wave / WPD;
-        const int kpart = wave % WPD;
-        constexpr int KSTEPS = KBLK / 16 / WPD;
-        // skip if every key of this block is above this q tile's diagonal (all dS zero)
-        if (!(CAUSAL && k0 > q0 + QT - 1)) {
-          f32x16 acc;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-          for (int ks = 0; ks < KSTEPS; ++ks) {
-            const int key0 = (kpart * KSTEPS + ks) * 16;
-            // A = dS[q][key]: from dS^T image X[key][q] (64-B rows, plain layout)
-            const int i16 = lane & 15, qq4 = i16 >> 2, p = i16 & 3;
-            const int col = 16 * ((lane >> 4) & 1) + 4 * p;  // q column
-            const int r1 = key0 + 8 * hh + qq4;
-            s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(St + r1 * DST_ROWB + col * 2));
-            s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(St + (r1 + 4) * DST_ROWB + col * 2));
-            s8_t av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            const bf16x8_t af = __builtin_bit_cast(bf16x8_t, av);
-            // B = K[key][d] with d on the lane
-            const bf16x8_t bf = tr_frag_nat<HD>(Ks, key0, d * 32, lane);
-            acc = mfma32(af, bf, acc);
-          }
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int qq = q0 + acc_row(i, hh);
-            if (qq < a.S) atomicAdd(dq_p + (long)qq * a.Hq * HD + d * 32 + r, acc[i]);
-          }
+          const int qq = q0 + acc_row(i, hh);
+          if (qq < a.S) atomicAdd(dq_p + (long)qq * a.Hq * HD + d * 32 + r, acc[i]);
         }
       }
     }
+    // next tile's Q / dO into the other buffer (last read during tile t-1, before this
+    // tile's first barrier); the barrier also orders this tile's St reads before the next
+    // tile's St writes
+    if (t + 1 < ntiles) commit(buf ^ 1);
+    __syncthreads();
   }
   // ---- write dK, dV (bf16) for this wave's keys: lane = key, regs = d
   if (my_key < a.S) {

@@ -17,6 +17,9 @@ ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--warmup", type=int, default=2)
 ap.add_argument("--attn", default="sdpa", help="sdpa | eager")
 ap.add_argument("--layers", type=int, default=32)
+ap.add_argument("--prefill", action="store_true",
+                help="serving TTFT as the reference server computes it: one fp16 full-prompt forward "
+                     "(server.py:199-206) for a [1, seq_len] prompt, p50 over 10 runs")
 a = ap.parse_args()
 
 from transformers import LlamaConfig, LlamaForCausalLM
@@ -25,6 +28,24 @@ cfg = LlamaConfig(vocab_size=32000, hidden_size=4096, intermediate_size=11008, n
                   num_attention_heads=32, num_key_value_heads=32, max_position_embeddings=4096,
                   rms_norm_eps=1e-5, tie_word_embeddings=False, attn_implementation=a.attn)
 torch.manual_seed(0)
+if a.prefill:
+    with torch.device("cuda"):
+        model = LlamaForCausalLM(cfg).to(torch.float16)  # reference loads fp16 (server.py:146-170)
+    model.eval()
+    ids = torch.randint(0, 32000, (1, a.seq_len), device="cuda")
+    ts = []
+    with torch.no_grad():
+        for i in range(12):
+            torch.cuda.synchronize(); t0 = time.perf_counter()
+            out = model(input_ids=ids, use_cache=True)
+            nxt = out.logits[:, -1].argmax(-1).item()
+            ts.append(time.perf_counter() - t0)
+    ts = sorted(ts[2:])
+    print(json.dumps({"stack": "hf-transformers-fp16-prefill", "attn": a.attn, "prompt_length": a.seq_len,
+                      "ttft_forward_p50_ms": round(1000 * ts[len(ts) // 2], 2),
+                      "ttft_forward_min_ms": round(1000 * ts[0], 2),
+                      "note": "reference server adds up to 10 ms of polling (server.py:345-347) on top"}), flush=True)
+    raise SystemExit(0)
 with torch.device("cuda"):
     model = LlamaForCausalLM(cfg).to(torch.bfloat16)
 model.train()
