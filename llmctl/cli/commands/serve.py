@@ -46,6 +46,21 @@ def start(
     console.print(f"[yellow]Artifact: {artifact}[/yellow]  [yellow]Endpoint: http://{host}:{port}[/yellow]")
     console.print(f"[yellow]Scheduler: {scheduler}, max batch {max_batch_size}, max tokens {max_batch_tokens}, "
                   f"max concurrent {max_concurrent}, device {device}[/yellow]")
+    if tensor_parallel > 1:
+        # one process per GPU: torchrun -> llmctl.serve.tp (rank 0 serves HTTP, the rest run
+        # the TP worker loop); started as a child process, never exec'd
+        import os
+        import subprocess
+        import sys
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={tensor_parallel}",
+               "--master-addr=127.0.0.1", f"--master-port={os.environ.get('MASTER_PORT', '29512')}",
+               "-m", "llmctl.serve.tp", "--artifact", artifact, "--host", host, "--port", str(port),
+               "--max-batch-size", str(max_batch_size), "--max-batch-tokens", str(max_batch_tokens),
+               "--max-concurrent", str(max_concurrent), "--kv-cache-fraction", str(kv_cache_fraction),
+               "--block-size", str(block_size), "--scheduler", scheduler] + ([] if cuda_graphs else ["--no-graphs"])
+        console.print(f"[yellow]Tensor parallel: {tensor_parallel} ranks (RCCL)[/yellow]")
+        raise typer.Exit(subprocess.call(cmd))
     server = create_inference_server(model_path=artifact, host=host, port=port, max_batch_size=max_batch_size,
                                      max_batch_tokens=max_batch_tokens, max_concurrent=max_concurrent,
                                      scheduler=scheduler, device=device, kv_cache_fraction=kv_cache_fraction,

@@ -44,7 +44,7 @@ class InferenceEngine:
     def __init__(self, model_path: str = "tiny", device: str = "auto", dtype=torch.bfloat16, max_batch_size: int = 8,
                  max_batch_tokens: int = 8192, max_model_len: Optional[int] = None, kv_cache_fraction: float = 0.85,
                  block_size: int = 16, num_kv_blocks: Optional[int] = None, scheduler: str = "dynamic",
-                 use_graphs: bool = True, seed: int = 0):
+                 use_graphs: bool = True, seed: int = 0, pc=None):
         if device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -55,7 +55,9 @@ class InferenceEngine:
         self.dtype = dtype
         self.model_path = model_path
         self.model: DecoderLM
-        self.model, self.cfg, self.ckpt = load_model(model_path, device=self.device, dtype=dtype, seed=seed)
+        self.pc = pc
+        self.tp = pc.tp_size if pc is not None else 1
+        self.model, self.cfg, self.ckpt = self._load(model_path, dtype, seed)
         self.model.eval()
         self.tokenizer = load_tokenizer(str(self.ckpt) if self.ckpt else None)
         cfg = self.cfg
@@ -69,11 +71,13 @@ class InferenceEngine:
                 budget = free * kv_cache_fraction
             else:
                 budget = 256 * 2 ** 20
-            num_kv_blocks = PagedKVCache.blocks_for_memory(budget, cfg.layers, block_size, cfg.kv_heads, cfg.head_dim,
-                                                           torch.tensor([], dtype=dtype).element_size())
+            num_kv_blocks = PagedKVCache.blocks_for_memory(budget, cfg.layers, block_size, cfg.kv_heads // self.tp,
+                                                           cfg.head_dim, torch.tensor([], dtype=dtype).element_size())
             num_kv_blocks = min(num_kv_blocks, 1 << 20)
-        self.kv_cache = PagedKVCache(cfg.layers, num_kv_blocks, block_size, cfg.kv_heads, cfg.head_dim, dtype,
-                                     self.device)
+            num_kv_blocks = self._agree_min(num_kv_blocks)
+        # each TP rank caches only its own KV heads
+        self.kv_cache = PagedKVCache(cfg.layers, num_kv_blocks, block_size, cfg.kv_heads // self.tp, cfg.head_dim,
+                                     dtype, self.device)
         self.kv = make_kv_manager(num_kv_blocks, block_size)
         self.scheduler = ContinuousBatchScheduler(self.kv, max_batch_size, max_batch_tokens, self.max_model_len,
                                                   scheduler, block_size)
@@ -87,10 +91,29 @@ class InferenceEngine:
         log.info("engine: %s on %s, %d KV blocks x %d tokens (%.1f GB)", cfg.name, self.device, num_kv_blocks,
                  block_size, self.kv_cache.nbytes / 1e9)
 
+    # ------------------------------------------------------------------ TP hooks (identity at tp=1)
+    def _load(self, model_path: str, dtype, seed: int):
+        return load_model(model_path, device=self.device, dtype=dtype, seed=seed)
+
+    def _agree_min(self, n: int) -> int:
+        return n
+
+    def _reduce(self, x: torch.Tensor) -> torch.Tensor:
+        return x
+
+    def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
+        return logits
+
     # ------------------------------------------------------------------ model pieces
     def _embed(self, ids: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
         m = self.model
-        x = F.embedding(ids, m.embed)
+        if self.tp > 1:  # vocab-parallel table: local rows + all-reduce
+            local = ids - m.vocab_start
+            ok = (local >= 0) & (local < m.embed.shape[0])
+            x = F.embedding(local.clamp(0, m.embed.shape[0] - 1), m.embed) * ok.unsqueeze(-1).to(m.embed.dtype)
+            x = self._reduce(x)
+        else:
+            x = F.embedding(ids, m.embed)
         if m.pos_embed is not None:
             x = x + m.pos_embed[positions]
         return x
@@ -117,6 +140,7 @@ class InferenceEngine:
             out = F.linear(ops.swiglu(F.linear(xn, layer.w_up, layer.b_up)), layer.w_down)
         else:
             out = F.linear(ops.gelu(F.linear(xn, layer.w_up, layer.b_up)), layer.w_down)
+        out = self._reduce(out)  # row-parallel down projection
         if layer.b_down is not None:
             out = out + layer.b_down
         return out
@@ -128,21 +152,32 @@ class InferenceEngine:
             xn, _ = ops.add_layernorm(x, res, m.final_norm_w, m.final_norm_b, eps)
         else:
             xn, _ = ops.add_rmsnorm(x, res, m.final_norm_w, eps)
-        return F.linear(xn, m.head_weight())
+        return self._gather_vocab(F.linear(xn, m.head_weight()))
 
     # ------------------------------------------------------------------ prefill
+    def prefill_plan(self, seqs: List[Sequence]) -> Dict:
+        """Host-side description of a prefill step (what TP ranks receive from rank 0)."""
+        lens = [s.num_tokens for s in seqs]
+        B, S = len(seqs), max(lens)
+        ids = np.zeros((B, S), dtype=np.int64)
+        slots = np.full((B, S), -1, dtype=np.int64)
+        for i, s in enumerate(seqs):
+            toks = s.all_ids
+            ids[i, :len(toks)] = toks
+            slots[i, :len(toks)] = np.asarray(self.kv.slots(s.seq_id, 0, len(toks)), dtype=np.int64)
+        return {"op": "prefill", "ids": ids, "slots": slots, "lens": lens}
+
     @torch.inference_mode()
     def prefill(self, seqs: List[Sequence]) -> torch.Tensor:
         """Run the prompts (all known tokens) of ``seqs``; returns last-position logits [n, V]."""
-        lens = [s.num_tokens for s in seqs]
-        B, S = len(seqs), max(lens)
-        ids = torch.zeros(B, S, dtype=torch.long)
-        slots = torch.full((B, S), -1, dtype=torch.long)
-        for i, s in enumerate(seqs):
-            toks = s.all_ids
-            ids[i, :len(toks)] = torch.tensor(toks)
-            slots[i, :len(toks)] = torch.from_numpy(np.asarray(self.kv.slots(s.seq_id, 0, len(toks)), dtype=np.int64))
-        ids = ids.to(self.device, non_blocking=True)
+        return self.prefill_exec(self.prefill_plan(seqs))
+
+    @torch.inference_mode()
+    def prefill_exec(self, plan: Dict) -> torch.Tensor:
+        lens = plan["lens"]
+        B, S = plan["ids"].shape
+        ids = torch.from_numpy(plan["ids"]).to(self.device, non_blocking=True)
+        slots = torch.from_numpy(plan["slots"])
         slots = slots.to(self.device, non_blocking=True).view(-1)
         pos = torch.arange(S, device=self.device).repeat(B)
         x = self._embed(ids.view(-1), pos)
@@ -154,7 +189,7 @@ class InferenceEngine:
             ops.kv_cache_write(k, v, kc[li], vc[li], slots)
             o = ops.flash_attention(q.view(B, S, layer.nq, layer.D), k.view(B, S, layer.nkv, layer.D),
                                     v.view(B, S, layer.nkv, layer.D), causal=True)
-            a = F.linear(o.view(B * S, -1), layer.wo)
+            a = self._reduce(F.linear(o.view(B * S, -1), layer.wo))
             if layer.bo is not None:
                 a = a + layer.bo
             xn, res = self._norm(layer, a, res, "mlp")
@@ -174,7 +209,7 @@ class InferenceEngine:
             q, k, v = self._qkv(layer, xn, positions, self.max_model_len)
             ops.kv_cache_write(k, v, kc[li], vc[li], slots)
             o = ops.paged_attention_decode(q, kc[li], vc[li], block_tables, ctx_lens)
-            a = F.linear(o.view(o.shape[0], -1), layer.wo)
+            a = self._reduce(F.linear(o.view(o.shape[0], -1), layer.wo))
             if layer.bo is not None:
                 a = a + layer.bo
             xn, res = self._norm(layer, a, res, "mlp")
@@ -210,14 +245,19 @@ class InferenceEngine:
                                                bufs["ctx_lens"])
         self._graphs[nb] = (g, bufs)
 
+    def decode_plan(self, seqs: List[Sequence]) -> Dict:
+        return {"op": "decode", "ids": [s.all_ids[-1] for s in seqs], "positions": [s.num_tokens - 1 for s in seqs],
+                "slots": [s._decode_slot for s in seqs], "ctx": [self.kv.num_tokens(s.seq_id) for s in seqs],
+                "bt": np.asarray(self.kv.block_tables([s.seq_id for s in seqs], self.max_blocks_per_seq))}
+
     @torch.inference_mode()
     def decode(self, seqs: List[Sequence]) -> torch.Tensor:
-        n = len(seqs)
-        ids = [s.all_ids[-1] for s in seqs]
-        positions = [s.num_tokens - 1 for s in seqs]
-        slots = [s._decode_slot for s in seqs]
-        ctx = [self.kv.num_tokens(s.seq_id) for s in seqs]
-        bt = np.asarray(self.kv.block_tables([s.seq_id for s in seqs], self.max_blocks_per_seq))
+        return self.decode_exec(self.decode_plan(seqs))
+
+    @torch.inference_mode()
+    def decode_exec(self, plan: Dict) -> torch.Tensor:
+        ids, positions, slots, ctx, bt = plan["ids"], plan["positions"], plan["slots"], plan["ctx"], plan["bt"]
+        n = len(ids)
         self.stats["decode_tokens"] += n
         if self.use_graphs:
             nb = self._bucket(n)

@@ -63,8 +63,9 @@ class InferenceServer:
         self.engine_kwargs = dict(model_path=model_path, device=device, max_batch_size=max_batch_size,
                                   max_batch_tokens=max_batch_tokens, kv_cache_fraction=kv_cache_fraction,
                                   block_size=block_size, scheduler=scheduler, use_graphs=use_graphs)
-        if tensor_parallel != 1:
-            raise NotImplementedError("TP serving runs one engine per rank under torchrun (llmctl.serve.tp)")
+        if tensor_parallel != 1 and engine is None:
+            raise ValueError("TP serving runs one engine per rank under torchrun: use llmctl.serve.tp "
+                             "(`llmctl serve start --tensor-parallel N` launches it)")
         self.engine = engine
         self.active_requests: Dict[str, Any] = {}
         self._lock = threading.Lock()

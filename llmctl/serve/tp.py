@@ -1,0 +1,172 @@
+"""Tensor-parallel serving: one process per GPU, Megatron TP over RCCL (BASELINE config
+"``llmctl serve`` GPT-7B paged-attention + dynamic batching, TP=8").
+
+The reference serves from one process with an HF model (``server.py:127-251``) and has no
+model parallelism.  Here every rank holds a TP shard of the weights:
+  * column-parallel QKV / gate-up, row-parallel o-proj / down-proj (one all-reduce each),
+  * a vocab-parallel embedding (all-reduce) and LM head (all-gather of the logits),
+  * its own paged KV cache for its ``kv_heads / tp`` heads (the block tables are shared).
+
+Control plane: rank 0 owns the scheduler, the KV block manager, sampling and (for ``llmctl
+serve``) the HTTP server.  For every engine step it broadcasts a small host-side *plan*
+(token ids, positions, KV slots, block tables) over a gloo group; all ranks then execute the
+same step, so every rank posts the identical RCCL sequence.  Ranks != 0 run
+:meth:`TPInferenceEngine.worker_loop` until rank 0 broadcasts ``stop``.
+
+Decode-step hipGraph capture stays on for TP (the collectives are captured with the
+rest) unless ``LLMCTL_TP_GRAPHS=0``.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from llmctl.models import ParallelContext
+from llmctl.utils.env import dist_env
+
+from .engine import InferenceEngine
+from .scheduler import Sequence
+
+log = logging.getLogger("llmctl.serve.tp")
+
+
+class TPInferenceEngine(InferenceEngine):
+    def __init__(self, model_path: str = "tiny", tp_group=None, control_group=None, **kw):
+        if not dist.is_initialized():
+            raise RuntimeError("TPInferenceEngine needs torch.distributed (launch with torchrun)")
+        self.tp_group = tp_group
+        self.tp_size = dist.get_world_size(tp_group)
+        self.tp_rank = dist.get_rank(tp_group)
+        self.control = control_group if control_group is not None else dist.new_group(backend="gloo")
+        pc = ParallelContext(tp_group=tp_group, tp_size=self.tp_size, tp_rank=self.tp_rank)
+        if kw.get("use_graphs", True) and os.environ.get("LLMCTL_TP_GRAPHS", "1") == "0":
+            kw["use_graphs"] = False
+        super().__init__(model_path, pc=pc, **kw)
+
+    # ------------------------------------------------------------------ TP hooks
+    def _load(self, model_path: str, dtype, seed: int):
+        """Checkpoints are resharded by ``load_model``; random-init templates are built whole
+        (same seed on every rank) and sliced, so TP=N serves exactly the TP=1 model."""
+        from llmctl.io.artifact import load_model, resolve_checkpoint_dir
+        from llmctl.io.checkpoint import _global_name, shard_tp
+        from llmctl.models import build_model, get_model_config
+
+        if resolve_checkpoint_dir(model_path) is not None:
+            return load_model(model_path, device=self.device, dtype=dtype, pc=self.pc, seed=seed)
+        cfg = get_model_config(model_path)
+        full = build_model(cfg, device=self.device, dtype=dtype, seed=seed)
+        model = build_model(cfg, device=self.device, dtype=dtype, pc=self.pc, seed=seed)
+        src = dict(full.named_parameters())
+        with torch.no_grad():
+            for n, p in model.named_parameters():
+                g = _global_name(n, 0)
+                p.copy_(shard_tp(g, src[n].detach(), self.tp_size, self.tp_rank, cfg))
+        del full, src
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        return model, cfg, None
+
+    def _agree_min(self, n: int) -> int:
+        t = torch.tensor([n], dtype=torch.long)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.control)
+        return int(t.item())
+
+    def _reduce(self, x: torch.Tensor) -> torch.Tensor:
+        dist.all_reduce(x, group=self.tp_group)
+        return x
+
+    def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
+        n, vl = logits.shape
+        out = torch.empty(self.tp_size * n, vl, dtype=logits.dtype, device=logits.device)
+        dist.all_gather_into_tensor(out, logits.contiguous(), group=self.tp_group)
+        return out.view(self.tp_size, n, vl).permute(1, 0, 2).reshape(n, self.tp_size * vl)
+
+    # ------------------------------------------------------------------ control plane
+    def _bcast(self, plan: Optional[Dict]) -> Dict:
+        box = [plan]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(self.control, 0), group=self.control)
+        return box[0]
+
+    @torch.inference_mode()
+    def prefill(self, seqs: List[Sequence]) -> torch.Tensor:
+        return self.prefill_exec(self._bcast(self.prefill_plan(seqs)))
+
+    @torch.inference_mode()
+    def decode(self, seqs: List[Sequence]) -> torch.Tensor:
+        return self.decode_exec(self._bcast(self.decode_plan(seqs)))
+
+    def stop_workers(self) -> None:
+        if self.tp_rank == 0:
+            self._bcast({"op": "stop"})
+
+    @torch.inference_mode()
+    def worker_loop(self) -> None:
+        """Ranks != 0: execute rank 0's plans until it broadcasts ``stop``."""
+        while True:
+            plan = self._bcast(None)
+            op = plan["op"]
+            if op == "stop":
+                return
+            if op == "prefill":
+                self.prefill_exec(plan)
+            elif op == "decode":
+                self.decode_exec(plan)
+            else:
+                raise RuntimeError(f"unknown TP plan op {op!r}")
+
+
+def init_tp(backend: str = "auto"):
+    """Initialise the default process group from torchrun's env; returns (tp_group, device)."""
+    env = dist_env()
+    if not dist.is_initialized():
+        if backend == "auto":
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(env.local_rank)
+        dist.init_process_group(backend=backend)
+    dev = f"cuda:{env.local_rank}" if torch.cuda.is_available() else "cpu"
+    return None, dev  # the whole world is one TP group (one node, TP <= 8)
+
+
+def main(argv=None) -> int:
+    """``python -m torch.distributed.run --nproc-per-node N -m llmctl.serve.tp --artifact ...``"""
+    import argparse
+
+    ap = argparse.ArgumentParser("llmctl.serve.tp")
+    ap.add_argument("--artifact", default="gpt-7b")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--max-batch-size", type=int, default=8)
+    ap.add_argument("--max-batch-tokens", type=int, default=8192)
+    ap.add_argument("--max-concurrent", type=int, default=128)
+    ap.add_argument("--kv-cache-fraction", type=float, default=0.85)
+    ap.add_argument("--block-size", type=int, default=16)
+    ap.add_argument("--scheduler", default="dynamic")
+    ap.add_argument("--no-graphs", action="store_true")
+    a = ap.parse_args(argv)
+    group, dev = init_tp()
+    eng = TPInferenceEngine(a.artifact, tp_group=group, device=dev, max_batch_size=a.max_batch_size,
+                            max_batch_tokens=a.max_batch_tokens, kv_cache_fraction=a.kv_cache_fraction,
+                            block_size=a.block_size, scheduler=a.scheduler, use_graphs=not a.no_graphs)
+    if eng.tp_rank != 0:
+        eng.worker_loop()
+        dist.destroy_process_group()
+        return 0
+    from .server import InferenceServer
+
+    try:
+        InferenceServer(a.artifact, host=a.host, port=a.port, max_batch_size=a.max_batch_size,
+                        max_batch_tokens=a.max_batch_tokens, max_concurrent=a.max_concurrent, engine=eng).run()
+    finally:
+        eng.stop_workers()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -91,3 +91,37 @@ def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: in
         out = eng.train_step(batches)
         losses.append(float(out["loss"]))  # already the mean over all micro-batches
     return {"losses": losses, "state": eng.gather_full_state_dict()}
+
+
+PROMPTS = [[1, 2, 3, 4, 5], [9] * 13, [7, 7], [3, 1, 4, 1, 5, 9, 2, 6]]
+
+
+def serve_generate(rank: int, world: int, max_tokens: int = 8) -> dict:
+    """Greedy generation through the serving engine: TP=world (TPInferenceEngine) or, with
+    world == 1, the single-process engine.  Rank 0 returns the produced token ids."""
+    import os
+
+    import torch.distributed as dist
+
+    from llmctl.serve.scheduler import SamplingParams
+
+    kw = dict(device="cpu", max_batch_size=4, num_kv_blocks=48, block_size=8, max_model_len=256,
+              max_batch_tokens=512, seed=0)
+    if world == 1:
+        from llmctl.serve.engine import InferenceEngine
+
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            os.environ.pop(k, None)
+        eng = InferenceEngine("tiny", **kw)
+    else:
+        from llmctl.serve.tp import TPInferenceEngine
+
+        dist.init_process_group("gloo")
+        eng = TPInferenceEngine("tiny", **kw)
+        if eng.tp_rank != 0:
+            eng.worker_loop()
+            return {}
+    seqs = eng.generate(PROMPTS, SamplingParams(max_tokens=max_tokens, temperature=0.0))
+    if world > 1:
+        eng.stop_workers()
+    return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": eng.kv_cache.k.shape[-2]}
