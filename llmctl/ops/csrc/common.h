@@ -52,6 +52,15 @@ __device__ __forceinline__ void store8(unsigned short* p, const float* in) {
   *reinterpret_cast<bf16x8*>(p) = v;
 }
 
+// Workgroup barrier ordering LDS only: __syncthreads() is also a release for global memory
+// (s_waitcnt vmcnt(0)), which would drain in-flight prefetch loads and no-return atomics
+// (~3k cycles each under load) at every barrier.  LDS-scoped fences lower to lgkmcnt(0).
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

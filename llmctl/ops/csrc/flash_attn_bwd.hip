@@ -74,7 +74,9 @@ __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restric
   store8(y + i * 8, v);
 }
 
-template <int HD, bool CAUSAL>
+// ABL: timing ablations for tools/attn_bench.py (results wrong): 1 no dQ atomics,
+// 2 no dQ product (and no dS^T exchange), 4 no Q/dO prefetch (tile 0 reused)
+template <int HD, bool CAUSAL, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
   constexpr int NKS = HD / 16;
   constexpr int NDB = HD / 32;
@@ -137,6 +139,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
   const int ntiles = group * nq;
   uint4 pq[Q_ITERS], pd[Q_ITERS];
   float pl = 0.f, pdl = 0.f;
+  // unconditional loads (rows past S clamped to S-1: their P is masked to 0, so they add
+  // nothing): no zero-init + branch, which made hipcc drain vmcnt at every fetch
   auto fetch = [&](int t) {
     const int g = t / nq;
     const int q0 = q_start + (t - g * nq) * QT;
@@ -147,19 +151,15 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
     for (int it = 0; it < Q_ITERS; ++it) {
       const int c = tid + 256 * it;
       const int row = c / CPR, ch = c % CPR;
-      const int qq = q0 + row;
-      pq[it] = make_uint4(0, 0, 0, 0);
-      pd[it] = make_uint4(0, 0, 0, 0);
-      if (qq < a.S) {
-        pq[it] = gload16(Qp + (long)qq * a.q_ss + ch * 8);
-        pd[it] = gload16(Dp + (long)qq * a.do_ss + ch * 8);
-      }
+      const int qq = min(q0 + row, a.S - 1);
+      pq[it] = gload16(Qp + (long)qq * a.q_ss + ch * 8);
+      pd[it] = gload16(Dp + (long)qq * a.do_ss + ch * 8);
     }
     if (tid < QT) {
-      const int qq = q0 + tid;
+      const int qq = min(q0 + tid, a.S - 1);
       const long base = ((long)b * a.Hq + hq) * a.S;
-      pl = qq < a.S ? a.lse[base + qq] * 1.4426950408889634f : 0.f;
-      pdl = qq < a.S ? a.delta[base + qq] : 0.f;
+      pl = a.lse[base + qq];  // scaled to log2 at commit (no use of the load here)
+      pdl = a.delta[base + qq];
     }
   };
   auto commit = [&](int buf) {
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
       *reinterpret_cast<uint4*>(Ds + tr_off<HD>(row, ch)) = pd[it];
     }
     if (tid < QT) {
-      lse_buf[buf * QT + tid] = pl;
+      lse_buf[buf * QT + tid] = pl * 1.4426950408889634f;
       del_buf[buf * QT + tid] = pdl;
     }
   };
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
     const unsigned char* Ds = Dbuf + buf * QT * ROWB;
     const float* lse_s = lse_buf + buf * QT;
     const float* del_s = del_buf + buf * QT;
-    if (t + 1 < ntiles) fetch(t + 1);  // in flight during this tile's MFMAs
+    if (!(ABL & 4) && t + 1 < ntiles) fetch(t + 1);  // in flight during this tile's MFMAs
 
     const bool active = !(CAUSAL && wkey0 > q0 + QT - 1) && wkey0 < a.S;
     float pbuf[16], dsbuf[16];
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
             make_uint2((unsigned)w4[0] | ((unsigned)w4[1] << 16), (unsigned)w4[2] | ((unsigned)w4[3] << 16));
       }
     }
-    __syncthreads();
+    lds_sync();
     // ---- dQ[q][d] += dS K over this block's 128 keys; waves split the d-blocks
     {
       constexpr int WPD = 4 / NDB;  // waves per d-block (1 for HD=128, 2 for HD=64)
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
       const int kpart = wave % WPD;
       constexpr int KSTEPS = KBLK / 16 / WPD;
       // skip if every key of this block is above this q tile's diagonal (all dS zero)
-      if (!(CAUSAL && k0 > q0 + QT - 1)) {
+      if (!(ABL & 2) && !(CAUSAL && k0 > q0 + QT - 1)) {
         f32x16 acc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -280,18 +280,26 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
           const bf16x8_t bf = tr_frag_nat<HD>(Ks, key0, d * 32, lane);
           acc = mfma32(af, bf, acc);
         }
+        // the next tile's Q / dO go to the other buffer BEFORE the atomics are issued, so
+        // the wait for the prefetch loads is not a wait for the (younger) atomics; that
+        // buffer was last read during tile t-1, before this tile's first barrier
+        if (!(ABL & 4) && t + 1 < ntiles) commit(buf ^ 1);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int qq = q0 + acc_row(i, hh);
-          if (qq < a.S) atomicAdd(dq_p + (long)qq * a.Hq * HD + d * 32 + r, acc[i]);
+          if constexpr (ABL & 1) {
+            asm volatile("" ::"v"(acc[i]));
+          } else {
+            // unconditional (rows past S add 0 to row S-1): a branch per atomic makes
+            // hipcc's vmcnt accounting assume they may not exist and drain them early
+            atomicAdd(dq_p + (long)min(qq, a.S - 1) * a.Hq * HD + d * 32 + r, qq < a.S ? acc[i] : 0.f);
+          }
         }
+      } else if (!(ABL & 4) && t + 1 < ntiles) {
+        commit(buf ^ 1);
       }
     }
-    // next tile's Q / dO into the other buffer (last read during tile t-1, before this
-    // tile's first barrier); the barrier also orders this tile's St reads before the next
-    // tile's St writes
-    if (t + 1 < ntiles) commit(buf ^ 1);
-    __syncthreads();
+    lds_sync();  // LDS-only: the dQ atomics and the next tile's loads stay in flight
   }
   // ---- write dK, dV (bf16) for this wave's keys: lane = key, regs = d
   if (my_key < a.S) {
@@ -373,6 +381,32 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
   return {dq, dk, dv};
 }
 
-TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("flash_attn_bwd", &flash_attn_bwd); }
+// timing-only ablation entry (HD=128, causal): same launch as flash_attn_bwd's main kernel
+void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                   const at::Tensor& o, const at::Tensor& lse, at::Tensor& dq_acc, at::Tensor& dk, at::Tensor& dv,
+                   int64_t abl) {
+  const int B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
+  LLMCTL_CHECK(D == 128, "fa_bwd_ablate: D=128 only");
+  const c10::DeviceGuard g(q.device());
+  BwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_ptr(o), bf_ptr(dout), lse.data_ptr<float>(), lse.data_ptr<float>(),
+            dq_acc.data_ptr<float>(), bf_mut(dk), bf_mut(dv), B, S, Hq, Hkv,
+            q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+            v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
+            dout.stride(0), dout.stride(1), dout.stride(2), 0.088f, 0.127f};
+  dim3 grid((unsigned)(B * Hkv * ((S + KBLK - 1) / KBLK))), block(256);
+  auto s = stream();
+  switch (abl) {
+    case 0: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 0>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 1>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 2>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 4>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 6>), grid, block, 0, s, a); break;
+  }
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("flash_attn_bwd", &flash_attn_bwd);
+  m.impl("fa_bwd_ablate", &fa_bwd_ablate);
+}
 
 }  // namespace llmctl
