@@ -138,6 +138,8 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
 template <bool AT, bool BT, bool ACC, int V>
@@ -146,20 +148,20 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(GemmArgs args) {
   //   1: issue a K-tile's whole DMA (A and B) in phase a instead of A in phase a, B in phase b
   //   2: compiler-counted lgkmcnt before the MFMAs instead of an explicit lgkmcnt(0) drain
   //   4: no s_setprio around the MFMA clusters
-  //   8: register staging (global_load_dwordx4 -> VGPR -> ds_write_b128) instead of LDS DMA:
-  //      tile kt+3 loaded in phase a(kt)'s MFMA section, written to LDS in phase a(kt+1)'s
-  //      read section
   //   16/32/48: tile-order group of 8 / 1 / 16 tile-rows instead of 4
   //   64: skew each tile's K start by (tile % 8) K-tiles (wrapping), so co-resident tiles
   //       stream different lines at any instant
   constexpr bool ONE = V & 1;
-  constexpr bool REG = V & 8;
   constexpr int GROUP = (V & 48) == 16 ? 8 : (V & 48) == 32 ? 1 : (V & 48) == 48 ? 16 : 4;
   constexpr bool SKEW = V & 64;
   constexpr bool BUF = V & 128;  // 128: buffer_load ... lds DMA instead of global_load_lds
   constexpr bool COUNTED = V & 2;
   constexpr bool PRIO = !(V & 4);
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[NSLOT * SLOT];
+  // timing ablations (results wrong): 512 no MFMA, 1024 no fragment reads
+  constexpr bool NOMFMA = V & 512, NOREAD = V & 1024;
+  constexpr int NS = (V & 256) ? 5 : NSLOT;  // 256: 5-slot ring (all 160 KB of LDS), distance 4
+  constexpr int DIST = NS - 1;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(GemmArgs args) {
     bvo[i] = (unsigned)(boff[i] * 2);
   }
   auto stage_a = [&](int kt) {  // A image of K-tile kt -> slot kt % 4
-    const unsigned l = lds0 + (kt & (NSLOT - 1)) * SLOT;
+    const unsigned l = lds0 + (kt % NS) * SLOT;
     if constexpr (BUF) {
       const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)(phys(kt) * a_kstep * 2));
 #pragma unroll
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(GemmArgs args) {
     }
   };
   auto stage_b = [&](int kt) {
-    const unsigned l = lds0 + (kt & (NSLOT - 1)) * SLOT + IMG;
+    const unsigned l = lds0 + (kt % NS) * SLOT + IMG;
     if constexpr (BUF) {
       const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)(phys(kt) * b_kstep * 2));
 #pragma unroll
@@ -223,22 +225,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(GemmArgs args) {
     } else {
 #pragma unroll
       for (int i = 0; i < PIECES; ++i) glds16(Bb + phys(kt) * b_kstep + boff[i], l + i * NTHR * 16);
-    }
-  };
-  uint4 ra[PIECES], rb[PIECES];
-  auto load_regs = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      ra[i] = *reinterpret_cast<const uint4*>(Ab + kt * a_kstep + aoff[i]);
-      rb[i] = *reinterpret_cast<const uint4*>(Bb + kt * b_kstep + boff[i]);
-    }
-  };
-  auto write_regs = [&](int kt) {
-    unsigned char* d = smem + (kt & (NSLOT - 1)) * SLOT + tid * 16;
-#pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      *reinterpret_cast<uint4*>(d + i * NTHR * 16) = ra[i];
-      *reinterpret_cast<uint4*>(d + IMG + i * NTHR * 16) = rb[i];
     }
   };
   auto pre_mfma = [&]() {
@@ -262,19 +248,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(GemmArgs args) {
   const int bn0 = wc * 64;   // this wave's rows in the B image
 
   // prologue: K-tiles 0, 1, 2 in flight; wait for tile 0
-  if constexpr (REG) {
-    load_regs(0);
-    write_regs(0);
-    if (KT > 1) { load_regs(1); write_regs(1); }
-    if (KT > 2) { load_regs(2); write_regs(2); }
-    if (KT > 3) load_regs(3);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  } else {
-    stage_a(0); stage_b(0);
-    if (KT > 1) { stage_a(1); stage_b(1); }
-    if (KT > 2) { stage_a(2); stage_b(2); }
-    if (KT > 2) wait_vm<8>();
-    else if (KT > 1) wait_vm<4>();
+  {
+#pragma unroll
+    for (int i = 0; i < DIST; ++i)
+      if (i < KT) { stage_a(i); stage_b(i); }
+    // wait for tile 0: the younger tiles 1..min(DIST,KT)-1 may stay in flight (4 pieces each)
+    const int younger = min(DIST, KT) - 1;
+    if (younger >= 3) wait_vm<12>();
+    else if (younger == 2) wait_vm<8>();
+    else if (younger == 1) wait_vm<4>();
     else wait_vm<0>();
   }
   bar();
@@ -282,55 +264,70 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(GemmArgs args) {
 
   bf16x8_t af[4], bfr[4];
   for (int kt = 0; kt < KT; ++kt) {
-    const unsigned char* sa = smem + (kt & (NSLOT - 1)) * SLOT;
+    const unsigned char* sa = smem + (kt % NS) * SLOT;
     const unsigned char* sb = sa + IMG;
-    // K-tile kt+3 goes to the slot last read by K-tile kt-1 (retired before its phase-b MFMAs)
-    const bool pf = kt + 3 < KT;
+    // K-tile kt+DIST goes to the slot last read by K-tile kt-1 (retired before its phase-b MFMAs)
+    const bool pf = kt + DIST < KT;
     // ---- phase a: m-tiles 0..3 x n-tiles 0..3
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = frag<AT>(sa, am0 + 16 * i, lane);
+    for (int i = 0; i < 4; ++i)
+      if (!NOREAD || kt == 0) af[i] = frag<AT>(sa, am0 + 16 * i, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = frag<BT>(sb, bn0 + 16 * j, lane);
-    if constexpr (REG) {
-      // tile kt+2's registers (loaded during kt-1) -> its slot, last read by tile kt-2
-      if (kt >= 1 && kt + 2 < KT) write_regs(kt + 2);
-    }
+    for (int j = 0; j < 4; ++j)
+      if (!NOREAD || kt == 0) bfr[j] = frag<BT>(sb, bn0 + 16 * j, lane);
     bar();
-    if constexpr (REG) {
-      if (kt >= 1 && pf) load_regs(kt + 3);
-    } else if (pf) {
-      stage_a(kt + 3);
-      if constexpr (ONE) stage_b(kt + 3);
+    if (pf) {
+      stage_a(kt + DIST);
+      if constexpr (ONE) stage_b(kt + DIST);
     }
     pre_mfma();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (NOMFMA) asm volatile("" ::"v"(bfr[j]), "v"(af[i]));
+        else acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      }
     post_mfma();
     bar();
     // ---- phase b: m-tiles 4..7 (B fragments reused); K-tile kt+1 must have landed before
     //      this phase's first barrier (both wave groups read it right after the next one)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = frag<AT>(sa, am0 + 64 + 16 * i, lane);
+    for (int i = 0; i < 4; ++i)
+      if (!NOREAD || kt == 0) af[i] = frag<AT>(sa, am0 + 64 + 16 * i, lane);
     // outstanding DMA pieces younger than K-tile kt+1's: tile kt+2 (4) + tile kt+3's A (2)
-    if constexpr (!REG) {
-      if (kt + 3 < KT) {
-        if constexpr (ONE) wait_vm<8>();
-        else wait_vm<6>();
-      } else if (kt + 2 < KT) {
-        wait_vm<4>();
-      } else if (kt + 1 < KT) {
-        wait_vm<0>();
+    {
+      // pieces younger than K-tile kt+1's: tiles kt+2 .. kt+DIST-1 (4 each) + tile kt+DIST's
+      // A (2; or A+B = 4 with ONE) issued in phase a
+      const int full = min(kt + DIST, KT) - (kt + 2);  // whole younger tiles already issued
+      if (kt + 1 < KT) {
+        if (kt + DIST < KT) {
+          if constexpr (DIST == 4) {
+            if constexpr (ONE) wait_vm<12>();
+            else wait_vm<10>();
+          } else {
+            if constexpr (ONE) wait_vm<8>();
+            else wait_vm<6>();
+          }
+        } else if (full >= 2) {
+          wait_vm<8>();
+        } else if (full == 1) {
+          wait_vm<4>();
+        } else {
+          wait_vm<0>();
+        }
       }
     }
     bar();
-    if (!REG && !ONE && pf) stage_b(kt + 3);
+    if (!ONE && pf) stage_b(kt + DIST);
     pre_mfma();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[4 + i][j] = mfma16(bfr[j], af[i], acc[4 + i][j]);
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (NOMFMA) asm volatile("" ::"v"(bfr[j]), "v"(af[i]));
+        else acc[4 + i][j] = mfma16(bfr[j], af[i], acc[4 + i][j]);
+      }
     post_mfma();
     bar();
   }
@@ -385,9 +382,6 @@ void launch(const GemmArgs& g, int variant) {
     case 5: launch_v<AT, BT, ACC, 5>(g); break;
     case 6: launch_v<AT, BT, ACC, 6>(g); break;
     case 7: launch_v<AT, BT, ACC, 7>(g); break;
-    case 8: launch_v<AT, BT, ACC, 8>(g); break;
-    case 10: launch_v<AT, BT, ACC, 10>(g); break;
-    case 12: launch_v<AT, BT, ACC, 12>(g); break;
     case 16: launch_v<AT, BT, ACC, 16>(g); break;
     case 32: launch_v<AT, BT, ACC, 32>(g); break;
     case 48: launch_v<AT, BT, ACC, 48>(g); break;
@@ -396,6 +390,12 @@ void launch(const GemmArgs& g, int variant) {
     case 128: launch_v<AT, BT, ACC, 128>(g); break;
     case 130: launch_v<AT, BT, ACC, 130>(g); break;
     case 129: launch_v<AT, BT, ACC, 129>(g); break;
+    case 384: launch_v<AT, BT, ACC, 384>(g); break;
+    case 640: launch_v<AT, BT, ACC, 640>(g); break;     // 128 | NOMFMA
+    case 1664: launch_v<AT, BT, ACC, 1664>(g); break;   // 128 | NOMFMA | NOREAD
+    case 1152: launch_v<AT, BT, ACC, 1152>(g); break;   // 128 | NOREAD
+    case 385: launch_v<AT, BT, ACC, 385>(g); break;
+    case 386: launch_v<AT, BT, ACC, 386>(g); break;
     default: launch_v<AT, BT, ACC, 14>(g); break;
   }
 }
