@@ -2,6 +2,16 @@
 // blocks in the individual .hip files; CUDA dispatch key == HIP on ROCm builds of PyTorch).
 #include <torch/library.h>
 
+namespace llmctl {  // custom_ar.hip: tensor-less helpers get catch-all kernels here
+int64_t car_malloc(int64_t bytes);
+void car_free(int64_t ptr);
+at::Tensor car_ipc_handle(int64_t ptr);
+int64_t car_ipc_open(const at::Tensor& handle);
+void car_ipc_close(int64_t ptr);
+int64_t car_sig_words();
+int64_t car_error(int64_t sig_ptr);
+}  // namespace llmctl
+
 TORCH_LIBRARY(llmctl, m) {
   // norms (norm.hip)
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
@@ -33,6 +43,15 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor uniform) -> Tensor");
   // benchmarks / tuning (gemm_bf16.hip, hbm_stream.hip)
   m.def("gemm_bf16(Tensor a, Tensor b) -> Tensor");
+  // custom all-reduce over xGMI peer memory (custom_ar.hip)
+  m.def("car_allreduce(Tensor inp, Tensor(a!) out, Tensor data_ptrs, Tensor sig_ptrs, int rank, int world, int half_bytes) -> ()");
+  m.def("car_malloc(int bytes) -> int", &llmctl::car_malloc);
+  m.def("car_free(int ptr) -> ()", &llmctl::car_free);
+  m.def("car_ipc_handle(int ptr) -> Tensor", &llmctl::car_ipc_handle);
+  m.def("car_ipc_open(Tensor handle) -> int", &llmctl::car_ipc_open);
+  m.def("car_ipc_close(int ptr) -> ()", &llmctl::car_ipc_close);
+  m.def("car_sig_words() -> int", &llmctl::car_sig_words);
+  m.def("car_error(int sig_ptr) -> int", &llmctl::car_error);
   m.def("gemm_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int variant=-1) -> ()");
   m.def("hbm_copy(Tensor src, Tensor(a!) dst) -> ()");
 }

@@ -14,7 +14,8 @@ same step, so every rank posts the identical RCCL sequence.  Ranks != 0 run
 :meth:`TPInferenceEngine.worker_loop` until rank 0 broadcasts ``stop``.
 
 Decode-step hipGraph capture stays on for TP (the collectives are captured with the
-rest) unless ``LLMCTL_TP_GRAPHS=0``.
+rest) unless ``LLMCTL_TP_GRAPHS=0``.  Decode-sized all-reduces (<= 4 MB) use the one-shot
+xGMI peer-memory kernel (:mod:`llmctl.comms.custom_ar`) unless ``LLMCTL_CUSTOM_AR=0``.
 """
 
 from __future__ import annotations
@@ -46,7 +47,15 @@ class TPInferenceEngine(InferenceEngine):
         pc = ParallelContext(tp_group=tp_group, tp_size=self.tp_size, tp_rank=self.tp_rank)
         if kw.get("use_graphs", True) and os.environ.get("LLMCTL_TP_GRAPHS", "1") == "0":
             kw["use_graphs"] = False
+        self.car = None
         super().__init__(model_path, pc=pc, **kw)
+        # decode-sized all-reduces go through the one-shot xGMI kernel (llmctl.comms.custom_ar);
+        # prefill-sized ones and CPU runs stay on RCCL / gloo
+        if (self.device.type == "cuda" and self.tp_size > 1
+                and os.environ.get("LLMCTL_CUSTOM_AR", "1") != "0"):
+            from llmctl.comms.custom_ar import CustomAllReduce
+
+            self.car = CustomAllReduce(self.tp_group, max_bytes=4 << 20, device=self.device)
 
     # ------------------------------------------------------------------ TP hooks
     def _load(self, model_path: str, dtype, seed: int):
@@ -77,6 +86,8 @@ class TPInferenceEngine(InferenceEngine):
         return int(t.item())
 
     def _reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.car is not None and self.car.eligible(x):
+            return self.car.all_reduce(x)
         dist.all_reduce(x, group=self.tp_group)
         return x
 

@@ -125,3 +125,60 @@ def serve_generate(rank: int, world: int, max_tokens: int = 8) -> dict:
     if world > 1:
         eng.stop_workers()
     return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": eng.kv_cache.k.shape[-2]}
+
+
+def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters: int = 20) -> dict:
+    """Two+ processes sharing one GPU: the IPC one-shot all-reduce must equal the sum of the
+    inputs (exact fp32 sum, bf16 output) over many calls (epoch parity) and under hipGraph
+    replay.  The process group is gloo (RCCL cannot put two ranks on one device)."""
+    import torch
+    import torch.distributed as dist
+
+    from llmctl.comms.custom_ar import CustomAllReduce
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    car = CustomAllReduce(max_bytes=2 << 20, device=torch.device("cuda", 0))
+    worst = 0.0
+    try:
+        g = torch.Generator().manual_seed(1234 + rank)
+        for n in sizes:
+            for it in range(iters):
+                x = (torch.randn(n, generator=g) * (1 + it)).to(torch.bfloat16)
+                parts = [torch.empty_like(x) for _ in range(world)]
+                dist.all_gather(parts, x)
+                want = torch.stack([p.float() for p in parts]).sum(0)
+                got = car.all_reduce(x.cuda()).float().cpu()
+                err = ((got - want).abs() / (want.abs() + 1e-2)).max().item()
+                worst = max(worst, err)
+        # graph capture: one captured call, replayed with fresh inputs
+        n = 16384
+        static = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+        out = torch.empty_like(static)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            car.all_reduce(static, out)
+        torch.cuda.current_stream().wait_stream(s)
+        dist.barrier()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            car.all_reduce(static, out)
+        dist.barrier()
+        for it in range(5):
+            x = (torch.randn(n, generator=g)).to(torch.bfloat16)
+            parts = [torch.empty_like(x) for _ in range(world)]
+            dist.all_gather(parts, x)
+            want = torch.stack([p.float() for p in parts]).sum(0)
+            static.copy_(x.cuda())
+            torch.cuda.synchronize()
+            dist.barrier()
+            graph.replay()
+            torch.cuda.synchronize()
+            err = ((out.float().cpu() - want).abs() / (want.abs() + 1e-2)).max().item()
+            worst = max(worst, err)
+        car.check()
+    finally:
+        dist.barrier()
+        car.close()
+    return {"worst_rel_err": worst}

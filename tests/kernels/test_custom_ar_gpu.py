@@ -1,0 +1,16 @@
+"""Custom IPC all-reduce (llmctl/comms/custom_ar.py): two processes on the one GPU of the
+test box map each other's buffers through hipIpc handles; results must match the exact sum."""
+
+import pytest
+
+from llmctl.testing.harness import run_ranks
+from llmctl.testing.workers import custom_ar_check
+
+pytestmark = pytest.mark.gpu
+
+
+def test_custom_allreduce_two_processes(native_lib):
+    out = run_ranks(custom_ar_check, 2, timeout=300)
+    for r in (0, 1):
+        # bf16 output of an fp32 sum: <= 1 bf16 ulp relative
+        assert out[r]["worst_rel_err"] < 1e-2, out
