@@ -135,6 +135,7 @@ class CheckpointManager:
         shard_id = pg.pp_rank * pg.layout.tp + pg.tp_rank
         n_shards = pg.layout.tp * pg.layout.pp
         write_model = pg.dp_rank == 0
+        e.optimizer.wait_params()  # ZeRO-1/2: parameter all-gathers may still be in flight
         model_sd = {}
         if write_model:
             if getattr(e, "zero3", None) is not None:
@@ -242,6 +243,7 @@ class CheckpointManager:
         if p.is_dir() and (p / "latest").exists() and not (p / "training_state.json").exists():
             p = p / (p / "latest").read_text().strip()
         state = json.loads((p / "training_state.json").read_text())
+        e.optimizer.wait_params()
         full = load_full_state_dict(p, e.model_config)
         # re-shard for this rank's layout
         named = (e.zero3.full_named_parameters() if getattr(e, "zero3", None) is not None

@@ -183,6 +183,8 @@ class TrainingEngine:
             self.sync = GradSyncEngine(self.flat, group=pg.dp_group, mode=mode,
                                        shard_view=self.optimizer.shard_view if mode == "reduce_scatter" else None,
                                        tp_group=pg.tp_group, sequence_parallel=pc.sequence_parallel)
+        if self.zero3 is None and self.optimizer.zero_stage >= 1 and dp > 1:
+            self._install_param_gather_hooks()
         total = c.max_steps if c.max_steps > 0 else 1000
         self.scheduler = LRSchedule(c.learning_rate, c.scheduler, c.warmup_steps, total)
         self.pipeline = None
@@ -193,6 +195,24 @@ class TrainingEngine:
         n_local = sum(p.numel() for p in self.model.parameters())
         log.info("rank %d: tp=%d pp=%d dp=%d zero=%d layers[%d:%d] local params %.3fB on %s",
                  self.rank, pg.layout.tp, pp, dp, c.zero_stage, lo, hi, n_local / 1e9, self.device)
+
+    def _install_param_gather_hooks(self) -> None:
+        """ZeRO-1/2: the post-step all-gather of updated parameter shards overlaps the next
+        forward — each decoder layer (and the top-level module, for embedding / head / final
+        norm) waits only for the buckets holding its own parameters."""
+        flat, opt = self.flat, self.optimizer
+
+        def buckets_of(params):
+            return sorted({flat.param_bucket[id(p)].index for p in params if id(p) in flat.param_bucket})
+
+        def hook_for(idx):
+            return lambda module, args: opt.wait_params(idx)
+
+        top = [p for n, p in self.model.named_parameters() if not n.startswith("layers.")]
+        self._gather_hooks = [self.model.register_forward_pre_hook(hook_for(buckets_of(top)))]
+        for layer in self.model.layers:
+            self._gather_hooks.append(layer.register_forward_pre_hook(hook_for(buckets_of(layer.parameters()))))
+        opt.overlap_param_gather = True
 
     # ------------------------------------------------------------------ data
     def make_data(self):
@@ -216,6 +236,7 @@ class TrainingEngine:
         if self.zero3 is not None:
             self.zero3.begin_step()
         if self.pipeline is not None:
+            self.optimizer.wait_params()  # stages call embed/head outside the hooked forward
             loss = self.pipeline.run(batches)
         else:
             n = len(batches)
@@ -247,6 +268,7 @@ class TrainingEngine:
 
     @torch.no_grad()
     def evaluate(self, batches) -> float:
+        self.optimizer.wait_params()
         self.model.eval()
         tot, n = 0.0, 0
         for x, y in batches:
@@ -337,6 +359,7 @@ class TrainingEngine:
         """Collective: every rank returns the full unsharded model (CPU tensors)."""
         from llmctl.io.checkpoint import _global_name, consolidate_tp
 
+        self.optimizer.wait_params()
         named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
         local = {_global_name(n, self.pc.layer_start): p.detach().float().cpu() for n, p in named}
         if self.zero3 is not None:

@@ -95,6 +95,8 @@ class FlatAdamW:
             self.exp_avg_sq = torch.zeros_like(self.master)
             self.grad_shard = torch.zeros(n, dtype=flat.grad_dtype, device=dev)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._pending = {}  # bucket index -> (all-gather work, input buffer)
+        self.overlap_param_gather = False  # engines with forward pre-hooks turn this on
         self.last_grad_norm: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ ZeRO helpers
@@ -141,6 +143,7 @@ class FlatAdamW:
         gradients are still sums; returns the (pre-clip, averaged) global grad norm as a
         device tensor."""
         self.step_count += 1
+        self.wait_params()  # defensive: never update a bucket whose previous gather is in flight
         lr = self.lr if lr is None else lr
         nsq = self.grad_norm_sq()
         norm = torch.sqrt(nsq) / grad_divisor
@@ -148,26 +151,54 @@ class FlatAdamW:
             coef = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0) / grad_divisor
         else:
             coef = torch.ones_like(norm) / grad_divisor
-        for pv, ms, g, m, v, decay, region in self._segments():
-            ops.adamw_step_(pv, ms, g, m, v, lr=lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
-                            weight_decay=self.weight_decay if decay else 0.0, step=self.step_count,
-                            grad_scale=coef)
-        if self.zero_stage > 0:
-            self._all_gather_params()
+        if self.zero_stage == 0:
+            for pv, ms, g, m, v, decay, region in self._segments():
+                ops.adamw_step_(pv, ms, g, m, v, lr=lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
+                                weight_decay=self.weight_decay if decay else 0.0, step=self.step_count,
+                                grad_scale=coef)
+        else:
+            # update shard -> all-gather, bucket by bucket in forward (flat-offset) order: the
+            # RCCL gather of bucket i runs while AdamW updates bucket i+1, and with
+            # ``overlap_param_gather`` the waits move to the next forward (per-module hooks)
+            f = self.flat
+            for b in sorted(f.buckets, key=lambda b: b.start):
+                off, c = self.shard_offsets[b.index]
+                s = b.start + self.dp_rank * c
+                ops.adamw_step_(f.data[s:s + c], self.master[off:off + c], self.grad_shard[off:off + c],
+                                self.exp_avg[off:off + c], self.exp_avg_sq[off:off + c], lr=lr, beta1=self.beta1,
+                                beta2=self.beta2, eps=self.eps,
+                                weight_decay=self.weight_decay if b.decay else 0.0, step=self.step_count,
+                                grad_scale=coef)
+                self._gather_bucket(b)
+            if not self.overlap_param_gather:
+                self.wait_params()
         self.last_grad_norm = norm
         return norm
 
+    def _gather_bucket(self, b: Bucket) -> None:
+        if self.dp == 1:
+            return
+        off, c = self.shard_offsets[b.index]
+        full = self.flat.data[b.start:b.end]
+        mine = full[self.dp_rank * c:(self.dp_rank + 1) * c].clone()  # distinct input buffer
+        work = dist.all_gather_into_tensor(full, mine, group=self.dp_group, async_op=True)
+        self._pending[b.index] = (work, mine)
+
+    def wait_params(self, bucket_indices=None) -> None:
+        """Make the current stream wait for the updated parameters of the given buckets (all
+        pending ones by default).  Called by forward pre-hooks and before any host-side use
+        of the parameters (eval, checkpointing)."""
+        if not self._pending:
+            return
+        keys = list(self._pending) if bucket_indices is None else [i for i in bucket_indices if i in self._pending]
+        for i in keys:
+            work, _ = self._pending.pop(i)
+            work.wait()
+
     def _all_gather_params(self) -> None:
-        f = self.flat
-        works = []
-        for b in f.buckets:
-            off, c = self.shard_offsets[b.index]
-            full = f.data[b.start:b.end]
-            mine = full[self.dp_rank * c:(self.dp_rank + 1) * c]
-            # all_gather_into_tensor needs a distinct input buffer
-            works.append(dist.all_gather_into_tensor(full, mine.clone(), group=self.dp_group, async_op=True))
-        for w in works:
-            w.wait()
+        for b in self.flat.buckets:
+            self._gather_bucket(b)
+        self.wait_params()
 
     # ------------------------------------------------------------------ state
     def state_dict(self) -> dict:
