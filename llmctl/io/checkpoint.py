@@ -146,6 +146,7 @@ class CheckpointManager:
                 model_sd[_global_name(n, e.pc.layer_start)] = p.detach().to("cpu", copy=True).contiguous()
         opt_sd = {k: (v.detach().to("cpu", copy=True) if torch.is_tensor(v) else v)
                   for k, v in e.optimizer.state_dict().items()}
+        opt_index = optimizer_index(e)
         rng = {"cpu": torch.get_rng_state(), "cuda": torch.cuda.get_rng_state() if e.device.type == "cuda" else None}
         state = {
             "global_step": e.global_step, "epoch": e.epoch,
@@ -166,6 +167,8 @@ class CheckpointManager:
                     save_file(model_sd, str(path / fname), metadata=meta)
                 (path / "optimizer").mkdir(exist_ok=True)
                 torch.save(opt_sd, path / "optimizer" / f"rank_{rank:05d}.pt")
+                if opt_index is not None:
+                    (path / "optimizer" / f"rank_{rank:05d}.index.json").write_text(json.dumps(opt_index))
                 (path / "rng").mkdir(exist_ok=True)
                 torch.save(rng, path / "rng" / f"rank_{rank:05d}.pt")
             except BaseException as ex:  # surfaced by wait()
@@ -262,8 +265,12 @@ class CheckpointManager:
         opt_file = p / "optimizer" / f"rank_{e.pg.rank:05d}.pt"
         if same_layout and opt_file.exists():
             e.optimizer.load_state_dict(torch.load(opt_file, map_location=e.device, weights_only=True))
+        elif getattr(e, "zero3", None) is None and list((p / "optimizer").glob("rank_*.index.json")):
+            # layout changed: fp32 master + Adam moments are resharded from the saved
+            # layout-independent index (TP consolidate -> re-split -> new ZeRO shard)
+            reshard_optimizer(e, p, state)
         else:
-            # layout changed: masters restart from the (resharded) bf16 weights
+            # no index (older checkpoint / ZeRO-3): masters restart from the resharded weights
             _reinit_master_from_params(e)
             e.optimizer.step_count = int(state.get("global_step", 0))
         rng_file = p / "rng" / f"rank_{e.pg.rank:05d}.pt"
@@ -275,6 +282,90 @@ class CheckpointManager:
         e.global_step = int(state["global_step"])
         e.epoch = int(state.get("epoch", 0))
         e.consumed_samples = int(state.get("consumed_samples", 0))
+
+
+def optimizer_index(e) -> Optional[Dict[str, Any]]:
+    """Map this rank's optimizer-state vector onto (global parameter, element range) pairs:
+    ``segments`` = [global_name, offset_in_local_param, offset_in_state, length] plus the
+    TP-local shape of every parameter, so the state can be re-split for any other layout.
+    ZeRO-3 (per-unit shard flats) is not indexed."""
+    if getattr(e, "zero3", None) is not None:
+        return None
+    opt, flat = e.optimizer, e.flat
+    start = e.pc.layer_start
+    params = [(flat.offsets[id(q)], q.numel(), _global_name(flat.names[id(q)], start), list(q.shape))
+              for q in flat.params]
+    segs = []
+    if opt.zero_stage == 0:
+        for off, n, g, _ in params:
+            segs.append([g, 0, off, n])
+    else:
+        for b in flat.buckets:
+            soff, c = opt.shard_offsets[b.index]
+            r0 = b.start + opt.dp_rank * c
+            r1 = r0 + c
+            for off, n, g, _ in params:
+                lo, hi = max(off, r0), min(off + n, r1)
+                if lo < hi:
+                    segs.append([g, lo - off, soff + lo - r0, hi - lo])
+    pg = e.pg
+    return {"tp_rank": pg.tp_rank, "pp_rank": pg.pp_rank, "dp_rank": pg.dp_rank, "zero": opt.zero_stage,
+            "shapes": {g: shp for _, _, g, shp in params}, "segments": segs}
+
+
+def reshard_optimizer(e, path: Path, state: Dict[str, Any]) -> None:
+    """Rebuild this rank's fp32 master / exp_avg / exp_avg_sq from a checkpoint written under
+    a different TP / PP / DP / ZeRO layout.  Old shards are memory-mapped, so a rank reads only
+    the byte ranges of the parameters it now owns."""
+    opt, flat, cfg = e.optimizer, e.flat, e.model_config
+    old: Dict[tuple, List] = {}  # (tp_rank, pp_rank) -> [(index, state_dict)]
+    for f in sorted((path / "optimizer").glob("rank_*.index.json")):
+        idx = json.loads(f.read_text())
+        sd = torch.load(f.with_name(f.name.replace(".index.json", ".pt")), map_location="cpu", weights_only=True,
+                        mmap=True)
+        old.setdefault((idx["tp_rank"], idx["pp_rank"]), []).append((idx, sd))
+    old_tp = int(state.get("layout", {}).get("tp", 1))
+    # global name -> (pp_rank, {tp_rank: [(index, sd, segments of that name)]})
+    where: Dict[str, Dict[int, list]] = {}
+    for (tr, pr), items in old.items():
+        for idx, sd in items:
+            for seg in idx["segments"]:
+                where.setdefault(seg[0], {}).setdefault(tr, []).append((idx, sd, seg))
+    keys = ("master", "exp_avg", "exp_avg_sq")
+    start = e.pc.layer_start
+    new_tp, new_tr = e.pg.layout.tp, e.pg.tp_rank
+    for q in flat.params:
+        g = _global_name(flat.names[id(q)], start)
+        if g not in where:
+            raise KeyError(f"optimizer state for {g} missing in {path}")
+        per_tp = where[g]
+        full = {}
+        for k in keys:
+            parts = []
+            for tr in range(old_tp if tp_split_rule(g, cfg) is not None else 1):
+                items = per_tp[tr]
+                shape = items[0][0]["shapes"][g]
+                buf = torch.zeros(int(torch.tensor(shape).prod().item()) if shape else 1, dtype=torch.float32)
+                for idx, sd, (_, poff, soff, n) in items:
+                    buf[poff:poff + n] = sd[k][soff:soff + n].float()
+                parts.append(buf.view(shape))
+            t = consolidate_tp(g, parts, cfg) if len(parts) > 1 else parts[0]
+            full[k] = shard_tp(g, t, new_tp, new_tr, cfg).reshape(-1)
+        off, n = flat.offsets[id(q)], q.numel()
+        with torch.no_grad():
+            if opt.zero_stage == 0:
+                for k in keys:
+                    getattr(opt, k)[off:off + n].copy_(full[k].to(opt.master.device))
+            else:
+                for b in flat.buckets:
+                    soff, c = opt.shard_offsets[b.index]
+                    r0 = b.start + opt.dp_rank * c
+                    lo, hi = max(off, r0), min(off + n, r0 + c)
+                    if lo < hi:
+                        for k in keys:
+                            getattr(opt, k)[soff + lo - r0:soff + hi - r0].copy_(
+                                full[k][lo - off:hi - off].to(opt.master.device))
+    opt.step_count = int(state.get("global_step", 0))
 
 
 def _reinit_master_from_params(e) -> None:

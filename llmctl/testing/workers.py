@@ -182,3 +182,57 @@ def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters
         dist.barrier()
         car.close()
     return {"worst_rel_err": worst}
+
+
+def _layout_config(layout: dict, model: str = "tiny"):
+    return _config(model_name_or_path=model, tensor_parallel=layout.get("tp", 1),
+                   pipeline_parallel=layout.get("pp", 1), zero_stage=layout.get("zero", 0),
+                   sequence_parallel=layout.get("sp", False), num_microbatches=layout.get("microbatches", 0),
+                   async_checkpoint=False)
+
+
+def ckpt_save_phase(rank: int, world: int, layout: dict, steps: int, out_dir: str) -> dict:
+    """Train ``steps`` steps under ``layout`` from the reference init, then checkpoint."""
+    from llmctl.io.checkpoint import CheckpointManager
+    from llmctl.runtime.engine import TrainingEngine
+
+    eng = TrainingEngine(_layout_config(layout))
+    eng.load_full_state_dict(reference_state("tiny"))
+    vocab, cfg = eng.model_config.vocab_size, eng.config
+    for s in range(steps):
+        eng.train_step([make_batch(vocab, cfg.seq_len, cfg.batch_size, s, eng.pg.dp_rank, 0)])
+    ck = CheckpointManager(eng, out_dir)
+    ck.save("ckpt", final=True)
+    ck.wait()
+    return {}
+
+
+def ckpt_resume_phase(rank: int, world: int, layout: dict, start: int, steps: int, out_dir: str) -> dict:
+    """Resume the checkpoint under a (possibly different) ``layout`` and train more steps."""
+    from llmctl.io.checkpoint import CheckpointManager
+    from llmctl.runtime.engine import TrainingEngine
+
+    eng = TrainingEngine(_layout_config(layout))
+    CheckpointManager(eng, out_dir).load(out_dir + "/ckpt")
+    vocab, cfg = eng.model_config.vocab_size, eng.config
+    assert eng.global_step == start and eng.optimizer.step_count == start
+    for s in range(start, start + steps):
+        eng.train_step([make_batch(vocab, cfg.seq_len, cfg.batch_size, s, eng.pg.dp_rank, 0)])
+    full = eng.gather_full_state_dict()
+    return {"state": full if rank == 0 else None}
+
+
+def train_reference_schedule(schedule) -> dict:
+    """Single process; ``schedule[s]`` = number of DP ranks whose micro-batches form step s."""
+    import os
+
+    from llmctl.runtime.engine import TrainingEngine
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    eng = TrainingEngine(_config(model_name_or_path="tiny"))
+    eng.load_full_state_dict(reference_state("tiny"))
+    vocab, cfg = eng.model_config.vocab_size, eng.config
+    for s, dp in enumerate(schedule):
+        eng.train_step([make_batch(vocab, cfg.seq_len, cfg.batch_size, s, r, 0) for r in range(dp)])
+    return {"state": eng.gather_full_state_dict()}
