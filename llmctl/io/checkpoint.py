@@ -152,7 +152,7 @@ class CheckpointManager:
             "global_step": e.global_step, "epoch": e.epoch,
             "config": {k: (list(v) if isinstance(v, tuple) else v) for k, v in vars(c).items()},
             "scheduler": e.scheduler.state_dict(), "consumed_samples": e.consumed_samples,
-            "world_size": world, "layout": {"tp": pg.layout.tp, "pp": pg.layout.pp, "dp": pg.layout.dp},
+            "world_size": world, "layout": {"tp": pg.layout.tp, "pp": pg.layout.pp, "dp": pg.layout.dp, "cp": pg.layout.cp},
             "zero_stage": c.zero_stage,
         }
 
@@ -260,7 +260,10 @@ class CheckpointManager:
                 prm.copy_(t.to(prm.dtype))
         if getattr(e, "zero3", None) is not None:
             e.zero3.reload_shards_from_full()
-        same_layout = (state.get("layout") == {"tp": e.pg.layout.tp, "pp": e.pg.layout.pp, "dp": e.pg.layout.dp}
+        old_layout = dict(state.get("layout", {}))
+        old_layout.setdefault("cp", 1)
+        same_layout = (old_layout == {"tp": e.pg.layout.tp, "pp": e.pg.layout.pp, "dp": e.pg.layout.dp,
+                                      "cp": e.pg.layout.cp}
                        and state.get("zero_stage", 0) == e.config.zero_stage)
         opt_file = p / "optimizer" / f"rank_{e.pg.rank:05d}.pt"
         if same_layout and opt_file.exists():

@@ -25,6 +25,7 @@ import torch.nn.functional as F
 
 from llmctl import ops
 from llmctl.exec.linear import linear, weight_grad
+from llmctl.parallel import context_parallel as cp
 from llmctl.parallel import tensor_parallel as tp
 from .config import ModelConfig
 
@@ -42,6 +43,10 @@ class ParallelContext:
     has_head: bool = True
     # recompute policy: "none" | "selective" | "full"
     activation_checkpoint: str = "none"
+    # context parallel (Ulysses all-to-all around attention; llmctl.parallel.context_parallel)
+    cp_group: Optional[object] = None
+    cp_size: int = 1
+    cp_rank: int = 0
 
 
 def _init_linear(w: torch.Tensor, std: float) -> None:
@@ -86,6 +91,8 @@ class DecoderLayer(nn.Module):
         t = pc.tp_size
         if cfg.heads % t or cfg.kv_heads % t or cfg.ffn % t:
             raise ValueError(f"heads/kv_heads/ffn must divide tp={t}")
+        if (cfg.kv_heads // t) % pc.cp_size or (cfg.heads // t) % pc.cp_size:
+            raise ValueError(f"(kv_)heads / tp must divide context_parallel={pc.cp_size}")
         self.nq, self.nkv, self.D = cfg.heads // t, cfg.kv_heads // t, cfg.head_dim
         self.f = cfg.ffn // t
         h = cfg.hidden
@@ -149,8 +156,13 @@ class DecoderLayer(nn.Module):
         q = q.view(B, S, self.nq, self.D)
         k = k.view(B, S, self.nkv, self.D)
         v = v.view(B, S, self.nkv, self.D)
-        o = ops.flash_attention(q, k, v, causal=True)
-        out = linear(o.view(B * S, self.nq * self.D), self.wo)
+        if self.pc.cp_size > 1:  # sequence chunk, all heads <-> all tokens, head chunk
+            g = self.pc.cp_group
+            o = cp.head_to_seq(ops.flash_attention(cp.seq_to_head(q, g), cp.seq_to_head(k, g),
+                                                   cp.seq_to_head(v, g), causal=True), g)
+        else:
+            o = ops.flash_attention(q, k, v, causal=True)
+        out = linear(o.reshape(B * S, self.nq * self.D), self.wo)
         out = self._row_out(out)
         if self.bo is not None:
             out = out + self.bo
@@ -257,14 +269,19 @@ class DecoderLM(nn.Module):
         else:
             x = F.embedding(ids, self.embed)
         if self.pos_embed is not None:
-            pos = self.pos_embed[:S].repeat(B, 1)
+            if pc.cp_size > 1:  # this rank's chunk of the sequence: global positions
+                pos = self.pos_embed[pc.cp_rank * S:(pc.cp_rank + 1) * S].repeat(B, 1)
+            else:
+                pos = self.pos_embed[:S].repeat(B, 1)
             if pc.tp_size > 1 and pc.sequence_parallel:
                 pos = tp._split_tokens(pos, pc.tp_group)
             x = x + pos
         return x
 
     def run_layers(self, x, B, S, residual=None, positions=None):
-        rope = self.rope_tables(S, x.device)
+        if self.pc.cp_size > 1 and positions is None:
+            positions = cp.local_positions(B, S, self.pc.cp_rank, x.device)
+        rope = self.rope_tables(S * self.pc.cp_size, x.device)
         ac = self.pc.activation_checkpoint
         for layer in self.layers:
             if ac == "full" and self.training and torch.is_grad_enabled():

@@ -64,6 +64,7 @@ class TrainingConfig:
     seq_len: int = 2048
     tensor_parallel: int = 1
     pipeline_parallel: int = 1
+    context_parallel: int = 1  # Ulysses CP: sequence split over cp ranks (llmctl.parallel.context_parallel)
     sequence_parallel: bool = False
     zero_stage: int = 0
     activation_checkpoint: str = "none"  # none | selective | full
@@ -129,7 +130,10 @@ class TrainingEngine:
             if backend == "nccl":
                 kw["device_id"] = self.device
             dist.init_process_group(backend=backend, **kw)
-        self.pg: ProcessGroups = build_process_groups(tp=c.tensor_parallel, pp=c.pipeline_parallel)
+        if c.context_parallel > 1 and c.pipeline_parallel > 1:
+            raise NotImplementedError("context_parallel with pipeline_parallel is not supported")
+        self.pg: ProcessGroups = build_process_groups(tp=c.tensor_parallel, pp=c.pipeline_parallel,
+                                                      cp=c.context_parallel)
         self.rank = self.pg.rank
         self.is_main = self.rank == 0
 
@@ -147,7 +151,8 @@ class TrainingEngine:
             tp_group=pg.tp_group, tp_size=pg.layout.tp, tp_rank=pg.tp_rank,
             sequence_parallel=c.sequence_parallel and pg.layout.tp > 1,
             layer_start=lo, layer_end=hi, has_embedding=pp_rank == 0, has_head=pp_rank == pp - 1,
-            activation_checkpoint=c.activation_checkpoint)
+            activation_checkpoint=c.activation_checkpoint,
+            cp_group=pg.cp_group, cp_size=pg.layout.cp, cp_rank=pg.cp_rank)
         # identical init on every DP replica (seeded; TP ranks get different shards, so
         # their seeds differ by tp_rank/pp_rank only)
         torch.manual_seed(c.seed + 1000 * pg.tp_rank + 100000 * pp_rank)
@@ -159,7 +164,7 @@ class TrainingEngine:
         if c.zero_stage >= 3 and dp > 1:
             from llmctl.parallel.zero import Zero3Model
 
-            self.zero3 = Zero3Model(self.model, dp_group=pg.dp_group, dtype=c.dtype)
+            self.zero3 = Zero3Model(self.model, dp_group=pg.dpcp_group, dtype=c.dtype)
             self.flat = self.zero3.flat
         else:
             self.zero3 = None
@@ -173,14 +178,15 @@ class TrainingEngine:
         norm_group = pg.pp_group if pp > 1 else None
         self.optimizer = FlatAdamW(self.flat, lr=c.learning_rate, betas=tuple(c.betas), eps=c.eps,
                                    weight_decay=c.weight_decay, max_grad_norm=c.gradient_clipping,
-                                   dp_group=pg.dp_group, zero_stage=min(c.zero_stage, 2) if self.zero3 is None else 0,
+                                   dp_group=pg.dpcp_group, zero_stage=min(c.zero_stage, 2) if self.zero3 is None else 0,
                                    tp_group=pg.tp_group, norm_group=norm_group)
         if self.zero3 is not None:
             self.zero3.attach_optimizer(self.optimizer)
             self.sync = None
         else:
             mode = "reduce_scatter" if self.optimizer.zero_stage >= 1 else "allreduce"
-            self.sync = GradSyncEngine(self.flat, group=pg.dp_group, mode=mode,
+            # gradients are summed over every replica of the parameters: DP × CP
+            self.sync = GradSyncEngine(self.flat, group=pg.dpcp_group, mode=mode,
                                        shard_view=self.optimizer.shard_view if mode == "reduce_scatter" else None,
                                        tp_group=pg.tp_group, sequence_parallel=pc.sequence_parallel)
         if self.zero3 is None and self.optimizer.zero_stage >= 1 and dp > 1:
@@ -240,7 +246,13 @@ class TrainingEngine:
             loss = self.pipeline.run(batches)
         else:
             n = len(batches)
-            tokens = batches[0][1].numel()
+            cpn = self.pg.layout.cp
+            if cpn > 1:  # this rank's contiguous chunk of every sequence
+                from llmctl.parallel.context_parallel import split_sequence
+
+                batches = [(split_sequence(x, cpn, self.pg.cp_rank), split_sequence(y, cpn, self.pg.cp_rank))
+                           for x, y in batches]
+            tokens = batches[0][1].numel() * cpn  # per replica: the CP ranks share one sequence
             # loss is a per-token mean inside each micro-batch; dividing the denominator
             # by n makes the accumulated gradient the mean over all n micro-batches
             denom = float(tokens * n)

@@ -48,7 +48,8 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
                   pipeline_parallel=layout.get("pp", 1), zero_stage=layout.get("zero", 0),
                   sequence_parallel=layout.get("sp", False),
                   activation_checkpoint=layout.get("ac", "none"),
-                  num_microbatches=layout.get("microbatches", 0))
+                  num_microbatches=layout.get("microbatches", 0),
+                  context_parallel=layout.get("cp", 1))
     eng = TrainingEngine(cfg)
     eng.load_full_state_dict(reference_state(model))
     vocab = eng.model_config.vocab_size
@@ -62,8 +63,10 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
         if eng.pipeline is not None:
             losses.append(eng.pipeline.broadcast_loss(loss))
         else:
-            # DP mean of the per-rank losses
+            # DP mean of the per-rank losses (CP ranks hold partial sums of one loss)
             lt = loss.detach().clone().reshape(1)
+            if eng.pg.cp_group is not None:
+                torch.distributed.all_reduce(lt, group=eng.pg.cp_group)
             if eng.pg.dp_group is not None:
                 torch.distributed.all_reduce(lt, group=eng.pg.dp_group)
                 lt /= eng.pg.layout.dp

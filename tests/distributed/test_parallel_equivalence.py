@@ -101,3 +101,16 @@ def test_zero3_pp2_dp2_matches_single(ref_dp2_m4):
     out = run_ranks(train_layout, 4, STEPS, {"zero": 3, "pp": 2, "microbatches": 4})
     _losses_close(out[0]["losses"], ref_dp2_m4["losses"])
     _close(out[0]["state"], ref_dp2_m4["state"])
+
+
+def test_cp2_ulysses_matches_single(ref_dp1):
+    """Context parallel: each rank holds half of every sequence; all-to-all around attention."""
+    out = run_ranks(train_layout, 2, STEPS, {"cp": 2})
+    _losses_close(out[0]["losses"], ref_dp1["losses"])
+    _close(out[0]["state"], ref_dp1["state"])
+
+
+def test_cp2_dp2_zero1_matches_single(ref_dp2):
+    out = run_ranks(train_layout, 4, STEPS, {"cp": 2, "zero": 1})
+    _losses_close(out[0]["losses"], ref_dp2["losses"])
+    _close(out[0]["state"], ref_dp2["state"])
