@@ -144,7 +144,7 @@ class DecoderLayer(nn.Module):
             return x
         return tp.reduce_scatter_to_sp(x, pc.tp_group) if pc.sequence_parallel else tp.reduce_from_tp(x, pc.tp_group)
 
-    def attention(self, xn, B, S, rope, positions=None):
+    def attention(self, xn, B, S, rope, positions=None, doc_start=None):
         qkv = linear(self._col_in(xn), self.wqkv, self.bqkv)
         if rope is not None:
             q, k, v = ops.rope_qkv(qkv, rope[0], rope[1], self.nq, self.nkv, S, positions)
@@ -161,7 +161,7 @@ class DecoderLayer(nn.Module):
             o = cp.head_to_seq(ops.flash_attention(cp.seq_to_head(q, g), cp.seq_to_head(k, g),
                                                    cp.seq_to_head(v, g), causal=True), g)
         else:
-            o = ops.flash_attention(q, k, v, causal=True)
+            o = ops.flash_attention(q, k, v, causal=True, doc_start=doc_start)
         out = linear(o.reshape(B * S, self.nq * self.D), self.wo)
         out = self._row_out(out)
         if self.bo is not None:
@@ -184,7 +184,7 @@ class DecoderLayer(nn.Module):
             out = out + self.b_down
         return out
 
-    def forward(self, x, residual, B, S, rope, positions=None):
+    def forward(self, x, residual, B, S, rope, positions=None, doc_start=None):
         """Pre-norm block with fused residual-add + norm.
 
         ``residual`` is the running residual stream (None for the first layer);
@@ -196,7 +196,7 @@ class DecoderLayer(nn.Module):
             xn = self._norm(x, self.attn_norm_w, self.attn_norm_b)
         else:
             xn, residual = self._add_norm(x, residual, self.attn_norm_w, self.attn_norm_b)
-        a = self.attention(xn, B, S, rope, positions)
+        a = self.attention(xn, B, S, rope, positions, doc_start)
         xn2, residual = self._add_norm(a, residual, self.mlp_norm_w, self.mlp_norm_b)
         m = self.mlp(xn2)
         return m, residual
@@ -260,7 +260,7 @@ class DecoderLM(nn.Module):
                 device=device)
         return self._rope_cache[key]
 
-    def embed_tokens(self, input_ids: torch.Tensor) -> torch.Tensor:
+    def embed_tokens(self, input_ids: torch.Tensor, positions: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, S = input_ids.shape
         ids = input_ids.reshape(-1)
         pc = self.pc
@@ -269,7 +269,9 @@ class DecoderLM(nn.Module):
         else:
             x = F.embedding(ids, self.embed)
         if self.pos_embed is not None:
-            if pc.cp_size > 1:  # this rank's chunk of the sequence: global positions
+            if positions is not None:  # explicit (e.g. per-document) positions
+                pos = self.pos_embed[positions.long()]
+            elif pc.cp_size > 1:  # this rank's chunk of the sequence: global positions
                 pos = self.pos_embed[pc.cp_rank * S:(pc.cp_rank + 1) * S].repeat(B, 1)
             else:
                 pos = self.pos_embed[:S].repeat(B, 1)
@@ -278,21 +280,24 @@ class DecoderLM(nn.Module):
             x = x + pos
         return x
 
-    def run_layers(self, x, B, S, residual=None, positions=None):
+    def run_layers(self, x, B, S, residual=None, positions=None, doc_start=None):
         if self.pc.cp_size > 1 and positions is None:
             positions = cp.local_positions(B, S, self.pc.cp_rank, x.device)
+        if doc_start is not None and positions is None:  # packed documents: RoPE restarts per document
+            positions = (torch.arange(S, device=x.device, dtype=torch.int32).view(1, S) - doc_start).reshape(-1)
         rope = self.rope_tables(S * self.pc.cp_size, x.device)
         ac = self.pc.activation_checkpoint
         for layer in self.layers:
             if ac == "full" and self.training and torch.is_grad_enabled():
                 if residual is None:
                     x, residual = torch.utils.checkpoint.checkpoint(
-                        lambda a, l=layer: l(a, None, B, S, rope, positions), x, use_reentrant=False)
+                        lambda a, l=layer: l(a, None, B, S, rope, positions, doc_start), x, use_reentrant=False)
                 else:
                     x, residual = torch.utils.checkpoint.checkpoint(
-                        lambda a, r, l=layer: l(a, r, B, S, rope, positions), x, residual, use_reentrant=False)
+                        lambda a, r, l=layer: l(a, r, B, S, rope, positions, doc_start), x, residual,
+                        use_reentrant=False)
             else:
-                x, residual = layer(x, residual, B, S, rope, positions)
+                x, residual = layer(x, residual, B, S, rope, positions, doc_start)
         return x, residual
 
     def head(self, x, residual):
@@ -319,10 +324,17 @@ class DecoderLM(nn.Module):
         return ops.cross_entropy(logits, lab, reduction_denom=denom)
 
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
-                loss_denom: Optional[float] = None):
+                loss_denom: Optional[float] = None, doc_start: Optional[torch.Tensor] = None):
+        """``doc_start`` (int32 [B,S], packed sequences): attention and positions restart at
+        every document boundary (see ``llmctl.ops.ref.document_starts``)."""
         B, S = input_ids.shape
-        x = self.embed_tokens(input_ids)
-        x, residual = self.run_layers(x, B, S)
+        positions = None
+        if doc_start is not None:
+            if self.pc.cp_size > 1:
+                raise NotImplementedError("packed sequences with context parallelism")
+            positions = (torch.arange(S, device=input_ids.device, dtype=torch.int32).view(1, S) - doc_start).reshape(-1)
+        x = self.embed_tokens(input_ids, positions)
+        x, residual = self.run_layers(x, B, S, positions=positions, doc_start=doc_start)
         logits = self.head(x, residual)
         if labels is None:
             return logits

@@ -34,8 +34,8 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("adamw_step_(Tensor(a!) param, Tensor(b!) master, Tensor grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, Tensor? grad_scale) -> ()");
   m.def("l2norm_sq_(Tensor x, Tensor(a!) out) -> ()");
   // attention (flash_attn_fwd.hip / flash_attn_bwd.hip)
-  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal) -> (Tensor, Tensor)");
-  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal) -> (Tensor, Tensor, Tensor)");
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, Tensor? doc_start=None) -> (Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, Tensor? doc_start=None) -> (Tensor, Tensor, Tensor)");
   m.def("fa_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq_acc, Tensor(b!) dk, Tensor(c!) dv, int abl) -> ()");
   // serving (paged_attn.hip, sampling.hip)
   m.def("kv_cache_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot_mapping) -> ()");

@@ -34,6 +34,7 @@ struct BwdArgs {
   int B, S, Hq, Hkv;
   long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh, do_sb, do_ss, do_sh;
   float scale, scale_log2;
+  const int* doc;  // [B, S] document start per token (packed sequences), or nullptr
 };
 
 template <int HD>
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restric
 
 // ABL: timing ablations for tools/attn_bench.py (results wrong): 1 no dQ atomics,
 // 2 no dQ product (and no dS^T exchange), 4 no Q/dO prefetch (tile 0 reused)
-template <int HD, bool CAUSAL, int ABL = 0>
+template <int HD, bool CAUSAL, int ABL = 0, bool DOC = false>
 __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
   constexpr int NKS = HD / 16;
   constexpr int NDB = HD / 32;
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
   constexpr int Q_ITERS = QT * CPR / 256;     // 2 for HD=128
   constexpr int DST_ROWB = QT * 2;            // dS^T rows: 32 q * 2 B = 64 B
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * KBLK * ROWB + 4 * QT * ROWB + KBLK * DST_ROWB +
-                                                             4 * QT * 4];
+                                                             6 * QT * 4];
   unsigned char* Ks = smem;
   unsigned char* Vs = Ks + KBLK * ROWB;
   unsigned char* Qbuf = Vs + KBLK * ROWB;       // [2][QT][HD] double-buffered Q tiles
@@ -94,6 +95,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
   unsigned char* St = Dbuf + 2 * QT * ROWB;     // dS^T [key][q]
   float* lse_buf = reinterpret_cast<float*>(St + KBLK * DST_ROWB);  // [2][QT]
   float* del_buf = lse_buf + 2 * QT;                                 // [2][QT]
+  int* doc_buf = reinterpret_cast<int*>(del_buf + 2 * QT);           // [2][QT] (packed documents)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -135,10 +137,24 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
   // delta are prefetched into registers while the current one is computed (register staging,
   // guide T14) and written to the other LDS buffer after it
   const int q_start = CAUSAL ? (k0 / QT) * QT : 0;
-  const int nq = (a.S - q_start + QT - 1) / QT;
+  int q_end = a.S;
+  if constexpr (DOC) {
+    // queries whose document starts after this block's last key see none of its keys:
+    // q_end = first position with doc_start > k0 + KBLK - 1 (doc_start is non-decreasing)
+    const int* ds = a.doc + (long)b * a.S;
+    int lo = min(k0 + KBLK, a.S), hi = a.S;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ds[mid] > k0 + KBLK - 1) hi = mid;
+      else lo = mid + 1;
+    }
+    q_end = lo;
+  }
+  const int nq = q_end > q_start ? (q_end - q_start + QT - 1) / QT : 0;
   const int ntiles = group * nq;
   uint4 pq[Q_ITERS], pd[Q_ITERS];
   float pl = 0.f, pdl = 0.f;
+  int pds = 0;
   // unconditional loads (rows past S clamped to S-1: their P is masked to 0, so they add
   // nothing): no zero-init + branch, which made hipcc drain vmcnt at every fetch
   auto fetch = [&](int t) {
@@ -160,6 +176,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
       const long base = ((long)b * a.Hq + hq) * a.S;
       pl = a.lse[base + qq];  // scaled to log2 at commit (no use of the load here)
       pdl = a.delta[base + qq];
+      if constexpr (DOC) pds = a.doc[(long)b * a.S + qq];
     }
   };
   auto commit = [&](int buf) {
@@ -175,6 +192,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
     if (tid < QT) {
       lse_buf[buf * QT + tid] = pl * 1.4426950408889634f;
       del_buf[buf * QT + tid] = pdl;
+      if constexpr (DOC) doc_buf[buf * QT + tid] = pds;
     }
   };
   if (ntiles > 0) {
@@ -193,9 +211,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
     const unsigned char* Ds = Dbuf + buf * QT * ROWB;
     const float* lse_s = lse_buf + buf * QT;
     const float* del_s = del_buf + buf * QT;
+    const int* doc_s = doc_buf + buf * QT;
+    // packed documents: the tile's smallest / largest document start (non-decreasing)
+    const int dmin = DOC ? doc_s[0] : 0, dmax = DOC ? doc_s[QT - 1] : 0;
     if (!(ABL & 4) && t + 1 < ntiles) fetch(t + 1);  // in flight during this tile's MFMAs
 
-    const bool active = !(CAUSAL && wkey0 > q0 + QT - 1) && wkey0 < a.S;
+    const bool active = !(CAUSAL && wkey0 > q0 + QT - 1) && wkey0 < a.S && !(DOC && wkey0 + 31 < dmin);
     float pbuf[16], dsbuf[16];
     if (active) {
       // ---- S = Q K^T and dP = dO V^T   (q on regs, key on lane)
@@ -211,14 +232,15 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
         const bf16x8_t vb = lds_read_b128(Vs, tr_off<HD>(wave * 32 + r, 2 * ks + hh));
         dp = mfma32(da, vb, dp);
       }
-      const bool need_mask = (CAUSAL && wkey0 + 31 > q0) || (q0 + QT > a.S) || (wkey0 + 32 > a.S);
+      const bool need_mask = (CAUSAL && wkey0 + 31 > q0) || (q0 + QT > a.S) || (wkey0 + 32 > a.S) ||
+                             (DOC && wkey0 < dmax);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qi = acc_row(i, hh);
         float p = fast_exp2(s[i] * a.scale_log2 - lse_s[qi]);
         if (need_mask) {
           const int qq = q0 + qi;
-          if ((CAUSAL && my_key > qq) || qq >= a.S || my_key >= a.S) p = 0.f;
+          if ((CAUSAL && my_key > qq) || qq >= a.S || my_key >= a.S || (DOC && my_key < doc_s[qi])) p = 0.f;
         }
         pbuf[i] = p;
         dsbuf[i] = p * (dp[i] - del_s[qi]) * a.scale;
@@ -261,7 +283,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
       const int kpart = wave % WPD;
       constexpr int KSTEPS = KBLK / 16 / WPD;
       // skip if every key of this block is above this q tile's diagonal (all dS zero)
-      if (!(ABL & 2) && !(CAUSAL && k0 > q0 + QT - 1)) {
+      if (!(ABL & 2) && !(CAUSAL && k0 > q0 + QT - 1) && !(DOC && k0 + KBLK - 1 < dmin)) {
         f32x16 acc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -329,7 +351,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
 std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q,
                                                               const at::Tensor& k, const at::Tensor& v,
                                                               const at::Tensor& o, const at::Tensor& lse,
-                                                              double scale, bool causal) {
+                                                              double scale, bool causal,
+                                                              const c10::optional<at::Tensor>& doc_start) {
   LLMCTL_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4 && o.dim() == 4 && dout.dim() == 4,
                "flash_attn_bwd: [B,S,H,D] tensors");
   const int B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
@@ -365,10 +388,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
             dq_acc.data_ptr<float>(), bf_mut(dk), bf_mut(dv), B, S, Hq, Hkv,
             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
-            dout.stride(0), dout.stride(1), dout.stride(2), (float)scale, (float)(scale * 1.4426950408889634)};
+            dout.stride(0), dout.stride(1), dout.stride(2), (float)scale, (float)(scale * 1.4426950408889634),
+            nullptr};
   const int nkb = (S + KBLK - 1) / KBLK;
   dim3 grid((unsigned)(B * Hkv * nkb)), block(256);
-  if (D == 128) {
+  if (doc_start.has_value() && doc_start->defined()) {
+    const at::Tensor& ds = *doc_start;
+    LLMCTL_CHECK(causal && ds.is_cuda() && ds.scalar_type() == at::kInt && ds.is_contiguous() && ds.dim() == 2 &&
+                     ds.size(0) == B && ds.size(1) == S,
+                 "flash_attn_bwd: doc_start must be contiguous int32 [B,S] (causal)");
+    a.doc = ds.data_ptr<int>();
+    if (D == 128) hipLaunchKernelGGL((fa_bwd_kernel<128, true, 0, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fa_bwd_kernel<64, true, 0, true>), grid, block, 0, s, a);
+  } else if (D == 128) {
     if (causal) hipLaunchKernelGGL((fa_bwd_kernel<128, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((fa_bwd_kernel<128, false>), grid, block, 0, s, a);
   } else {
@@ -392,7 +424,7 @@ void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
             dq_acc.data_ptr<float>(), bf_mut(dk), bf_mut(dv), B, S, Hq, Hkv,
             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
-            dout.stride(0), dout.stride(1), dout.stride(2), 0.088f, 0.127f};
+            dout.stride(0), dout.stride(1), dout.stride(2), 0.088f, 0.127f, nullptr};
   dim3 grid((unsigned)(B * Hkv * ((S + KBLK - 1) / KBLK))), block(256);
   auto s = stream();
   switch (abl) {

@@ -15,7 +15,10 @@
 //   * causal: tiles wholly above a wave's diagonal are skipped, the mask is applied only
 //     on diagonal tiles; the heaviest q-blocks are dispatched first;
 //   * blocks that share a K/V head are B*Hq apart in dispatch order, i.e. on one XCD (L2
-//     reuse of the K/V stream) when B*Hq % 8 == 0.
+//     reuse of the K/V stream) when B*Hq % 8 == 0;
+//   * packed sequences (optional ``doc_start[B,S]``: position where each token's document
+//     begins, non-decreasing): key j is visible to query i iff doc_start[i] <= j <= i; the
+//     K/V loop starts at the block's first document start, so the work is sum(doc_len^2).
 // Outputs O [B,S,Hq,HD] bf16 and LSE [B,Hq,S] fp32 (natural log) for the backward pass.
 #include "attn_common.h"
 
@@ -38,9 +41,10 @@ struct FwdArgs {
   long v_sb, v_ss, v_sh;
   long o_sb, o_ss, o_sh;
   float scale_log2;  // softmax_scale * log2(e)
+  const int* doc;    // [B, S] document start per token, or nullptr
 };
 
-template <int HD, bool CAUSAL>
+template <int HD, bool CAUSAL, bool DOC = false>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
   constexpr int NKS = HD / 16;  // k-steps of QK^T
   constexpr int NDB = HD / 32;  // 32-wide d blocks of O
@@ -85,6 +89,16 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 
   const int kv_end = CAUSAL ? min(a.S, qblk * QB + QB) : a.S;
   const int ntiles = (kv_end + KB - 1) / KB;
+  // packed documents: this lane's first visible key, the wave's min / max of it (doc_start is
+  // non-decreasing) and the block's first tile
+  int my_start = 0, w_min = 0, w_max = 0, t0 = 0;
+  if constexpr (DOC) {
+    const int* ds = a.doc + (long)b * a.S;
+    my_start = ds[min(my_q, a.S - 1)];
+    w_min = ds[min(q_row0, a.S - 1)];
+    w_max = ds[min(q_row0 + 31, a.S - 1)];
+    t0 = ds[min(qblk * QB, a.S - 1)] / KB;
+  }
 
   // ---- staging registers for one K and one V tile
   uint4 kst[LD_ITERS], vst[LD_ITERS];
@@ -113,14 +127,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     }
   };
 
-  issue(0);
-  for (int t = 0; t < ntiles; ++t) {
+  issue(t0);
+  for (int t = t0; t < ntiles; ++t) {
     __syncthreads();  // all waves finished reading the previous tile
     commit();
     __syncthreads();
     if (t + 1 < ntiles) issue(t + 1);  // overlaps the MFMAs below
     const int kv0 = t * KB;
     if (CAUSAL && kv0 > q_row0 + 31) continue;  // tile entirely above this wave's diagonal
+    if (DOC && kv0 + KB <= w_min) continue;     // tile entirely before every query's document
 
     // ---- S^T = K Q^T  (two 32-key blocks)
     f32x16 s[2];
@@ -135,7 +150,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
       }
     }
     // ---- scale, mask, online softmax (exp2 domain)
-    const bool need_mask = (CAUSAL && kv0 + KB - 1 > q_row0) || (kv0 + KB > a.S);
+    const bool need_mask = (CAUSAL && kv0 + KB - 1 > q_row0) || (kv0 + KB > a.S) || (DOC && kv0 < w_max);
     float mx = -INFINITY;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -144,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
         float x = s[kb][i] * a.scale_log2;
         if (need_mask) {
           const int key = kv0 + kb * 32 + acc_row(i, hh);
-          if ((CAUSAL && key > my_q) || key >= a.S) x = -INFINITY;
+          if ((CAUSAL && key > my_q) || key >= a.S || (DOC && key < my_start)) x = -INFINITY;
         }
         s[kb][i] = x;
         mx = fmaxf(mx, x);
@@ -210,7 +225,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 }  // namespace
 
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                                  double scale, bool causal) {
+                                                  double scale, bool causal,
+                                                  const c10::optional<at::Tensor>& doc_start) {
   LLMCTL_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "flash_attn_fwd: GPU tensors");
   LLMCTL_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 &&
                    v.scalar_type() == at::kBFloat16,
@@ -234,10 +250,21 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   FwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_mut(o), lse.data_ptr<float>(), B, S, Hq, Hkv,
             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
-            (float)(scale * 1.4426950408889634)};
+            (float)(scale * 1.4426950408889634), nullptr};
   const int nqb = (S + QB - 1) / QB;
   dim3 grid((unsigned)(B * Hq * nqb)), block(256);
   auto s = stream();
+  if (doc_start.has_value() && doc_start->defined()) {
+    const at::Tensor& ds = *doc_start;
+    LLMCTL_CHECK(causal, "flash_attn_fwd: doc_start (packed sequences) needs causal attention");
+    LLMCTL_CHECK(ds.is_cuda() && ds.scalar_type() == at::kInt && ds.is_contiguous() && ds.dim() == 2 &&
+                     ds.size(0) == B && ds.size(1) == S,
+                 "flash_attn_fwd: doc_start must be contiguous int32 [B,S]");
+    a.doc = ds.data_ptr<int>();
+    if (D == 128) hipLaunchKernelGGL((fa_fwd_kernel<128, true, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<64, true, true>), grid, block, 0, s, a);
+    return {o, lse};
+  }
   if (D == 128) {
     if (causal) hipLaunchKernelGGL((fa_fwd_kernel<128, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((fa_fwd_kernel<128, false>), grid, block, 0, s, a);

@@ -174,13 +174,13 @@ def rope_qkv(qkv, cos, sin, nq: int, nkv: int, seq_len: int, positions: Optional
 # =============================================================================== attention
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, scale, causal):
+    def forward(ctx, q, k, v, scale, causal, doc_start):
         if use_native(q):
-            o, lse = native().flash_attn_fwd(q, k, v, scale, causal)
+            o, lse = native().flash_attn_fwd(q, k, v, scale, causal, doc_start)
         else:
-            o, lse = ref.attention_fwd(q, k, v, scale, causal)
+            o, lse = ref.attention_fwd(q, k, v, scale, causal, doc_start)
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.scale, ctx.causal = scale, causal
+        ctx.scale, ctx.causal, ctx.doc_start = scale, causal, doc_start
         return o
 
     @staticmethod
@@ -188,16 +188,18 @@ class _FlashAttn(torch.autograd.Function):
         q, k, v, o, lse = ctx.saved_tensors
         do = do.contiguous()
         if use_native(do):
-            dq, dk, dv = native().flash_attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
+            dq, dk, dv = native().flash_attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal, ctx.doc_start)
         else:
-            dq, dk, dv = ref.attention_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
-        return dq, dk, dv, None, None
+            dq, dk, dv = ref.attention_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal, ctx.doc_start)
+        return dq, dk, dv, None, None, None
 
 
-def flash_attention(q, k, v, causal: bool = True, softmax_scale: Optional[float] = None):
-    """Causal flash attention.  q ``[B,S,Hq,D]``, k/v ``[B,S,Hkv,D]`` (Hq % Hkv == 0)."""
+def flash_attention(q, k, v, causal: bool = True, softmax_scale: Optional[float] = None,
+                    doc_start: Optional[torch.Tensor] = None):
+    """Causal flash attention.  q ``[B,S,Hq,D]``, k/v ``[B,S,Hkv,D]`` (Hq % Hkv == 0).
+    ``doc_start`` (int32 ``[B,S]``, packed sequences): attention stays inside each document."""
     scale = softmax_scale if softmax_scale is not None else q.shape[-1] ** -0.5
-    return _FlashAttn.apply(q, k, v, scale, causal)
+    return _FlashAttn.apply(q, k, v, scale, causal, doc_start)
 
 
 # =============================================================================== MLP

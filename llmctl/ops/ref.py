@@ -123,7 +123,25 @@ def rope_qkv_bwd(dq, dk, dv, cos, sin, seq_len: int, positions=None):
 
 
 # ----------------------------------------------------------------------------- attention
-def attention_fwd(q, k, v, scale: float, causal: bool = True):
+def _doc_mask(doc_start, S: int, device):
+    """[B,1,S,S] visibility of packed documents: key j visible to query i iff doc_start[i] <= j."""
+    j = torch.arange(S, device=device)
+    return (j.view(1, 1, 1, S) >= doc_start.to(device).long().view(doc_start.shape[0], 1, S, 1))
+
+
+def document_starts(input_ids: torch.Tensor, separator: int) -> torch.Tensor:
+    """[B,S] position where each token's document begins; a document ends with (includes) the
+    ``separator`` token, the next one starts right after it."""
+    B, S = input_ids.shape
+    pos = torch.arange(S, device=input_ids.device).expand(B, S)
+    is_start = torch.zeros_like(input_ids, dtype=torch.bool)
+    is_start[:, 0] = True
+    is_start[:, 1:] = input_ids[:, :-1] == separator
+    starts = torch.where(is_start, pos, torch.zeros_like(pos))
+    return torch.cummax(starts, dim=1).values.to(torch.int32).contiguous()
+
+
+def attention_fwd(q, k, v, scale: float, causal: bool = True, doc_start=None):
     """q [B,S,Hq,D], k/v [B,S,Hkv,D] -> o [B,S,Hq,D], lse [B,Hq,S] (natural log)."""
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
@@ -136,13 +154,15 @@ def attention_fwd(q, k, v, scale: float, causal: bool = True):
     if causal:
         mask = torch.ones(S, Sk, dtype=torch.bool, device=q.device).tril(Sk - S)
         s = s.masked_fill(~mask, float("-inf"))
+    if doc_start is not None:
+        s = s.masked_fill(~_doc_mask(doc_start, S, q.device), float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
     p = torch.exp(s - lse.unsqueeze(-1))
     o = torch.matmul(p, vf).transpose(1, 2)
     return o.to(q.dtype).contiguous(), lse
 
 
-def attention_bwd(do, q, k, v, o, lse, scale: float, causal: bool = True):
+def attention_bwd(do, q, k, v, o, lse, scale: float, causal: bool = True, doc_start=None):
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
     rep = Hq // Hkv
@@ -156,6 +176,8 @@ def attention_bwd(do, q, k, v, o, lse, scale: float, causal: bool = True):
     if causal:
         mask = torch.ones(S, Sk, dtype=torch.bool, device=q.device).tril(Sk - S)
         s = s.masked_fill(~mask, float("-inf"))
+    if doc_start is not None:
+        s = s.masked_fill(~_doc_mask(doc_start, S, q.device), float("-inf"))
     p = torch.exp(s - lse.unsqueeze(-1))
     dv = torch.matmul(p.transpose(-1, -2), dof)
     dp = torch.matmul(dof, vf.transpose(-1, -2))

@@ -65,6 +65,8 @@ class TrainingConfig:
     tensor_parallel: int = 1
     pipeline_parallel: int = 1
     context_parallel: int = 1  # Ulysses CP: sequence split over cp ranks (llmctl.parallel.context_parallel)
+    pack_sequences: bool = False  # documents packed into sequences: attention/positions reset at separators
+    doc_separator: int = 0  # token that ends a document (byte tokenizer / tokenize_to_bin use 0)
     sequence_parallel: bool = False
     zero_stage: int = 0
     activation_checkpoint: str = "none"  # none | selective | full
@@ -132,6 +134,8 @@ class TrainingEngine:
             dist.init_process_group(backend=backend, **kw)
         if c.context_parallel > 1 and c.pipeline_parallel > 1:
             raise NotImplementedError("context_parallel with pipeline_parallel is not supported")
+        if c.pack_sequences and (c.context_parallel > 1 or c.pipeline_parallel > 1):
+            raise NotImplementedError("pack_sequences with context / pipeline parallelism is not supported")
         self.pg: ProcessGroups = build_process_groups(tp=c.tensor_parallel, pp=c.pipeline_parallel,
                                                       cp=c.context_parallel)
         self.rank = self.pg.rank
@@ -229,7 +233,14 @@ class TrainingEngine:
 
     # ------------------------------------------------------------------ step
     def _forward_backward(self, input_ids, labels, denom):
-        loss = self.model(input_ids, labels, loss_denom=denom)
+        doc_start = None
+        if self.config.pack_sequences:
+            from llmctl.ops.ref import document_starts
+
+            doc_start = document_starts(input_ids, self.config.doc_separator)
+            # a separator's next-token label belongs to the next document: not a target
+            labels = labels.masked_fill(input_ids == self.config.doc_separator, -100)
+        loss = self.model(input_ids, labels, loss_denom=denom, doc_start=doc_start)
         loss.backward()
         return loss.detach()
 

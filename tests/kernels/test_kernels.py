@@ -164,6 +164,49 @@ def test_flash_attn(native_lib, B, S, Hq, Hkv, D, causal):
     assert _rel(dq, dqr) < 3e-2, _rel(dq, dqr)
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(2, 384, 4, 2, 128), (1, 1000, 2, 2, 64), (2, 256, 4, 4, 128)])
+def test_flash_attn_packed_documents(native_lib, B, S, Hq, Hkv, D):
+    """Document-masked (packed) attention: a key is visible iff it is in the query's document."""
+    g = torch.Generator().manual_seed(S)
+    ids = torch.randint(1, 50, (B, S), generator=g)
+    for b in range(B):  # a few separators per row, incl. adjacent ones and one at the end
+        cut = torch.randint(0, S, (5,), generator=g)
+        ids[b, cut] = 0
+        ids[b, S - 1] = 0
+    ids[0, 10:12] = 0
+    doc = ref.document_starts(ids, 0).to(DEV)
+    q, k, v = _bf(B, S, Hq, D, seed=41), _bf(B, S, Hkv, D, seed=42), _bf(B, S, Hkv, D, seed=43)
+    scale = D ** -0.5
+    o, lse = native_lib.flash_attn_fwd(q, k, v, scale, True, doc)
+    orf, lser = ref.attention_fwd(q, k, v, scale, True, doc_start=doc)
+    assert _rel(o, orf) < 2e-2, _rel(o, orf)
+    assert torch.allclose(lse, lser, atol=2e-2, rtol=1e-3)
+    do = _bf(B, S, Hq, D, seed=44)
+    dq, dk, dv = native_lib.flash_attn_bwd(do, q, k, v, o, lse, scale, True, doc)
+    dqr, dkr, dvr = ref.attention_bwd(do, q, k, v, o, lse, scale, True, doc_start=doc)
+    assert _rel(dv, dvr) < 3e-2, _rel(dv, dvr)
+    assert _rel(dk, dkr) < 3e-2, _rel(dk, dkr)
+    assert _rel(dq, dqr) < 3e-2, _rel(dq, dqr)
+
+
+def test_packed_model_matches_separate_documents(native_lib):
+    """A packed row [d1 | d2] through the HIP model gives each document's standalone logits."""
+    from llmctl.models import get_model_config, build_model
+
+    cfg = get_model_config("tiny")
+    torch.manual_seed(0)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16)
+    d1 = torch.randint(1, cfg.vocab_size, (1, 70), device=DEV)
+    d1[0, -1] = 0
+    d2 = torch.randint(1, cfg.vocab_size, (1, 58), device=DEV)
+    packed = torch.cat([d1, d2], 1)
+    doc = ref.document_starts(packed, 0)
+    with torch.no_grad():
+        lp = m(packed, doc_start=doc).reshape(128, -1)
+        l1, l2 = m(d1).reshape(70, -1), m(d2).reshape(58, -1)
+    assert _rel(lp[:70], l1) < 2e-2 and _rel(lp[70:], l2) < 2e-2
+
+
 def test_flash_attn_forced_rescale(native_lib):
     """Spike one key so the running max jumps mid-sequence (guide rule 26)."""
     B, S, H, D = 1, 512, 2, 128
