@@ -66,6 +66,7 @@ def launch(
     max_steps: Optional[int] = typer.Option(None, help="Stop after N optimizer steps"),
     seq_len: Optional[int] = typer.Option(None, help="Sequence length"),
     max_restarts: int = typer.Option(0, help="Elastic restarts (auto-resume from the latest checkpoint)"),
+    save_steps: Optional[int] = typer.Option(None, help="Checkpoint every N steps"),
     device: Optional[str] = typer.Option(None, help="auto | cuda | cpu"),
     dry_run: bool = typer.Option(False, help="Dry run - show command without executing"),
 ) -> None:
@@ -86,6 +87,10 @@ def launch(
     args = build_worker_args(model, data, output_dir, batch_size, learning_rate, num_epochs, mixed_precision,
                              grad_accum, clip_grad, config, plan, checkpoint, max_steps, seq_len, rc.seed,
                              rc.deterministic, rc.log_level, device)
+    if save_steps:
+        args += ["--save-steps", str(save_steps)]
+    if max_restarts and not checkpoint:
+        args += ["--resume-from-checkpoint", "auto"]  # each (re)start resumes from <output_dir>/latest if present
     lc = LaunchConfig(nodes=nodes, gpus_per_node=gpus_per_node, launcher=launcher, mixed_precision=mixed_precision,
                       config_path=str(config) if config else None, data_path=str(data) if data else None,
                       plan_path=str(plan) if plan else None, checkpoint_path=checkpoint,

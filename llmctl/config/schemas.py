@@ -216,6 +216,11 @@ def resolve_training_config(train_file: Optional[Dict[str, Any]] = None, plan: O
             out["gradient_clipping"] = tr.gradient_clipping
         if tr.mixed_precision:
             out["mixed_precision"] = tr.mixed_precision
+        prof = (t.telemetry or {}).get("profiling") if isinstance(t.telemetry, dict) else None
+        if isinstance(prof, dict) and prof.get("enable"):
+            out["profile_dir"] = str(prof.get("dir", "profiles"))
+            if prof.get("schedule"):
+                out["profile_schedule"] = str(prof["schedule"])
         mx = t.data.get("max_length") if isinstance(t.data, dict) else None
         if mx:
             out["seq_len"] = int(mx)

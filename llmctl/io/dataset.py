@@ -86,6 +86,12 @@ class MemmapTokens:
         while True:
             yield self.next_batch()
 
+    def skip(self, n_batches: int) -> None:
+        """Resume: position after ``n_batches`` micro-batches of this rank (same epoch
+        roll-over rule as :meth:`next_batch`)."""
+        per_epoch = max((self.n_samples // self.world) // self.B, 1)
+        self.load_state_dict({"epoch": n_batches // per_epoch, "pos": (n_batches % per_epoch) * self.B})
+
     def state_dict(self):
         if self._native is not None:
             e, p = self._native.position()

@@ -32,6 +32,10 @@ class SyntheticTokens:
             yield self.batch(self.step)
             self.step += 1
 
+    def skip(self, n_batches: int) -> None:
+        """Resume: continue after ``n_batches`` already-consumed micro-batches."""
+        self.step += n_batches
+
     def state_dict(self):
         return {"step": self.step, "seed": self.seed, "rank": self.rank}
 

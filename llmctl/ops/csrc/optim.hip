@@ -5,7 +5,7 @@
 // bf16 param (14 B) — ~28 B/param, HBM-bound by design; 8 elements per lane (16-B bf16 and
 // 2×16-B fp32 vectors), grid-stride at ~8 blocks per CU.  The clip coefficient and the
 // 1/world DP average arrive as a device scalar (grad_scale), so clipping needs no host
-// synchronisation.
+// synchronisation.  A non-finite scale skips the update (overflow skip-step policy).
 //
 // l2norm_sq_: grid-stride sum of squares, one wave shuffle + LDS reduction per block and ONE
 // float atomic per block into the fp32 accumulator.
@@ -34,6 +34,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(unsigned short* __restrict__
                                                      float eps, float wd, float inv_bc1, float inv_sqrt_bc2,
                                                      const float* __restrict__ gscale) {
   const float gs = gscale ? gscale[0] : 1.f;
+  // non-finite grad scale (the optimizer passes NaN when the global grad norm overflowed):
+  // skip the whole update — params, master and moments stay untouched on every rank
+  if (!__builtin_isfinite(gs)) return;
   const float decay = 1.f - lr * wd;
   const float step = lr * inv_bc1;
   const long n8 = n >> 3;

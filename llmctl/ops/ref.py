@@ -280,7 +280,10 @@ def cross_entropy_bwd(dloss: torch.Tensor, logits: torch.Tensor, lse: torch.Tens
 # ----------------------------------------------------------------------------- optimizer
 def adamw_step_(param, master, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step,
                 grad_scale: float = 1.0):
-    """Decoupled-weight-decay Adam on an fp32 master copy; writes the bf16 param."""
+    """Decoupled-weight-decay Adam on an fp32 master copy; writes the bf16 param.  A
+    non-finite ``grad_scale`` skips the update (same policy as the HIP kernel)."""
+    if not math.isfinite(grad_scale):
+        return
     g = grad.float() * grad_scale
     bc1 = 1 - beta1 ** step
     bc2 = 1 - beta2 ** step

@@ -25,6 +25,7 @@ import torch.distributed as dist
 from llmctl.comms.overlap import GradSyncEngine
 from llmctl.models import ModelConfig, ParallelContext, build_model, get_model_config
 from llmctl.parallel.groups import ProcessGroups, build_process_groups
+from llmctl.runtime.faults import FaultInjector
 from llmctl.runtime.flat import FlatParameters
 from llmctl.runtime.optimizer import FlatAdamW, LRSchedule
 from llmctl.utils.env import dist_env
@@ -80,6 +81,9 @@ class TrainingConfig:
     async_checkpoint: bool = True
     sharded_checkpoint: bool = True
     keep_latest: int = 0
+    profile_dir: Optional[str] = None  # torch.profiler (ROCm/roctracer activities) Chrome traces per rank
+    profile_schedule: str = "wait=1,warmup=1,active=2"  # or "step(N)" (telemetry.profiling.schedule)
+    collective_timeout_s: float = 1800.0  # RCCL/gloo watchdog: a dead peer fails the job instead of hanging it
     plan_file: Optional[str] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -111,6 +115,7 @@ class TrainingEngine:
         self.consumed_samples = 0
         self.metrics_hooks: List = []
         self._build()
+        self.faults = FaultInjector(self.rank, c.output_dir)
 
     # ------------------------------------------------------------------ setup
     def _setup_distributed(self) -> None:
@@ -123,14 +128,24 @@ class TrainingEngine:
                 self.device = torch.device("cuda", self.env.local_rank)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+            if os.environ.get("LLMCTL_STREAM_CHECK") == "1":
+                # stream-race checker: every tensor access is tracked per stream and an access
+                # not ordered after the last conflicting one (event/wait_stream) raises
+                from torch.cuda._sanitizer import enable_cuda_sanitizer
+
+                enable_cuda_sanitizer()
         backend = c.distributed_backend
         if backend == "auto":
             backend = "nccl" if self.device.type == "cuda" else "gloo"
         self.backend = backend
         if self.env.world_size > 1 and not dist.is_initialized():
-            kw = {}
+            import datetime
+
+            kw = {"timeout": datetime.timedelta(seconds=c.collective_timeout_s)}
             if backend == "nccl":
                 kw["device_id"] = self.device
+                # surface collective timeouts/errors as exceptions (torchrun then restarts)
+                os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
             dist.init_process_group(backend=backend, **kw)
         if c.context_parallel > 1 and c.pipeline_parallel > 1:
             raise NotImplementedError("context_parallel with pipeline_parallel is not supported")
@@ -241,6 +256,8 @@ class TrainingEngine:
             # a separator's next-token label belongs to the next document: not a target
             labels = labels.masked_fill(input_ids == self.config.doc_separator, -100)
         loss = self.model(input_ids, labels, loss_denom=denom, doc_start=doc_start)
+        if self.faults and self.faults.nan_loss(self.global_step + 1):
+            loss = loss * float("nan")
         loss.backward()
         return loss.detach()
 
@@ -309,18 +326,28 @@ class TrainingEngine:
         from llmctl.runtime.replay import write_manifest
 
         c = self.config
-        data = data_iter if data_iter is not None else iter(self.make_data())
         ckpt = CheckpointManager(self, c.output_dir)
-        if c.resume_from_checkpoint:
-            ckpt.load(c.resume_from_checkpoint)
+        resume = c.resume_from_checkpoint
+        if resume == "auto":  # elastic restarts: newest complete checkpoint of this run, if any
+            resume = c.output_dir if (Path(c.output_dir) / "latest").exists() else None
+        if resume:
+            ckpt.load(resume)
         accum = max(c.gradient_accumulation_steps, 1)
         if self.pipeline is not None:
             accum = self.pipeline.num_microbatches
+        if data_iter is not None:
+            data = data_iter
+        else:
+            ds = self.make_data()
+            if self.global_step and hasattr(ds, "skip"):
+                ds.skip(self.global_step * accum)  # resume: continue the sample stream, not restart it
+            data = iter(ds)
         max_steps = c.max_steps if c.max_steps > 0 else None
         if max_steps is None:
             spe = c.samples_per_epoch or 1000 * c.batch_size
             steps_per_epoch = max(spe // (c.batch_size * accum * self.pg.layout.dp), 1)
             max_steps = steps_per_epoch * c.num_epochs
+        prof = self._make_profiler()
         tokens_per_step = c.batch_size * c.seq_len * accum * self.pg.layout.dp
         flops_per_token = self.model_config.flops_per_token(c.seq_len)
         t_last = time.time()
@@ -328,7 +355,12 @@ class TrainingEngine:
         history = []
         while self.global_step < max_steps:
             batches = [next(data) for _ in range(accum)]
-            out = self.train_step(batches)
+            if prof is not None:
+                with torch.profiler.record_function("llmctl.train_step"):
+                    out = self.train_step(batches)
+                prof.step()
+            else:
+                out = self.train_step(batches)
             s = self.global_step
             if s % c.logging_steps == 0 or s == max_steps:
                 if self.device.type == "cuda":
@@ -349,6 +381,8 @@ class TrainingEngine:
                              gn, rec["lr"], dt, tps, 100 * mfu)
                 for h in self.metrics_hooks:
                     h(rec)
+            if self.faults:
+                self.faults.after_step(s)
             if c.eval_steps and s % c.eval_steps == 0:
                 ev = [next(data) for _ in range(c.eval_batches)]
                 vl = self.evaluate(ev)
@@ -357,6 +391,8 @@ class TrainingEngine:
             if c.save_steps and s % c.save_steps == 0:
                 ckpt.save(f"checkpoint-{s}")
                 write_manifest(self, history)
+        if prof is not None:
+            prof.stop()
         ckpt.save("final", final=True)
         ckpt.wait()
         write_manifest(self, history, status="complete")
@@ -398,6 +434,35 @@ class TrainingEngine:
             for k, v in sd.items():
                 by_name.setdefault(k, {})[tp_rank] = v
         return {k: consolidate_tp(k, [s[i] for i in sorted(s)], self.model_config) for k, s in by_name.items()}
+
+    def _make_profiler(self):
+        """``torch.profiler`` over the schedule ``profile_schedule`` (``wait=a,warmup=b,active=c``
+        or the reference config's ``step(N)`` = profile step N); one Chrome trace per rank."""
+        c = self.config
+        if not c.profile_dir:
+            return None
+        import re
+
+        m = re.fullmatch(r"\s*step\((\d+)\)\s*", c.profile_schedule)
+        if m:
+            n = max(int(m.group(1)), 1)
+            kw = dict(wait=max(n - 2, 0), warmup=1 if n >= 2 else 0, active=1, repeat=1)
+        else:
+            kw = {k.strip(): int(v) for k, v in (x.split("=") for x in c.profile_schedule.split(",") if x.strip())}
+            kw.setdefault("repeat", 1)
+        out = Path(c.profile_dir)
+        out.mkdir(parents=True, exist_ok=True)
+        rank = self.rank
+
+        def ready(p):
+            p.export_chrome_trace(str(out / f"trace_rank{rank:05d}_step{self.global_step}.json"))
+
+        acts = [torch.profiler.ProfilerActivity.CPU]
+        if self.device.type == "cuda":
+            acts.append(torch.profiler.ProfilerActivity.CUDA)  # roctracer on ROCm
+        prof = torch.profiler.profile(activities=acts, schedule=torch.profiler.schedule(**kw), on_trace_ready=ready)
+        prof.start()
+        return prof
 
     def _peak_flops(self) -> float:
         if self.device.type == "cuda":

@@ -50,9 +50,10 @@ class LaunchConfig:
     gradient_accumulation_steps: int = 1
     gradient_clipping: float = 1.0
     master_addr: str = "127.0.0.1"
-    master_port: int = 29500
+    master_port: int = field(default_factory=lambda: int(os.environ.get("LLMCTL_MASTER_PORT", "29500")))
     node_rank: int = 0
     max_restarts: int = 0
+    debug: bool = False  # race/fault hunting: serialized kernels, blocking collectives, verbose RCCL
     extra_env: Dict[str, str] = field(default_factory=dict)
 
     def total_gpus(self) -> int:
@@ -80,6 +81,15 @@ class BaseLauncher(ABC):
             env["PYTHONHASHSEED"] = str(c.seed)
             env["HIP_LAUNCH_BLOCKING"] = "1"
             env["LLMCTL_DETERMINISTIC"] = "1"
+        if c.debug or os.environ.get("LLMCTL_DEBUG") == "1":
+            # every kernel completes before the next is launched (a fault points at its kernel),
+            # collectives block with the timeout (a hang becomes an error on the rank that hung)
+            env["AMD_SERIALIZE_KERNEL"] = "3"
+            env["AMD_SERIALIZE_COPY"] = "3"
+            env["HIP_LAUNCH_BLOCKING"] = "1"
+            env["TORCH_NCCL_BLOCKING_WAIT"] = "1"
+            env["NCCL_DEBUG"] = "INFO"
+            env["LLMCTL_STREAM_CHECK"] = "1"
         repo_root = str(Path(__file__).resolve().parents[2])
         env["PYTHONPATH"] = repo_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         env.update(c.extra_env)

@@ -72,6 +72,7 @@ class FlatAdamW:
         self.dp_sharded = False  # set by ZeRO-3: every rank holds a disjoint parameter shard
         self.step_count = 0
         dev = flat.device
+        self.skipped_steps = torch.zeros((), dtype=torch.int32, device=dev)  # non-finite-norm steps (device)
         if self.zero_stage == 0:
             self.master = flat.data.float().clone()
             self.exp_avg = torch.zeros_like(self.master)
@@ -151,6 +152,11 @@ class FlatAdamW:
             coef = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0) / grad_divisor
         else:
             coef = torch.ones_like(norm) / grad_divisor
+        # skip-step policy: a non-finite global norm (identical on every rank) turns the scale
+        # into NaN, which the fused kernel treats as "leave everything untouched"
+        finite = torch.isfinite(norm)
+        coef = torch.where(finite, coef, torch.full_like(coef, float("nan")))
+        self.skipped_steps = self.skipped_steps + (~finite).to(torch.int32)
         if self.zero_stage == 0:
             for pv, ms, g, m, v, decay, region in self._segments():
                 ops.adamw_step_(pv, ms, g, m, v, lr=lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,

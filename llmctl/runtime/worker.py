@@ -68,6 +68,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device", type=str, default=S)
     p.add_argument("--metrics-jsonl", type=str, default=S)
     p.add_argument("--prometheus-port", type=int, default=S)
+    p.add_argument("--pack-sequences", action="store_true", default=S, help="document-masked packed sequences")
+    p.add_argument("--profile-dir", type=str, default=S, help="torch.profiler Chrome traces per rank")
+    p.add_argument("--profile-schedule", type=str, default=S, help="wait=a,warmup=b,active=c | step(N)")
+    p.add_argument("--collective-timeout-s", type=float, default=S)
     return p
 
 

@@ -127,3 +127,26 @@ def test_health_check_json(tmp_path):
     rep = tmp_path / "h.json"
     _ok(llmctl("health", "check", "--component", "system", "--save-report", str(rep)))
     assert "system" in json.loads(rep.read_text())
+
+
+def test_elastic_restart_after_rank_kill(tmp_path):
+    """Fault injection (LLMCTL_FAULT) kills rank 1 after step 3 of a 2-process gloo run; the
+    elastic restart resumes from checkpoint-2 and finishes all 5 steps."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "run"
+    env = dict(os.environ, PYTHONPATH=str(ROOT), LLMCTL_DEVICE="cpu", LLMCTL_FAULT="kill_rank:1@step:3",
+               LLMCTL_MASTER_PORT=str(port), OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "llmctl", "train", "launch", "--model", "tiny", "--device", "cpu",
+                        "--gpus-per-node", "2", "--max-steps", "5", "--batch-size", "2", "--seq-len", "32",
+                        "--save-steps", "2", "--max-restarts", "1", "--mixed-precision", "fp32",
+                        "--output-dir", str(out)], capture_output=True, text=True, env=env, timeout=900)
+    _ok(r)
+    assert (out / ".faults" / "kill_rank-1-3").exists()
+    st = json.loads((out / "final" / "training_state.json").read_text())
+    assert st["global_step"] == 5
+    man = json.loads((out / "run_manifest.json").read_text())
+    assert man["status"] == "complete"

@@ -130,6 +130,18 @@ def test_adamw(native_lib, n, gdt):
     assert torch.equal(p, master.to(torch.bfloat16))
 
 
+def test_adamw_nonfinite_scale_skips(native_lib):
+    n = 4096 + 5
+    master = torch.randn(n, device=DEV)
+    p = master.to(torch.bfloat16)
+    g = torch.randn(n, device=DEV)
+    m, v = torch.randn(n, device=DEV), torch.rand(n, device=DEV)
+    snap = [t.clone() for t in (p, master, m, v)]
+    native_lib.adamw_step_(p, master, g, m, v, 1e-3, 0.9, 0.95, 1e-8, 0.1, 0.1, 0.05,
+                           torch.tensor([float("nan")], device=DEV))
+    assert all(torch.equal(a, b) for a, b in zip((p, master, m, v), snap))
+
+
 def test_l2norm(native_lib):
     x = _bf(1 << 20, seed=3)
     out = torch.zeros(1, device=DEV)

@@ -202,3 +202,43 @@ def test_engine_pack_sequences_step():
     assert np.isfinite(l_sep)
     with pytest.raises(NotImplementedError):
         TrainingEngine(_config(pack_sequences=True, context_parallel=2))
+
+
+def test_nonfinite_grad_skips_step(monkeypatch, tmp_path):
+    """nan_grad fault on step 2: the fused AdamW leaves params/moments untouched and counts
+    the skipped step; steps 1 and 3 update normally."""
+    from llmctl.testing.workers import _config
+    from llmctl.runtime.engine import TrainingEngine
+
+    monkeypatch.setenv("LLMCTL_FAULT", "nan_grad@step:2")
+    eng = TrainingEngine(_config(output_dir=str(tmp_path)))
+    g = torch.Generator().manual_seed(0)
+    batch = lambda: [(torch.randint(1, 500, (2, 32), generator=g), torch.randint(1, 500, (2, 32), generator=g))]
+    eng.train_step(batch())
+    before = eng.flat.data.clone(), eng.optimizer.exp_avg.clone()
+    out = eng.train_step(batch())
+    assert not torch.isfinite(out["grad_norm"]).item()
+    assert torch.equal(eng.flat.data, before[0]) and torch.equal(eng.optimizer.exp_avg, before[1])
+    assert int(eng.optimizer.skipped_steps) == 1
+    eng.train_step(batch())
+    assert not torch.equal(eng.flat.data, before[0])
+
+
+def test_fault_spec_parse():
+    from llmctl.runtime.faults import parse
+
+    f = parse("kill_rank:3@step:50, nan_grad@step:2")
+    assert (f[0].kind, f[0].rank, f[0].step) == ("kill_rank", 3, 50) and f[1].rank is None
+    with pytest.raises(ValueError):
+        parse("explode@now")
+
+
+def test_scheduled_profiler_writes_trace(tmp_path):
+    from llmctl.testing.workers import _config
+    from llmctl.runtime.engine import TrainingEngine
+
+    eng = TrainingEngine(_config(output_dir=str(tmp_path / "run"), max_steps=4, save_steps=0, eval_steps=0,
+                                 profile_dir=str(tmp_path / "prof"), profile_schedule="step(3)", logging_steps=2))
+    eng.train()
+    traces = list((tmp_path / "prof").glob("trace_rank00000_step*.json"))
+    assert len(traces) == 1 and "llmctl.train_step" in traces[0].read_text()
