@@ -104,5 +104,29 @@ __device__ __forceinline__ bf16x8_t to_bf16x8(const float* x) {
 
 __device__ __forceinline__ uint4 gload16(const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// ---- LDS DMA (global_load_lds) ---------------------------------------------------------------
+// One wave-instruction writes 64 lanes x {16, 4} B to LDS bytes [lds_byte, +1024 / +256),
+// lane-linear; the global source address is per lane (a swizzled image is built by permuting
+// the SOURCE, guide §5.4 rule 21).  Inline asm: through the builtin, hipcc drains vmcnt(0)
+// before every later ds_read; here ordering is explicit (counted vmcnt + s_barrier).
+__device__ __forceinline__ void dma16(const void* g, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_byte) : "memory");
+}
+__device__ __forceinline__ void dma4(const void* g, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds_byte) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N <= 15, "vmcnt immediate");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  else static_assert(N == 0 || N == 5 || N == 9, "add the immediate");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p);
+}
+
 }  // namespace attn
 }  // namespace llmctl

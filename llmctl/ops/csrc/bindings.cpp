@@ -36,7 +36,7 @@ TORCH_LIBRARY(llmctl, m) {
   // attention (flash_attn_fwd.hip / flash_attn_bwd.hip)
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, Tensor? doc_start=None) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, Tensor? doc_start=None) -> (Tensor, Tensor, Tensor)");
-  m.def("fa_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq_acc, Tensor(b!) dk, Tensor(c!) dv, int abl) -> ()");
+  m.def("fa_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor delta, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int abl) -> ()");
   // serving (paged_attn.hip, sampling.hip)
   m.def("kv_cache_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot_mapping) -> ()");
   m.def("paged_attention_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, float scale) -> Tensor");

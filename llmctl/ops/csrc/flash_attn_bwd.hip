@@ -1,38 +1,52 @@
-// Flash-attention backward (causal / full, GQA) for gfx950 — MFMA 32x32x16 bf16.
+// Flash-attention backward (causal / full, GQA, packed documents) for gfx950 — MFMA 32x32x16 bf16.
 //
-// Algorithm (CDNA guide App. B "Attention backward"): recompute P from Q, K and the
-// forward's LSE; five MFMA products per tile:
-//     S = Q K^T,  dP = dO V^T,  dV^T += dO^T P,  dK^T += Q^T dS,  dQ += dS K
-// Structure:
-//   * workgroup = 4 waves = 128 keys of one (batch, kv-head); wave w owns keys
-//     [32w, 32w+32) and keeps dK^T / dV^T for them in registers across ALL query tiles and
-//     ALL q-heads of its GQA group (no cross-workgroup sum for dK/dV);
-//   * keys on the MFMA lane: S and dP accumulators are directly the B operands of the dV^T
-//     and dK^T products (accumulator-as-operand, no LDS round trip);
-//   * one LDS image per tile for K, V, Q, dO (XOR-swizzled "tr image": conflict-free for
-//     both ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads, guide T10);
-//   * only dS crosses LDS (as dS^T, 64-B rows), for dQ = dS K, which is split over the 4
-//     waves by d-block and accumulated with fp32 atomics (two 128-B row segments per
-//     wave-instruction = the full atomic rate, guide "Global float atomics");
-//   * LSE / delta are folded in as per-row constants; exp2 domain throughout.
-// A pre-kernel computes delta = rowsum(dO*O) and a post-kernel converts dQ (fp32) to bf16.
+// Recompute P from Q, K and the forward's LSE (CDNA guide App. B "Attention backward"):
+//     S = Q K^T,  P = exp(scale S - lse),  dP = dO V^T,  dS = P (dP - delta),
+//     dV = P^T dO,  dK = scale dS^T Q,  dQ = scale dS K          (delta = rowsum(dO * O))
+//
+// Two kernels, no atomics (the fused single-pass form summed dQ across key-block workgroups with
+// fp32 atomics: 16 KB of atomic adds per 32x128 tile, ~3.4 GB per GPT-7B layer at mb 12, i.e. the
+// ~1.3 TB/s chip-wide atomic rate alone was 2.6 ms of its 3.4 ms; MI355X_MICROARCH "Global float
+// atomics").  Splitting costs 2 extra MFMA products (S and dP recomputed for dQ: 7 instead of 5)
+// and buys: no dQ fp32 buffer memset / conversion pass, no dS LDS exchange, no atomics, and a
+// shorter dependency chain in each kernel.
+//
+// fa_bwd_dkv_kernel — key-stationary: workgroup = 4 waves = 128 keys of one (batch, kv-head);
+//   wave w owns keys [32w, 32w+32): their K / V fragments live in registers (B operands) and
+//   dK^T / dV^T accumulate in registers across all query tiles of all q-heads of the GQA group.
+//   Keys on the MFMA lane: the S / dP accumulators are directly the B operands of the dV^T and
+//   dK^T products (accumulator-as-operand, guide §3).  Query tiles of 64 rows (two independent
+//   32-row halves per wave: ILP between the MFMA chains and the exp/VALU work) stream through a
+//   3-deep LDS ring filled by LDS-DMA (global_load_lds_dwordx4, source-swizzled "tr image" read
+//   by ds_read_b128 rows AND ds_read_b64_tr_b16 columns, guide T10), one tile in flight across
+//   each raw s_barrier behind a counted vmcnt; lse / delta (/ document starts) ride in the same
+//   DMA ring as 256-B row-constant vectors.
+// fa_bwd_dq_kernel — query-stationary, the forward's structure: workgroup = 4 waves = 128 query
+//   rows of one (batch, q-head), Q and dO fragments in registers, K/V tiles of 64 keys staged
+//   through LDS (register staging split around the MFMAs, guide T14); "swapped" products keep the
+//   key on the registers so dS^T is directly the B operand of dQ^T += K^T dS^T.  dQ is written
+//   once, in bf16.
+// A pre-kernel computes delta.
 #include "attn_common.h"
 
 namespace llmctl {
 using namespace attn;
 namespace {
 
-constexpr int KBLK = 128;  // keys per workgroup
-constexpr int QT = 32;     // query rows per iteration
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr int KV_KB = 128;  // keys per dK/dV workgroup
+constexpr int KV_QT = 64;   // query rows per streamed tile
+constexpr int KV_NBUF = 3;  // LDS ring depth
+constexpr int DQ_QB = 128;  // query rows per dQ workgroup
+constexpr int DQ_KB = 64;   // keys per dQ tile
 
 struct BwdArgs {
-  const unsigned short *q, *k, *v, *o, *dout;
+  const unsigned short *q, *k, *v, *dout;
   const float* lse;    // [B,Hq,S] natural log
   const float* delta;  // [B,Hq,S]
-  float* dq_acc;       // [B,S,Hq,HD] fp32 (contiguous)
-  unsigned short *dk, *dv;  // [B,S,Hkv,HD] contiguous
+  unsigned short *dq, *dk, *dv;  // [B,S,H,HD] contiguous
   int B, S, Hq, Hkv;
-  long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh, do_sb, do_ss, do_sh;
+  long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, do_sb, do_ss, do_sh;
   float scale, scale_log2;
   const int* doc;  // [B, S] document start per token (packed sequences), or nullptr
 };
@@ -65,66 +79,57 @@ __global__ __launch_bounds__(256) void delta_kernel(const unsigned short* __rest
   if (row < R && sub == 0) delta[((long)b * Hq + hq) * S + sq] = s;
 }
 
-__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ x, unsigned short* __restrict__ y,
-                                                           long n8) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n8) return;
-  float v[8];
-  *reinterpret_cast<float4*>(v) = reinterpret_cast<const float4*>(x + i * 8)[0];
-  *reinterpret_cast<float4*>(v + 4) = reinterpret_cast<const float4*>(x + i * 8)[1];
-  store8(y + i * 8, v);
+__device__ __forceinline__ void store_bf16x4(unsigned short* p, const float* x, float mul) {
+  unsigned short w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = f2bf(x[j] * mul);
+  *reinterpret_cast<uint2*>(p) =
+      make_uint2((unsigned)w[0] | ((unsigned)w[1] << 16), (unsigned)w[2] | ((unsigned)w[3] << 16));
 }
 
-// ABL: timing ablations for tools/attn_bench.py (results wrong): 1 no dQ atomics,
-// 2 no dQ product (and no dS^T exchange), 4 no Q/dO prefetch (tile 0 reused)
-template <int HD, bool CAUSAL, int ABL = 0, bool DOC = false>
-__global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
+// =============================================================================================
+// dK / dV
+// =============================================================================================
+template <int HD, bool CAUSAL, bool DOC>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
   constexpr int NKS = HD / 16;
   constexpr int NDB = HD / 32;
   constexpr int ROWB = HD * 2;
-  constexpr int CPR = HD / 8;
-  constexpr int KV_ITERS = KBLK * CPR / 256;  // 8 for HD=128
-  constexpr int Q_ITERS = QT * CPR / 256;     // 2 for HD=128
-  constexpr int DST_ROWB = QT * 2;            // dS^T rows: 32 q * 2 B = 64 B
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * KBLK * ROWB + 4 * QT * ROWB + KBLK * DST_ROWB +
-                                                             6 * QT * 4];
-  unsigned char* Ks = smem;
-  unsigned char* Vs = Ks + KBLK * ROWB;
-  unsigned char* Qbuf = Vs + KBLK * ROWB;       // [2][QT][HD] double-buffered Q tiles
-  unsigned char* Dbuf = Qbuf + 2 * QT * ROWB;   // [2][QT][HD] double-buffered dO tiles
-  unsigned char* St = Dbuf + 2 * QT * ROWB;     // dS^T [key][q]
-  float* lse_buf = reinterpret_cast<float*>(St + KBLK * DST_ROWB);  // [2][QT]
-  float* del_buf = lse_buf + 2 * QT;                                 // [2][QT]
-  int* doc_buf = reinterpret_cast<int*>(del_buf + 2 * QT);           // [2][QT] (packed documents)
+  constexpr int TILE_B = KV_QT * ROWB;     // one Q (or dO) tile
+  constexpr int NP = TILE_B / 1024 / 4;    // 1-KiB DMA pieces per wave per operand
+  constexpr int VM = 2 * NP + 1;           // DMA instructions per wave per tile
+  constexpr int RC_B = KV_QT * 4;          // one row-constant vector
+  constexpr int BUF_B = 2 * TILE_B + 4 * RC_B;  // Q | dO | lse | delta | doc | (dummy)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[KV_NBUF * BUF_B];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int BH = a.B * a.Hkv;
   const int bh = blockIdx.x % BH;
   const int kblk = blockIdx.x / BH;  // small kblk = most query tiles under causal: dispatched first
   const int b = bh / a.Hkv, hk = bh % a.Hkv;
   const int group = a.Hq / a.Hkv;
-  const int k0 = kblk * KBLK;
-  const int wkey0 = k0 + wave * 32;  // this wave's first key
+  const int k0 = kblk * KV_KB;
+  const int wkey0 = k0 + wave * 32;
   const int my_key = wkey0 + r;
 
-  const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh;
-  const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh;
-
-  // ---- stage this block's K and V (tr images) once
+  // ---- this wave's K / V fragments (B operands): lane holds X[my_key][16ks + 8hh + j]
+  bf16x8_t kf[NKS], vf[NKS];
+  {
+    const int kc = min(my_key, a.S - 1);  // keys past S: real finite data, P masked to 0
+    const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh + (long)kc * a.k_ss + 8 * hh;
+    const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh + (long)kc * a.v_ss + 8 * hh;
 #pragma unroll
-  for (int it = 0; it < KV_ITERS; ++it) {
-    const int c = tid + 256 * it;
-    const int row = c / CPR, ch = c % CPR;
-    const int key = k0 + row;
-    uint4 kk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (key < a.S) {
-      kk = gload16(Kp + (long)key * a.k_ss + ch * 8);
-      vv = gload16(Vp + (long)key * a.v_ss + ch * 8);
+    for (int ks = 0; ks < NKS; ++ks) {
+      kf[ks] = __builtin_bit_cast(bf16x8_t, gload16(Kp + 16 * ks));
+      vf[ks] = __builtin_bit_cast(bf16x8_t, gload16(Vp + 16 * ks));
     }
-    *reinterpret_cast<uint4*>(Ks + tr_off<HD>(row, ch)) = kk;
-    *reinterpret_cast<uint4*>(Vs + tr_off<HD>(row, ch)) = vv;
+    // retire these loads HERE: a compiler wait inside the tile loop would be a vmcnt(0) that also
+    // drains the (compiler-invisible) LDS-DMA prefetch of the next tile
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(kf[ks]), "v"(vf[ks]));
   }
 
   f32x16 dk[NDB], dv[NDB];
@@ -133,197 +138,121 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[d][i] = dv[d][i] = 0.f;
 
-  // flattened (q-head of the GQA group, query tile) sequence; the next tile's Q / dO / lse /
-  // delta are prefetched into registers while the current one is computed (register staging,
-  // guide T14) and written to the other LDS buffer after it
-  const int q_start = CAUSAL ? (k0 / QT) * QT : 0;
+  const int q_start = CAUSAL ? k0 : 0;  // k0 is a multiple of KV_QT
   int q_end = a.S;
   if constexpr (DOC) {
-    // queries whose document starts after this block's last key see none of its keys:
-    // q_end = first position with doc_start > k0 + KBLK - 1 (doc_start is non-decreasing)
+    // queries whose document starts after this block's last key see none of its keys
     const int* ds = a.doc + (long)b * a.S;
-    int lo = min(k0 + KBLK, a.S), hi = a.S;
+    int lo = min(k0 + KV_KB, a.S), hi = a.S;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (ds[mid] > k0 + KBLK - 1) hi = mid;
+      if (ds[mid] > k0 + KV_KB - 1) hi = mid;
       else lo = mid + 1;
     }
     q_end = lo;
   }
-  const int nq = q_end > q_start ? (q_end - q_start + QT - 1) / QT : 0;
+  const int nq = q_end > q_start ? (q_end - q_start + KV_QT - 1) / KV_QT : 0;
   const int ntiles = group * nq;
-  uint4 pq[Q_ITERS], pd[Q_ITERS];
-  float pl = 0.f, pdl = 0.f;
-  int pds = 0;
-  // unconditional loads (rows past S clamped to S-1: their P is masked to 0, so they add
-  // nothing): no zero-init + branch, which made hipcc drain vmcnt at every fetch
-  auto fetch = [&](int t) {
+  const unsigned lds0 = lds_addr(smem);
+
+  // ---- DMA of tile t into ring slot t % 3: every wave issues exactly VM instructions
+  auto issue = [&](int t) {
     const int g = t / nq;
-    const int q0 = q_start + (t - g * nq) * QT;
+    const int q0 = q_start + (t - g * nq) * KV_QT;
     const int hq = hk * group + g;
+    const unsigned slot = lds0 + (unsigned)((t % KV_NBUF) * BUF_B);
     const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh;
     const unsigned short* Dp = a.dout + b * a.do_sb + hq * a.do_sh;
 #pragma unroll
-    for (int it = 0; it < Q_ITERS; ++it) {
-      const int c = tid + 256 * it;
-      const int row = c / CPR, ch = c % CPR;
-      const int qq = min(q0 + row, a.S - 1);
-      pq[it] = gload16(Qp + (long)qq * a.q_ss + ch * 8);
-      pd[it] = gload16(Dp + (long)qq * a.do_ss + ch * 8);
+    for (int i = 0; i < NP; ++i) {
+      const int piece = i * 4 + wave;
+      const int byte = piece * 1024 + lane * 16;
+      const int row = byte / ROWB;
+      const int pch = (byte % ROWB) >> 4;                // physical chunk in the tr image
+      const int lch = pch ^ swz_tr<HD>(row);             // logical chunk it holds
+      const long qq = min(q0 + row, a.S - 1);            // rows past S: P masked to 0
+      dma16(Qp + qq * a.q_ss + lch * 8, slot + piece * 1024);
+      dma16(Dp + qq * a.do_ss + lch * 8, slot + TILE_B + piece * 1024);
     }
-    if (tid < QT) {
-      const int qq = min(q0 + tid, a.S - 1);
-      const long base = ((long)b * a.Hq + hq) * a.S;
-      pl = a.lse[base + qq];  // scaled to log2 at commit (no use of the load here)
-      pdl = a.delta[base + qq];
-      if constexpr (DOC) pds = a.doc[(long)b * a.S + qq];
-    }
+    const int qq = min(q0 + lane, a.S - 1);
+    const long rc = ((long)b * a.Hq + hq) * a.S + qq;
+    const void* src = wave == 1 ? (const void*)(a.delta + rc)
+                    : (DOC && wave == 2) ? (const void*)(a.doc + (long)b * a.S + qq)
+                                         : (const void*)(a.lse + rc);
+    dma4(src, slot + 2 * TILE_B + wave * RC_B);
   };
-  auto commit = [&](int buf) {
-    unsigned char* Qs = Qbuf + buf * QT * ROWB;
-    unsigned char* Ds = Dbuf + buf * QT * ROWB;
-#pragma unroll
-    for (int it = 0; it < Q_ITERS; ++it) {
-      const int c = tid + 256 * it;
-      const int row = c / CPR, ch = c % CPR;
-      *reinterpret_cast<uint4*>(Qs + tr_off<HD>(row, ch)) = pq[it];
-      *reinterpret_cast<uint4*>(Ds + tr_off<HD>(row, ch)) = pd[it];
-    }
-    if (tid < QT) {
-      lse_buf[buf * QT + tid] = pl * 1.4426950408889634f;
-      del_buf[buf * QT + tid] = pdl;
-      if constexpr (DOC) doc_buf[buf * QT + tid] = pds;
-    }
-  };
-  if (ntiles > 0) {
-    fetch(0);
-    commit(0);
-  }
-  __syncthreads();
 
+  if (ntiles > 0) issue(0);
+  if (ntiles > 1) issue(1);
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    const int g = t / nq;
-    const int q0 = q_start + (t - g * nq) * QT;
-    const int hq = hk * group + g;
-    float* dq_p = a.dq_acc + (long)b * a.S * a.Hq * HD + (long)hq * HD;
-    const unsigned char* Qs = Qbuf + buf * QT * ROWB;
-    const unsigned char* Ds = Dbuf + buf * QT * ROWB;
-    const float* lse_s = lse_buf + buf * QT;
-    const float* del_s = del_buf + buf * QT;
-    const int* doc_s = doc_buf + buf * QT;
-    // packed documents: the tile's smallest / largest document start (non-decreasing)
-    const int dmin = DOC ? doc_s[0] : 0, dmax = DOC ? doc_s[QT - 1] : 0;
-    if (!(ABL & 4) && t + 1 < ntiles) fetch(t + 1);  // in flight during this tile's MFMAs
+    if (t + 1 < ntiles) vm_wait<VM>();  // this wave's DMA of tile t landed (t+1 stays in flight)
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();       // ... and every other wave's; slot (t+2)%3 is free
+    if (t + 2 < ntiles) issue(t + 2);
 
-    const bool active = !(CAUSAL && wkey0 > q0 + QT - 1) && wkey0 < a.S && !(DOC && wkey0 + 31 < dmin);
-    float pbuf[16], dsbuf[16];
-    if (active) {
-      // ---- S = Q K^T and dP = dO V^T   (q on regs, key on lane)
+    const int g = t / nq;
+    const int q0 = q_start + (t - g * nq) * KV_QT;
+    const unsigned char* Qs = smem + (t % KV_NBUF) * BUF_B;
+    const unsigned char* Ds = Qs + TILE_B;
+    const float* lse_s = reinterpret_cast<const float*>(Ds + TILE_B);
+    const float* del_s = lse_s + KV_QT;
+    const int* doc_s = reinterpret_cast<const int*>(del_s + KV_QT);
+    // no early-out for tiles a wave sees nothing of (only the first tile of a causal block, for
+    // half the waves): a branch here makes hipcc shuttle dK/dV between AGPRs and VGPRs every tile
+
+    // ---- per 32-row half: S = Q K^T, dP = dO V^T (q on regs, key on lane), then
+    //      dV^T += dO^T P and dK^T += Q^T dS (sum over the half's rows = the registers).
+    //      Masks are branch-free selects; the halves are independent MFMA chains.
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
       f32x16 s, dp;
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8_t qa = lds_read_b128(Qs, tr_off<HD>(r, 2 * ks + hh));
-        const bf16x8_t kb = lds_read_b128(Ks, tr_off<HD>(wave * 32 + r, 2 * ks + hh));
-        s = mfma32(qa, kb, s);
-        const bf16x8_t da = lds_read_b128(Ds, tr_off<HD>(r, 2 * ks + hh));
-        const bf16x8_t vb = lds_read_b128(Vs, tr_off<HD>(wave * 32 + r, 2 * ks + hh));
-        dp = mfma32(da, vb, dp);
+        const bf16x8_t qa = lds_read_b128(Qs, tr_off<HD>(32 * h + r, 2 * ks + hh));
+        const bf16x8_t da = lds_read_b128(Ds, tr_off<HD>(32 * h + r, 2 * ks + hh));
+        s = mfma32(qa, kf[ks], s);
+        dp = mfma32(da, vf[ks], dp);
       }
-      const bool need_mask = (CAUSAL && wkey0 + 31 > q0) || (q0 + QT > a.S) || (wkey0 + 32 > a.S) ||
-                             (DOC && wkey0 < dmax);
+      float p[16], dsv[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = acc_row(i, hh);
-        float p = fast_exp2(s[i] * a.scale_log2 - lse_s[qi]);
-        if (need_mask) {
-          const int qq = q0 + qi;
-          if ((CAUSAL && my_key > qq) || qq >= a.S || my_key >= a.S || (DOC && my_key < doc_s[qi])) p = 0.f;
+      for (int gq = 0; gq < 4; ++gq) {
+        const int row0 = 32 * h + 8 * gq + 4 * hh;  // rows of registers 4gq .. 4gq+3
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + row0);
+        const float4 d4 = *reinterpret_cast<const float4*>(del_s + row0);
+        int4 s4 = make_int4(0, 0, 0, 0);
+        if constexpr (DOC) s4 = *reinterpret_cast<const int4*>(doc_s + row0);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+        const int sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * gq + j;
+          const int qq = q0 + row0 + j;
+          bool dead = (qq >= a.S) | (my_key >= a.S);
+          if constexpr (CAUSAL) dead |= my_key > qq;
+          if constexpr (DOC) dead |= my_key < sv[j];
+          const float pv = dead ? 0.f : fast_exp2(s[i] * a.scale_log2 - lv[j] * LOG2E);
+          p[i] = pv;
+          dsv[i] = pv * (dp[i] - dv4[j]);
         }
-        pbuf[i] = p;
-        dsbuf[i] = p * (dp[i] - del_s[qi]) * a.scale;
       }
-      // ---- dV^T += dO^T P ; dK^T += Q^T dS
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        const bf16x8_t pb = to_bf16x8(pbuf + 8 * st);
-        const bf16x8_t sb = to_bf16x8(dsbuf + 8 * st);
+        const bf16x8_t pb = to_bf16x8(p + 8 * st);
+        const bf16x8_t sb = to_bf16x8(dsv + 8 * st);
 #pragma unroll
         for (int d = 0; d < NDB; ++d) {
-          const bf16x8_t da = tr_frag<HD>(Ds, 16 * st, d * 32, lane);
+          const bf16x8_t da = tr_frag<HD>(Ds, 32 * h + 16 * st, d * 32, lane);
           dv[d] = mfma32(da, pb, dv[d]);
-          const bf16x8_t qa = tr_frag<HD>(Qs, 16 * st, d * 32, lane);
+          const bf16x8_t qa = tr_frag<HD>(Qs, 32 * h + 16 * st, d * 32, lane);
           dk[d] = mfma32(qa, sb, dk[d]);
         }
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dsbuf[i] = 0.f;
     }
-    // ---- dS^T -> LDS [key][q] (64-B rows): lane = key, 4 groups of 4 contiguous q
-    {
-      unsigned char* rowp = St + (wave * 32 + r) * DST_ROWB;
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int qc = 8 * gq + 4 * hh;
-        unsigned short w4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w4[j] = f2bf(dsbuf[4 * gq + j]);
-        *reinterpret_cast<uint2*>(rowp + qc * 2) =
-            make_uint2((unsigned)w4[0] | ((unsigned)w4[1] << 16), (unsigned)w4[2] | ((unsigned)w4[3] << 16));
-      }
-    }
-    lds_sync();
-    // ---- dQ[q][d] += dS K over this block's 128 keys; waves split the d-blocks
-    {
-      constexpr int WPD = 4 / NDB;  // waves per d-block (1 for HD=128, 2 for HD=64)
-      const int d = wave / WPD;
-      const int kpart = wave % WPD;
-      constexpr int KSTEPS = KBLK / 16 / WPD;
-      // skip if every key of this block is above this q tile's diagonal (all dS zero)
-      if (!(ABL & 2) && !(CAUSAL && k0 > q0 + QT - 1) && !(DOC && k0 + KBLK - 1 < dmin)) {
-        f32x16 acc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KSTEPS; ++ks) {
-          const int key0 = (kpart * KSTEPS + ks) * 16;
-          // A = dS[q][key]: from dS^T image X[key][q] (64-B rows, plain layout)
-          const int i16 = lane & 15, qq4 = i16 >> 2, p = i16 & 3;
-          const int col = 16 * ((lane >> 4) & 1) + 4 * p;  // q column
-          const int r1 = key0 + 8 * hh + qq4;
-          s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(St + r1 * DST_ROWB + col * 2));
-          s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(St + (r1 + 4) * DST_ROWB + col * 2));
-          s8_t av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          const bf16x8_t af = __builtin_bit_cast(bf16x8_t, av);
-          // B = K[key][d] with d on the lane
-          const bf16x8_t bf = tr_frag_nat<HD>(Ks, key0, d * 32, lane);
-          acc = mfma32(af, bf, acc);
-        }
-        // the next tile's Q / dO go to the other buffer BEFORE the atomics are issued, so
-        // the wait for the prefetch loads is not a wait for the (younger) atomics; that
-        // buffer was last read during tile t-1, before this tile's first barrier
-        if (!(ABL & 4) && t + 1 < ntiles) commit(buf ^ 1);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qq = q0 + acc_row(i, hh);
-          if constexpr (ABL & 1) {
-            asm volatile("" ::"v"(acc[i]));
-          } else {
-            // unconditional (rows past S add 0 to row S-1): a branch per atomic makes
-            // hipcc's vmcnt accounting assume they may not exist and drain them early
-            atomicAdd(dq_p + (long)min(qq, a.S - 1) * a.Hq * HD + d * 32 + r, qq < a.S ? acc[i] : 0.f);
-          }
-        }
-      } else if (!(ABL & 4) && t + 1 < ntiles) {
-        commit(buf ^ 1);
-      }
-    }
-    lds_sync();  // LDS-only: the dQ atomics and the next tile's loads stay in flight
   }
-  // ---- write dK, dV (bf16) for this wave's keys: lane = key, regs = d
+  // ---- write dK (scaled), dV: lane = key, registers = d
   if (my_key < a.S) {
     unsigned short* dkp = a.dk + ((long)b * a.S + my_key) * a.Hkv * HD + (long)hk * HD;
     unsigned short* dvp = a.dv + ((long)b * a.S + my_key) * a.Hkv * HD + (long)hk * HD;
@@ -332,18 +261,196 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         const int col = d * 32 + 8 * gq + 4 * hh;
-        unsigned short k4[4], v4[4];
+        float kx[4], vx[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          k4[j] = f2bf(dk[d][4 * gq + j]);
-          v4[j] = f2bf(dv[d][4 * gq + j]);
+          kx[j] = dk[d][4 * gq + j];
+          vx[j] = dv[d][4 * gq + j];
         }
-        *reinterpret_cast<uint2*>(dkp + col) =
-            make_uint2((unsigned)k4[0] | ((unsigned)k4[1] << 16), (unsigned)k4[2] | ((unsigned)k4[3] << 16));
-        *reinterpret_cast<uint2*>(dvp + col) =
-            make_uint2((unsigned)v4[0] | ((unsigned)v4[1] << 16), (unsigned)v4[2] | ((unsigned)v4[3] << 16));
+        store_bf16x4(dkp + col, kx, a.scale);
+        store_bf16x4(dvp + col, vx, 1.f);
       }
   }
+}
+
+// =============================================================================================
+// dQ
+// =============================================================================================
+template <int HD, bool CAUSAL, bool DOC>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
+  constexpr int NKS = HD / 16;
+  constexpr int NDB = HD / 32;
+  constexpr int ROWB = HD * 2;
+  constexpr int CPR = HD / 8;
+  constexpr int LD_ITERS = DQ_KB * CPR / 256;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * DQ_KB * ROWB];
+  unsigned char* Ks = smem;                // tr image: row reads (S^T) and column reads (dQ^T)
+  unsigned char* Vs = smem + DQ_KB * ROWB;  // row image
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = (a.S + DQ_QB - 1) / DQ_QB;
+  const int BH = a.B * a.Hq;
+  const int bh = blockIdx.x % BH;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest first
+  const int b = bh / a.Hq, hq = bh % a.Hq;
+  const int hk = hq / (a.Hq / a.Hkv);
+  const int q_row0 = qblk * DQ_QB + wave * 32;
+  const int my_q = q_row0 + r;
+  const int qc = min(my_q, a.S - 1);
+
+  const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh;
+  const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh;
+
+  // ---- Q and dO fragments (B operands of S^T = K Q^T and dP^T = V dO^T)
+  bf16x8_t qf[NKS], df[NKS];
+  {
+    const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh + (long)qc * a.q_ss + 8 * hh;
+    const unsigned short* Dp = a.dout + b * a.do_sb + hq * a.do_sh + (long)qc * a.do_ss + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      qf[ks] = __builtin_bit_cast(bf16x8_t, gload16(Qp + 16 * ks));
+      df[ks] = __builtin_bit_cast(bf16x8_t, gload16(Dp + 16 * ks));
+    }
+  }
+  const long rc = ((long)b * a.Hq + hq) * a.S + qc;
+  const float nlse2 = -a.lse[rc] * LOG2E;
+  const float dlt = a.delta[rc];
+
+  f32x16 dq[NDB];
+#pragma unroll
+  for (int d = 0; d < NDB; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[d][i] = 0.f;
+
+  const int kv_end = CAUSAL ? min(a.S, qblk * DQ_QB + DQ_QB) : a.S;
+  const int ntiles = (kv_end + DQ_KB - 1) / DQ_KB;
+  int my_start = 0, w_min = 0, w_max = 0, t0 = 0;
+  if constexpr (DOC) {
+    const int* ds = a.doc + (long)b * a.S;
+    my_start = ds[qc];
+    w_min = ds[min(q_row0, a.S - 1)];
+    w_max = ds[min(q_row0 + 31, a.S - 1)];
+    t0 = ds[min(qblk * DQ_QB, a.S - 1)] / DQ_KB;
+  }
+
+  uint4 kst[LD_ITERS], vst[LD_ITERS];
+  auto issue = [&](int t) {
+#pragma unroll
+    for (int it = 0; it < LD_ITERS; ++it) {
+      const int c = tid + 256 * it;
+      const int row = c / CPR, ch = c % CPR;
+      const int key = min(t * DQ_KB + row, a.S - 1);  // keys past S: masked
+      kst[it] = gload16(Kp + (long)key * a.k_ss + ch * 8);
+      vst[it] = gload16(Vp + (long)key * a.v_ss + ch * 8);
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int it = 0; it < LD_ITERS; ++it) {
+      const int c = tid + 256 * it;
+      const int row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<uint4*>(Ks + tr_off<HD>(row, ch)) = kst[it];
+      *reinterpret_cast<uint4*>(Vs + row_off<HD>(row, ch)) = vst[it];
+    }
+  };
+
+  if (t0 < ntiles) issue(t0);
+  for (int t = t0; t < ntiles; ++t) {
+    __syncthreads();  // all waves finished reading the previous tile
+    commit();
+    __syncthreads();
+    if (t + 1 < ntiles) issue(t + 1);  // overlaps the MFMAs below
+    const int kv0 = t * DQ_KB;
+    if (CAUSAL && kv0 > q_row0 + 31) continue;  // tile entirely above this wave's diagonal
+    if (DOC && kv0 + DQ_KB <= w_min) continue;  // tile entirely before every row's document
+    const bool need_mask = (CAUSAL && kv0 + DQ_KB - 1 > q_row0) || (kv0 + DQ_KB > a.S) || (DOC && kv0 < w_max);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      // ---- S^T = K Q^T, dP^T = V dO^T   (key on regs, q on lane)
+      f32x16 s, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8_t kfr = lds_read_b128(Ks, tr_off<HD>(kb * 32 + r, 2 * ks + hh));
+        s = mfma32(kfr, qf[ks], s);
+        const bf16x8_t vfr = lds_read_b128(Vs, row_off<HD>(kb * 32 + r, 2 * ks + hh));
+        dp = mfma32(vfr, df[ks], dp);
+      }
+      float dsv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pv = fast_exp2(s[i] * a.scale_log2 + nlse2);
+        if (need_mask) {
+          const int key = kv0 + kb * 32 + acc_row(i, hh);
+          if ((CAUSAL && key > my_q) || key >= a.S || (DOC && key < my_start)) pv = 0.f;
+        }
+        dsv[i] = pv * (dp[i] - dlt);
+      }
+      // ---- dQ^T += K^T dS^T   (sum over keys = the registers of dS^T)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8_t sbf = to_bf16x8(dsv + 8 * st);
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) {
+          const bf16x8_t kt = tr_frag<HD>(Ks, kb * 32 + 16 * st, d * 32, lane);
+          dq[d] = mfma32(kt, sbf, dq[d]);
+        }
+      }
+    }
+  }
+  // ---- dQ = scale * (dQ^T)^T: lane = q row, registers = d
+  if (my_q < a.S) {
+    unsigned short* Op = a.dq + ((long)b * a.S + my_q) * a.Hq * HD + (long)hq * HD;
+#pragma unroll
+    for (int d = 0; d < NDB; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = dq[d][4 * g + j];
+        store_bf16x4(Op + d * 32 + 8 * g + 4 * hh, x, a.scale);
+      }
+  }
+}
+
+template <int HD, bool CAUSAL, bool DOC>
+void launch_bwd(const BwdArgs& a, hipStream_t s, bool do_dq, bool do_dkv) {
+  if (do_dq) {
+    const int nqb = (a.S + DQ_QB - 1) / DQ_QB;
+    hipLaunchKernelGGL((fa_bwd_dq_kernel<HD, CAUSAL, DOC>), dim3((unsigned)(a.B * a.Hq * nqb)), dim3(256), 0, s, a);
+  }
+  if (do_dkv) {
+    const int nkb = (a.S + KV_KB - 1) / KV_KB;
+    hipLaunchKernelGGL((fa_bwd_dkv_kernel<HD, CAUSAL, DOC>), dim3((unsigned)(a.B * a.Hkv * nkb)), dim3(256), 0, s,
+                       a);
+  }
+}
+
+void dispatch_bwd(const BwdArgs& a, int D, bool causal, bool doc, hipStream_t s, bool do_dq = true,
+                  bool do_dkv = true) {
+  if (doc) {
+    if (D == 128) launch_bwd<128, true, true>(a, s, do_dq, do_dkv);
+    else launch_bwd<64, true, true>(a, s, do_dq, do_dkv);
+  } else if (D == 128) {
+    if (causal) launch_bwd<128, true, false>(a, s, do_dq, do_dkv);
+    else launch_bwd<128, false, false>(a, s, do_dq, do_dkv);
+  } else {
+    if (causal) launch_bwd<64, true, false>(a, s, do_dq, do_dkv);
+    else launch_bwd<64, false, false>(a, s, do_dq, do_dkv);
+  }
+}
+
+BwdArgs make_args(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                  const at::Tensor& lse, const at::Tensor& delta, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
+                  double scale) {
+  return BwdArgs{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                 bf_mut(dq), bf_mut(dk), bf_mut(dv), (int)q.size(0), (int)q.size(1), (int)q.size(2),
+                 (int)k.size(2), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                 v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2),
+                 (float)scale, (float)(scale * 1.4426950408889634), nullptr};
 }
 
 }  // namespace
@@ -358,24 +465,25 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
   const int B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
   const int Hkv = k.size(2);
   LLMCTL_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128");
-  LLMCTL_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && k.sizes() == v.sizes(), "shape mismatch");
+  LLMCTL_CHECK(Hkv > 0 && Hq % Hkv == 0, "Hq must be a multiple of Hkv");
+  LLMCTL_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && k.sizes() == v.sizes() && k.size(0) == B &&
+                   k.size(1) == S && k.size(3) == D,
+               "shape mismatch");
   LLMCTL_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (long)B * Hq * S,
                "lse must be contiguous fp32 [B,Hq,S]");
   for (const at::Tensor* t : {&dout, &q, &k, &v, &o})
-    LLMCTL_CHECK(t->scalar_type() == at::kBFloat16 && t->stride(3) == 1 && t->stride(0) % 8 == 0 &&
+    LLMCTL_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->stride(3) == 1 && t->stride(0) % 8 == 0 &&
                      t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0 &&
                      (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
                  "flash_attn_bwd: bf16, d-contiguous, 16-B aligned rows");
   const c10::DeviceGuard g(q.device());
-  auto dq_acc = at::zeros({B, S, Hq, D}, q.options().dtype(at::kFloat));
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  auto dq = at::empty({B, S, Hq, D}, q.options());
   auto dk = at::empty({B, S, Hkv, D}, q.options());
   auto dv = at::empty({B, S, Hkv, D}, q.options());
-  auto dq = at::empty({B, S, Hq, D}, q.options());
   if ((long)B * S * Hq == 0) return {dq, dk, dv};
   auto s = stream();
-  const long R = (long)B * S * Hq;
-  const long threads = R * (D / 8);
+  const long threads = (long)B * S * Hq * (D / 8);
   if (D == 128)
     hipLaunchKernelGGL(delta_kernel<128>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
                        delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
@@ -384,56 +492,33 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
     hipLaunchKernelGGL(delta_kernel<64>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
                        delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
                        o.stride(1), o.stride(2));
-  BwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_ptr(o), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
-            dq_acc.data_ptr<float>(), bf_mut(dk), bf_mut(dv), B, S, Hq, Hkv,
-            q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
-            v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
-            dout.stride(0), dout.stride(1), dout.stride(2), (float)scale, (float)(scale * 1.4426950408889634),
-            nullptr};
-  const int nkb = (S + KBLK - 1) / KBLK;
-  dim3 grid((unsigned)(B * Hkv * nkb)), block(256);
+  BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, scale);
+  bool doc = false;
   if (doc_start.has_value() && doc_start->defined()) {
     const at::Tensor& ds = *doc_start;
     LLMCTL_CHECK(causal && ds.is_cuda() && ds.scalar_type() == at::kInt && ds.is_contiguous() && ds.dim() == 2 &&
                      ds.size(0) == B && ds.size(1) == S,
                  "flash_attn_bwd: doc_start must be contiguous int32 [B,S] (causal)");
     a.doc = ds.data_ptr<int>();
-    if (D == 128) hipLaunchKernelGGL((fa_bwd_kernel<128, true, 0, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fa_bwd_kernel<64, true, 0, true>), grid, block, 0, s, a);
-  } else if (D == 128) {
-    if (causal) hipLaunchKernelGGL((fa_bwd_kernel<128, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fa_bwd_kernel<128, false>), grid, block, 0, s, a);
-  } else {
-    if (causal) hipLaunchKernelGGL((fa_bwd_kernel<64, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fa_bwd_kernel<64, false>), grid, block, 0, s, a);
+    doc = true;
   }
-  const long n8 = dq.numel() / 8;
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((n8 + 255) / 256), dim3(256), 0, s, dq_acc.data_ptr<float>(),
-                     bf_mut(dq), n8);
+  dispatch_bwd(a, D, causal, doc, s);
   return {dq, dk, dv};
 }
 
-// timing-only ablation entry (HD=128, causal): same launch as flash_attn_bwd's main kernel
+// timing-only entry for tools/attn_ablate.py (causal, no documents): abl 0 = both kernels,
+// 1 = dK/dV kernel only, 2 = dQ kernel only.  ``delta`` is taken as given.
 void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                   const at::Tensor& o, const at::Tensor& lse, at::Tensor& dq_acc, at::Tensor& dk, at::Tensor& dv,
+                   const at::Tensor& delta, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
                    int64_t abl) {
-  const int B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
-  LLMCTL_CHECK(D == 128, "fa_bwd_ablate: D=128 only");
+  const int D = q.size(3);
+  LLMCTL_CHECK(D == 64 || D == 128, "fa_bwd_ablate: head_dim 64 or 128");
+  LLMCTL_CHECK(dq.scalar_type() == at::kBFloat16 && dq.sizes() == q.sizes() && dk.sizes() == k.sizes() &&
+                   dv.sizes() == k.sizes() && delta.numel() == lse.numel(),
+               "fa_bwd_ablate: bf16 dq/dk/dv, fp32 delta");
   const c10::DeviceGuard g(q.device());
-  BwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_ptr(o), bf_ptr(dout), lse.data_ptr<float>(), lse.data_ptr<float>(),
-            dq_acc.data_ptr<float>(), bf_mut(dk), bf_mut(dv), B, S, Hq, Hkv,
-            q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
-            v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
-            dout.stride(0), dout.stride(1), dout.stride(2), 0.088f, 0.127f, nullptr};
-  dim3 grid((unsigned)(B * Hkv * ((S + KBLK - 1) / KBLK))), block(256);
-  auto s = stream();
-  switch (abl) {
-    case 0: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 0>), grid, block, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 1>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 2>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 4>), grid, block, 0, s, a); break;
-    default: hipLaunchKernelGGL((fa_bwd_kernel<128, true, 6>), grid, block, 0, s, a); break;
-  }
+  BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, 1.0 / std::sqrt((double)D));
+  dispatch_bwd(a, D, true, false, stream(), abl != 1, abl != 2);
 }
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {

@@ -128,6 +128,9 @@ class TrainingEngine:
                 self.device = torch.device("cuda", self.env.local_rank)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+            from llmctl.exec.gemm_tuning import enable_tuned_gemms
+
+            enable_tuned_gemms()
             if os.environ.get("LLMCTL_STREAM_CHECK") == "1":
                 # stream-race checker: every tensor access is tracked per stream and an access
                 # not ordered after the last conflicting one (event/wait_stream) raises

@@ -157,6 +157,9 @@ ATTN_CASES = [
     (1, 192, 4, 4, 128, False),
     (1, 100, 2, 2, 64, False),
     (1, 1024, 2, 1, 128, True),
+    (2, 320, 8, 2, 128, True),
+    (1, 130, 4, 1, 64, True),
+    (1, 300, 4, 1, 128, False),
 ]
 
 
