@@ -39,6 +39,7 @@ constexpr int KV_QT = 64;   // query rows per streamed tile
 constexpr int KV_NBUF = 3;  // LDS ring depth
 constexpr int DQ_QB = 128;  // query rows per dQ workgroup
 constexpr int DQ_KB = 64;   // keys per dQ tile
+constexpr int DKV_VAR = 0;  // dK/dV loop-body schedule (see fa_bwd_dkv_kernel); A/B: fa_bwd_ablate 3/4
 
 struct BwdArgs {
   const unsigned short *q, *k, *v, *dout;
@@ -90,7 +91,7 @@ __device__ __forceinline__ void store_bf16x4(unsigned short* p, const float* x, 
 // =============================================================================================
 // dK / dV
 // =============================================================================================
-template <int HD, bool CAUSAL, bool DOC>
+template <int HD, bool CAUSAL, bool DOC, int VAR = DKV_VAR>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
   constexpr int NKS = HD / 16;
   constexpr int NDB = HD / 32;
@@ -200,21 +201,37 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
     // no early-out for tiles a wave sees nothing of (only the first tile of a causal block, for
     // half the waves): a branch here makes hipcc shuttle dK/dV between AGPRs and VGPRs every tile
 
-    // ---- per 32-row half: S = Q K^T, dP = dO V^T (q on regs, key on lane), then
+    // ---- per 32-row half h: S = Q K^T, dP = dO V^T (q on regs, key on lane), then
     //      dV^T += dO^T P and dK^T += Q^T dS (sum over the half's rows = the registers).
-    //      Masks are branch-free selects; the halves are independent MFMA chains.
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f32x16 s, dp;
+    //      Masks are branch-free selects.  VAR 0: half after half; VAR 1: both halves'
+    //      S/dP chains first (the second half's MFMAs cover the first half's exp/VALU work);
+    //      VAR 2: as 1 with each half's operand fragments read into registers ahead of its MFMAs.
+    auto sdp = [&](int h, f32x16& s, f32x16& dp) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
+      if constexpr (VAR == 2) {
+        bf16x8_t qa[NKS], da[NKS];
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8_t qa = lds_read_b128(Qs, tr_off<HD>(32 * h + r, 2 * ks + hh));
-        const bf16x8_t da = lds_read_b128(Ds, tr_off<HD>(32 * h + r, 2 * ks + hh));
-        s = mfma32(qa, kf[ks], s);
-        dp = mfma32(da, vf[ks], dp);
+        for (int ks = 0; ks < NKS; ++ks) {
+          qa[ks] = lds_read_b128(Qs, tr_off<HD>(32 * h + r, 2 * ks + hh));
+          da[ks] = lds_read_b128(Ds, tr_off<HD>(32 * h + r, 2 * ks + hh));
+        }
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          s = mfma32(qa[ks], kf[ks], s);
+          dp = mfma32(da[ks], vf[ks], dp);
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8_t qa = lds_read_b128(Qs, tr_off<HD>(32 * h + r, 2 * ks + hh));
+          const bf16x8_t da = lds_read_b128(Ds, tr_off<HD>(32 * h + r, 2 * ks + hh));
+          s = mfma32(qa, kf[ks], s);
+          dp = mfma32(da, vf[ks], dp);
+        }
       }
+    };
+    auto soft = [&](int h, const f32x16& s, const f32x16& dp, bf16x8_t* pb, bf16x8_t* sb) {
       float p[16], dsv[16];
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
@@ -238,18 +255,40 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
           dsv[i] = pv * (dp[i] - dv4[j]);
         }
       }
+      pb[0] = to_bf16x8(p);
+      pb[1] = to_bf16x8(p + 8);
+      sb[0] = to_bf16x8(dsv);
+      sb[1] = to_bf16x8(dsv + 8);
+    };
+    auto dvdk = [&](int h, const bf16x8_t* pb, const bf16x8_t* sb) {
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8_t pb = to_bf16x8(p + 8 * st);
-        const bf16x8_t sb = to_bf16x8(dsv + 8 * st);
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int d = 0; d < NDB; ++d) {
           const bf16x8_t da = tr_frag<HD>(Ds, 32 * h + 16 * st, d * 32, lane);
-          dv[d] = mfma32(da, pb, dv[d]);
+          dv[d] = mfma32(da, pb[st], dv[d]);
           const bf16x8_t qa = tr_frag<HD>(Qs, 32 * h + 16 * st, d * 32, lane);
-          dk[d] = mfma32(qa, sb, dk[d]);
+          dk[d] = mfma32(qa, sb[st], dk[d]);
         }
+    };
+    if constexpr (VAR == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x16 s, dp;
+        bf16x8_t pb[2], sb[2];
+        sdp(h, s, dp);
+        soft(h, s, dp, pb, sb);
+        dvdk(h, pb, sb);
       }
+    } else {
+      f32x16 s0, dp0, s1, dp1;
+      bf16x8_t pb0[2], sb0[2], pb1[2], sb1[2];
+      sdp(0, s0, dp0);
+      sdp(1, s1, dp1);
+      soft(0, s0, dp0, pb0, sb0);
+      dvdk(0, pb0, sb0);
+      soft(1, s1, dp1, pb1, sb1);
+      dvdk(1, pb1, sb1);
     }
   }
   // ---- write dK (scaled), dV: lane = key, registers = d
@@ -507,7 +546,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
 }
 
 // timing-only entry for tools/attn_ablate.py (causal, no documents): abl 0 = both kernels,
-// 1 = dK/dV kernel only, 2 = dQ kernel only.  ``delta`` is taken as given.
+// 1 = dK/dV kernel only, 2 = dQ kernel only, 3 / 4 = dK/dV schedule variants 1 / 2.  ``delta`` is taken as given.
 void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                    const at::Tensor& delta, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
                    int64_t abl) {
@@ -518,6 +557,14 @@ void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
                "fa_bwd_ablate: bf16 dq/dk/dv, fp32 delta");
   const c10::DeviceGuard g(q.device());
   BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, 1.0 / std::sqrt((double)D));
+  if (abl == 3 || abl == 4) {
+    LLMCTL_CHECK(D == 128, "fa_bwd_ablate: schedule variants at head_dim 128");
+    const int nkb = (a.S + KV_KB - 1) / KV_KB;
+    const dim3 grid((unsigned)(a.B * a.Hkv * nkb));
+    if (abl == 3) hipLaunchKernelGGL((fa_bwd_dkv_kernel<128, true, false, 1>), grid, dim3(256), 0, stream(), a);
+    else hipLaunchKernelGGL((fa_bwd_dkv_kernel<128, true, false, 2>), grid, dim3(256), 0, stream(), a);
+    return;
+  }
   dispatch_bwd(a, D, true, false, stream(), abl != 1, abl != 2);
 }
 

@@ -101,7 +101,136 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const unsigned short* __r
 }
 
 template <int NV, bool LN, bool DRES>
-__global__ __launch_bounds__(256) void norm_bwd_kernel(const unsigned short* __restrict__ dy,
+__global__ __launch_bounds__(256, LN ? 1 : 2) void norm_bwd_kernel(const unsigned short* __restrict__ dy,
+                                                                    const unsigned short* __restrict__ x,
+                                                                    const unsigned short* __restrict__ w,
+                                                                    const float* __restrict__ mu,
+                                                                    const float* __restrict__ rstd,
+                                                                    const unsigned short* __restrict__ dres,
+                                                                    unsigned short* __restrict__ dx,
+                                                                    float* __restrict__ dw_part,
+                                                                    float* __restrict__ db_part, int T, int H) {
+  // * software-pipelined over the wave's rows: the next row's x / dy (raw bf16) are in
+  //   flight while the current row is reduced and written (HBM latency, not bandwidth, bounded
+  //   the one-row-at-a-time form at ~2.9 TB/s);
+  // * the per-column dW (dB) sums live in a wave-private LDS slab (float4 read-modify-write per
+  //   row), not in 64 accumulator registers per lane, so two blocks fit per CU (RMSNorm).
+  constexpr int W = NV * 512;
+  __shared__ __attribute__((aligned(16))) float acc[(LN ? 2 : 1) * kWaves * W];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wave = blockIdx.x * kWaves + wid;
+  const int nwaves = gridDim.x * kWaves;
+  const float invH = 1.f / (float)H;
+  float4* dwl = reinterpret_cast<float4*>(acc + wid * W);              // this wave's dW slab
+  float4* dbl = reinterpret_cast<float4*>(acc + (kWaves + wid) * W);   // (LN) dB slab
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = (i * 512 + lane * 8) / 4;
+    dwl[c4] = dwl[c4 + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (LN) dbl[c4] = dbl[c4 + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  bf16x8 xr[NV], gr[NV], dr[DRES ? NV : 1];
+  float r = 0.f, m = 0.f;
+  auto fetch = [&](int row, bf16x8* xo, bf16x8* go, float& ro, float& mo) {
+    const int rr = min(row, T - 1);  // unconditional (clamped) loads: no branch around them
+    const size_t base = (size_t)rr * H;
+    ro = rstd[rr];
+    if constexpr (LN) mo = mu[rr];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = min(i * 512 + lane * 8, H - 8);
+      xo[i] = *reinterpret_cast<const bf16x8*>(x + base + col);
+      go[i] = *reinterpret_cast<const bf16x8*>(dy + base + col);
+    }
+  };
+  if (wave < T) fetch(wave, xr, gr, r, m);
+  for (int row = wave; row < T; row += nwaves) {
+    const size_t base = (size_t)row * H;
+    if constexpr (DRES) {  // consumed by the second pass: the reductions cover its latency
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        dr[i] = *reinterpret_cast<const bf16x8*>(dres + base + min(i * 512 + lane * 8, H - 8));
+    }
+    bf16x8 xn[NV], gn[NV];
+    float rn = 0.f, mn = 0.f;
+    fetch(row + nwaves, xn, gn, rn, mn);
+    float dot = 0.f, gs = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = i * 512 + lane * 8;
+      if (col < H) {
+        float wf[8], pw[8], pb[8];
+        load8(w + col, wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (bf2f(xr[i][j]) - m) * r;
+          const float dyf = bf2f(gr[i][j]);
+          const float g = dyf * wf[j];
+          dot += g * xh;
+          gs += g;
+          pw[j] = dyf * xh;
+          pb[j] = dyf;
+        }
+        const int c4 = col / 4;
+        float4 a0 = dwl[c4], a1 = dwl[c4 + 1];
+        dwl[c4] = make_float4(a0.x + pw[0], a0.y + pw[1], a0.z + pw[2], a0.w + pw[3]);
+        dwl[c4 + 1] = make_float4(a1.x + pw[4], a1.y + pw[5], a1.z + pw[6], a1.w + pw[7]);
+        if constexpr (LN) {
+          float4 b0 = dbl[c4], b1 = dbl[c4 + 1];
+          dbl[c4] = make_float4(b0.x + pb[0], b0.y + pb[1], b0.z + pb[2], b0.w + pb[3]);
+          dbl[c4 + 1] = make_float4(b1.x + pb[4], b1.y + pb[5], b1.z + pb[6], b1.w + pb[7]);
+        }
+      }
+    }
+    const float mdot = wave_sum(dot) * invH;
+    const float mg = LN ? wave_sum(gs) * invH : 0.f;
+    // re-expand the packed row in the second pass (no 2 x 64 live fp32 values across the
+    // reductions: hipcc would otherwise keep the first pass's conversions and spill)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) asm volatile("" : "+v"(xr[i]), "+v"(gr[i]));
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = i * 512 + lane * 8;
+      if (col < H) {
+        float wf[8], o[8];
+        load8(w + col, wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (bf2f(xr[i][j]) - m) * r;
+          o[j] = r * (bf2f(gr[i][j]) * wf[j] - mg - xh * mdot);
+          if constexpr (DRES) o[j] += bf2f(dr[i][j]);
+        }
+        store8(dx + base + col, o);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      xr[i] = xn[i];
+      gr[i] = gn[i];
+    }
+    r = rn;
+    m = mn;
+  }
+  // block-reduce the 4 wave slabs: one fp32 partial row per block (no float atomics)
+  __syncthreads();
+#pragma unroll
+  for (int pass = 0; pass < (LN ? 2 : 1); ++pass) {
+    float* out = pass == 0 ? dw_part : db_part;
+    const float* slab = acc + pass * kWaves * W;
+    for (int c = threadIdx.x; c < H; c += 256) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < kWaves; ++k) s += slab[k * W + c];
+      out[(size_t)blockIdx.x * H + c] = s;
+    }
+  }
+}
+
+// rows wider than 4096: one row at a time, fp32 row in registers (the pipelined form spills)
+template <int NV, bool LN, bool DRES>
+__global__ __launch_bounds__(256) void norm_bwd_wide_kernel(const unsigned short* __restrict__ dy,
                                                         const unsigned short* __restrict__ x,
                                                         const unsigned short* __restrict__ w,
                                                         const float* __restrict__ mu,
@@ -192,6 +321,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const unsigned short* __r
   }
 }
 
+
 // sum partial rows [P, H] -> out[H] (bf16).  Block = 64 columns x 4 waves; wave w sums rows
 // w, w+4, ... (4 independent loads in flight per lane), then the 4 waves combine via LDS.
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ part, int P, int H,
@@ -252,7 +382,9 @@ void launch_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, 
                 at::Tensor* db) {
   const int T = x.size(0), H = x.size(1);
   const int nv = (H + 511) / 512;
-  const int grid = std::max(1, std::min((T + kWaves - 1) / kWaves, num_cus()));
+  // pipelined kernel (H <= 4096): 2 blocks per CU for RMSNorm (LDS dW slabs, 64 KB each)
+  const int per_cu = (nv <= 8 && !LN) ? 2 : 1;
+  const int grid = std::max(1, std::min((T + kWaves - 1) / kWaves, per_cu * num_cus()));
   auto opts = x.options().dtype(at::kFloat);
   at::Tensor dw_part = at::empty({grid, H}, opts);
   at::Tensor db_part = LN ? at::empty({grid, H}, opts) : at::Tensor();
@@ -268,6 +400,17 @@ void launch_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, 
     hipLaunchKernelGGL((norm_bwd_kernel<NV, LN, false>), dim3(grid), dim3(256), 0, s, bf_ptr(dy), bf_ptr(x), \
                        bf_ptr(w), mu ? mu->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), nullptr,     \
                        bf_mut(dx), dw_part.data_ptr<float>(), LN ? db_part.data_ptr<float>() : nullptr, T, H)
+#define LAUNCHW(NV)                                                                                          \
+  if (has_dres)                                                                                              \
+    hipLaunchKernelGGL((norm_bwd_wide_kernel<NV, LN, true>), dim3(grid), dim3(256), 0, s, bf_ptr(dy),          \
+                       bf_ptr(x), bf_ptr(w), mu ? mu->data_ptr<float>() : nullptr, rstd.data_ptr<float>(),    \
+                       bf_ptr(*dres), bf_mut(dx), dw_part.data_ptr<float>(),                                   \
+                       LN ? db_part.data_ptr<float>() : nullptr, T, H);                                       \
+  else                                                                                                       \
+    hipLaunchKernelGGL((norm_bwd_wide_kernel<NV, LN, false>), dim3(grid), dim3(256), 0, s, bf_ptr(dy),         \
+                       bf_ptr(x), bf_ptr(w), mu ? mu->data_ptr<float>() : nullptr, rstd.data_ptr<float>(),    \
+                       nullptr, bf_mut(dx), dw_part.data_ptr<float>(), LN ? db_part.data_ptr<float>() : nullptr, \
+                       T, H)
   switch (nv) {
     case 1: LAUNCH(1); break;
     case 2: LAUNCH(2); break;
@@ -275,10 +418,11 @@ void launch_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, 
     case 4: LAUNCH(4); break;
     case 5: case 6: LAUNCH(6); break;
     case 7: case 8: LAUNCH(8); break;
-    case 9: case 10: case 11: case 12: LAUNCH(12); break;
-    default: LAUNCH(16); break;
+    case 9: case 10: case 11: case 12: LAUNCHW(12); break;
+    default: LAUNCHW(16); break;
   }
 #undef LAUNCH
+#undef LAUNCHW
   hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), dim3(256), 0, s, dw_part.data_ptr<float>(), grid, H,
                      bf_mut(dw));
   if (LN)
