@@ -98,6 +98,7 @@ class ParallelSection(_Open):
     pipeline_parallel: int = 1
     sequence_parallel: bool = False
     context_parallel: int = 1
+    context_parallel_mode: str = "ulysses"  # ulysses | ring
     zero_stage: int = Field(1, ge=0, le=3)
     activation_checkpoint: Union[str, bool] = "selective"
     micro_batch_size: int = 1
@@ -193,7 +194,7 @@ def resolve_training_config(train_file: Optional[Dict[str, Any]] = None, plan: O
         p = t.parallel
         out.update(tensor_parallel=p.tensor_parallel, pipeline_parallel=p.pipeline_parallel,
                    sequence_parallel=p.sequence_parallel, zero_stage=p.zero_stage,
-                   context_parallel=p.context_parallel,
+                   context_parallel=p.context_parallel, context_parallel_mode=p.context_parallel_mode,
                    batch_size=p.micro_batch_size)
         ac = p.activation_checkpoint
         out["activation_checkpoint"] = ("selective" if ac is True else "none" if ac in (False, None) else str(ac))

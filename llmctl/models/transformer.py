@@ -43,10 +43,12 @@ class ParallelContext:
     has_head: bool = True
     # recompute policy: "none" | "selective" | "full"
     activation_checkpoint: str = "none"
-    # context parallel (Ulysses all-to-all around attention; llmctl.parallel.context_parallel)
+    # context parallel (llmctl.parallel.context_parallel): "ulysses" all-to-all around
+    # attention, or "ring" attention (K/V chunks rotated over the CP ring)
     cp_group: Optional[object] = None
     cp_size: int = 1
     cp_rank: int = 0
+    cp_mode: str = "ulysses"
 
 
 def _init_linear(w: torch.Tensor, std: float) -> None:
@@ -91,8 +93,11 @@ class DecoderLayer(nn.Module):
         t = pc.tp_size
         if cfg.heads % t or cfg.kv_heads % t or cfg.ffn % t:
             raise ValueError(f"heads/kv_heads/ffn must divide tp={t}")
-        if (cfg.kv_heads // t) % pc.cp_size or (cfg.heads // t) % pc.cp_size:
-            raise ValueError(f"(kv_)heads / tp must divide context_parallel={pc.cp_size}")
+        if pc.cp_mode not in ("ulysses", "ring"):
+            raise ValueError(f"unknown context-parallel mode {pc.cp_mode!r} (ulysses | ring)")
+        if pc.cp_mode == "ulysses" and ((cfg.kv_heads // t) % pc.cp_size or (cfg.heads // t) % pc.cp_size):
+            raise ValueError(f"(kv_)heads / tp must divide context_parallel={pc.cp_size} (ulysses; "
+                             f"ring attention has no head constraint)")
         self.nq, self.nkv, self.D = cfg.heads // t, cfg.kv_heads // t, cfg.head_dim
         self.f = cfg.ffn // t
         h = cfg.hidden
@@ -156,7 +161,9 @@ class DecoderLayer(nn.Module):
         q = q.view(B, S, self.nq, self.D)
         k = k.view(B, S, self.nkv, self.D)
         v = v.view(B, S, self.nkv, self.D)
-        if self.pc.cp_size > 1:  # sequence chunk, all heads <-> all tokens, head chunk
+        if self.pc.cp_size > 1 and self.pc.cp_mode == "ring":  # K/V chunks around the CP ring
+            o = cp.ring_attention(q, k, v, self.pc.cp_group)
+        elif self.pc.cp_size > 1:  # sequence chunk, all heads <-> all tokens, head chunk
             g = self.pc.cp_group
             o = cp.head_to_seq(ops.flash_attention(cp.seq_to_head(q, g), cp.seq_to_head(k, g),
                                                    cp.seq_to_head(v, g), causal=True), g)

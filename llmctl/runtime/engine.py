@@ -65,7 +65,8 @@ class TrainingConfig:
     seq_len: int = 2048
     tensor_parallel: int = 1
     pipeline_parallel: int = 1
-    context_parallel: int = 1  # Ulysses CP: sequence split over cp ranks (llmctl.parallel.context_parallel)
+    context_parallel: int = 1  # CP: sequence split over cp ranks (llmctl.parallel.context_parallel)
+    context_parallel_mode: str = "ulysses"  # ulysses (all-to-all, xGMI-mesh friendly) | ring
     pack_sequences: bool = False  # documents packed into sequences: attention/positions reset at separators
     doc_separator: int = 0  # token that ends a document (byte tokenizer / tokenize_to_bin use 0)
     sequence_parallel: bool = False
@@ -174,7 +175,7 @@ class TrainingEngine:
             sequence_parallel=c.sequence_parallel and pg.layout.tp > 1,
             layer_start=lo, layer_end=hi, has_embedding=pp_rank == 0, has_head=pp_rank == pp - 1,
             activation_checkpoint=c.activation_checkpoint,
-            cp_group=pg.cp_group, cp_size=pg.layout.cp, cp_rank=pg.cp_rank)
+            cp_group=pg.cp_group, cp_size=pg.layout.cp, cp_rank=pg.cp_rank, cp_mode=c.context_parallel_mode)
         # identical init on every DP replica (seeded; TP ranks get different shards, so
         # their seeds differ by tp_rank/pp_rank only)
         torch.manual_seed(c.seed + 1000 * pg.tp_rank + 100000 * pp_rank)

@@ -49,7 +49,8 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
                   sequence_parallel=layout.get("sp", False),
                   activation_checkpoint=layout.get("ac", "none"),
                   num_microbatches=layout.get("microbatches", 0),
-                  context_parallel=layout.get("cp", 1))
+                  context_parallel=layout.get("cp", 1),
+                  context_parallel_mode=layout.get("cp_mode", "ulysses"))
     eng = TrainingEngine(cfg)
     eng.load_full_state_dict(reference_state(model))
     vocab = eng.model_config.vocab_size
@@ -239,3 +240,29 @@ def train_reference_schedule(schedule) -> dict:
     for s, dp in enumerate(schedule):
         eng.train_step([make_batch(vocab, cfg.seq_len, cfg.batch_size, s, r, 0) for r in range(dp)])
     return {"state": eng.gather_full_state_dict()}
+
+
+def ring_attention_check(rank: int, world: int, B: int = 2, S: int = 48, Hq: int = 4, Hkv: int = 2,
+                         D: int = 16) -> dict:
+    """Ring attention over a ``world``-rank CP group vs full causal attention (fp32, gloo):
+    returns this rank's output / gradient chunks and the oracle's."""
+    import torch.distributed as dist
+
+    from llmctl.ops import ref
+    from llmctl.parallel.context_parallel import ring_attention, split_sequence
+
+    dist.init_process_group("gloo")
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(B, S, Hq, D, generator=g)
+    k = torch.randn(B, S, Hkv, D, generator=g)
+    v = torch.randn(B, S, Hkv, D, generator=g)
+    do = torch.randn(B, S, Hq, D, generator=g)
+    scale = D ** -0.5
+    o_full, lse = ref.attention_fwd(q, k, v, scale, True)
+    dq_full, dk_full, dv_full = ref.attention_bwd(do, q, k, v, o_full, lse, scale, True)
+    ql, kl, vl = (split_sequence(t, world, rank).requires_grad_(True) for t in (q, k, v))
+    o = ring_attention(ql, kl, vl, None if world == 1 else dist.group.WORLD, scale)
+    o.backward(split_sequence(do, world, rank))
+    ch = lambda t: split_sequence(t, world, rank)  # noqa: E731
+    return {"o": o.detach(), "dq": ql.grad, "dk": kl.grad, "dv": vl.grad,
+            "o_ref": ch(o_full), "dq_ref": ch(dq_full), "dk_ref": ch(dk_full), "dv_ref": ch(dv_full)}
