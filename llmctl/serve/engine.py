@@ -52,6 +52,10 @@ class InferenceEngine:
             self.device = torch.device("cuda", torch.cuda.current_device())
         if self.device.type == "cpu" and dtype == torch.bfloat16:
             dtype = torch.float32  # the CPU oracle path
+        if self.device.type == "cuda":  # pre-tuned prefill projection GEMMs (llmctl.exec.gemm_tuning)
+            from llmctl.exec.gemm_tuning import enable_tuned_gemms
+
+            enable_tuned_gemms()
         self.dtype = dtype
         self.model_path = model_path
         self.model: DecoderLM

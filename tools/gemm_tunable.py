@@ -45,7 +45,10 @@ def main():
     ap.add_argument("--csv", default="gpurun_out/tunableop.csv")
     ap.add_argument("--json", default=None)
     ap.add_argument("--skip-rocblas", action="store_true")
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad", help="subset to time/tune")
+    ap.add_argument("--append", action="store_true", help="load --csv first and add to it")
     args = ap.parse_args()
+    want = set(args.ops.split(","))
     from llmctl.ops._lib import native
 
     ops = native()
@@ -61,11 +64,11 @@ def main():
 
     def ops_for(name):
         x, w, dy, dw = data[name]
-        return {
+        return {k: f for k, f in {
             "fwd": lambda: F.linear(x, w),
             "dgrad": lambda: dy @ w,
             "wgrad": lambda: torch.mm(dy.t(), x, out=dw),
-        }
+        }.items() if k in want}
 
     res = {}
 
@@ -79,7 +82,7 @@ def main():
                 print(name, op, tag, res[name][f"{op}_{tag}"], flush=True)
 
     run("hipblaslt")
-    for name in SHAPES:  # the llmctl MFMA wgrad kernel
+    for name in (SHAPES if "wgrad" in want else []):  # the llmctl MFMA wgrad kernel
         N, K = SHAPES[name]
         x, w, dy, dw = data[name]
         ms = timeit(lambda: ops.gemm_ex(dy, x, dw, True, True, False))
@@ -93,6 +96,8 @@ def main():
     os.makedirs(os.path.dirname(os.path.abspath(args.csv)), exist_ok=True)
     tun.set_filename(args.csv, insert_device_ordinal=False)
     tun.enable(True)
+    if args.append and os.path.exists(args.csv):
+        tun.read_file(args.csv)
     tun.tuning_enable(True)
     tun.set_max_tuning_duration(40)
     tun.set_max_tuning_iterations(30)
@@ -102,7 +107,6 @@ def main():
             f()
             torch.cuda.synchronize()
             print("tuned", name, op, f"{time.time() - t0:.0f}s", flush=True)
-    tun.write_file()
     tun.tuning_enable(False)
     run("tunableop")
     tun.enable(False)
@@ -111,7 +115,7 @@ def main():
         tot = 0.0
         ok = True
         for name in SHAPES:
-            for op in ("fwd", "dgrad", "wgrad"):
+            for op in sorted(want):
                 k = f"{op}_{tag}"
                 if k not in res[name]:
                     ok = False
@@ -119,9 +123,10 @@ def main():
                 tot += res[name][k]["ms"]
         if ok:
             summary[tag] = round(tot, 3)
-    summary["hipblaslt_with_llmctl_wgrad"] = round(sum(
-        res[n]["fwd_hipblaslt"]["ms"] + res[n]["dgrad_hipblaslt"]["ms"] + res[n]["wgrad_llmctl"]["ms"]
-        for n in SHAPES), 3)
+    if want == {"fwd", "dgrad", "wgrad"}:
+        summary["hipblaslt_with_llmctl_wgrad"] = round(sum(
+            res[n]["fwd_hipblaslt"]["ms"] + res[n]["dgrad_hipblaslt"]["ms"] + res[n]["wgrad_llmctl"]["ms"]
+            for n in SHAPES), 3)
     res["summary_ms_one_layer_each"] = summary
     print(json.dumps(summary), flush=True)
     if args.json:
