@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--cp", type=int, default=1, help="context-parallel degree")
     ap.add_argument("--cp-mode", default="ulysses", choices=["ulysses", "ring"])
+    ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree (MoE models)")
     ap.add_argument("--activation-checkpoint", default="none")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--device", default="auto")
@@ -70,7 +71,7 @@ def main():
         warmup_steps=10, max_steps=args.warmup + args.steps, gradient_clipping=1.0, mixed_precision="bf16",
         tensor_parallel=args.tp, pipeline_parallel=args.pp, zero_stage=zero,
         sequence_parallel=args.sequence_parallel, activation_checkpoint=args.activation_checkpoint,
-        context_parallel=args.cp, context_parallel_mode=args.cp_mode,
+        context_parallel=args.cp, context_parallel_mode=args.cp_mode, expert_parallel=args.ep,
         bucket_mb=args.bucket_mb, device=args.device, seed=1234, log_level="warning")
     eng = TrainingEngine(cfg, mc)
     dev = eng.device
@@ -114,7 +115,8 @@ def main():
     mfu = tps * fpt / (2.5e15 * world) if dev.type == "cuda" else None
     par = f"dp{dp}" + (f"-tp{args.tp}" if args.tp > 1 else "") + (f"-pp{args.pp}" if args.pp > 1 else "") + \
         (f"-zero{zero}" if zero else "") + ("-sp" if args.sequence_parallel else "") + \
-        (f"-cp{args.cp}{'ring' if args.cp_mode == 'ring' else ''}" if args.cp > 1 else "")
+        (f"-cp{args.cp}{'ring' if args.cp_mode == 'ring' else ''}" if args.cp > 1 else "") + \
+        (f"-ep{args.ep}" if args.ep > 1 else "")
     vs = None
     if REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU and mc.name == "gpt-7b" and args.seq_len == 2048 and dev.type == "cuda":
         vs = tps / (REFERENCE_STACK_TOKENS_PER_SEC_PER_GPU * world)

@@ -99,6 +99,7 @@ class ParallelSection(_Open):
     sequence_parallel: bool = False
     context_parallel: int = 1
     context_parallel_mode: str = "ulysses"  # ulysses | ring
+    expert_parallel: int = 1  # MoE models: experts sharded over this many DP ranks
     zero_stage: int = Field(1, ge=0, le=3)
     activation_checkpoint: Union[str, bool] = "selective"
     micro_batch_size: int = 1
@@ -158,6 +159,7 @@ class PlanParallelism(_Open):
     estimated_flops: Optional[float] = None
     sequence_parallel: bool = False
     context_parallel: int = 1
+    expert_parallel: int = 1
     activation_checkpoint: str = "none"
     grad_accum: int = 1
 
@@ -195,7 +197,7 @@ def resolve_training_config(train_file: Optional[Dict[str, Any]] = None, plan: O
         out.update(tensor_parallel=p.tensor_parallel, pipeline_parallel=p.pipeline_parallel,
                    sequence_parallel=p.sequence_parallel, zero_stage=p.zero_stage,
                    context_parallel=p.context_parallel, context_parallel_mode=p.context_parallel_mode,
-                   batch_size=p.micro_batch_size)
+                   expert_parallel=p.expert_parallel, batch_size=p.micro_batch_size)
         ac = p.activation_checkpoint
         out["activation_checkpoint"] = ("selective" if ac is True else "none" if ac in (False, None) else str(ac))
         if p.gradient_accumulation_steps:
@@ -234,7 +236,7 @@ def resolve_training_config(train_file: Optional[Dict[str, Any]] = None, plan: O
         out.update(tensor_parallel=pp.tensor_parallel, pipeline_parallel=pp.pipeline_parallel,
                    zero_stage=pp.zero_stage, batch_size=pp.micro_batch_size,
                    sequence_parallel=pp.sequence_parallel, activation_checkpoint=pp.activation_checkpoint,
-                   context_parallel=pp.context_parallel,
+                   context_parallel=pp.context_parallel, expert_parallel=pp.expert_parallel,
                    gradient_accumulation_steps=max(pp.grad_accum, 1))
     if cli:
         out.update({k: v for k, v in cli.items() if v is not None})

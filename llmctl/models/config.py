@@ -38,6 +38,12 @@ class ModelConfig:
     tie_word_embeddings: bool = False
     rope: Dict[str, Any] = field(default_factory=lambda: {"base": 10000, "scaling": "linear"})
     attention: Dict[str, Any] = field(default_factory=lambda: {"type": "causal", "bias": False, "dropout": 0.0})
+    # mixture of experts (0 = dense): every layer's MLP becomes num_experts SwiGLU experts of
+    # width moe_ffn (default ffn) with top-``experts_per_token`` softmax routing
+    num_experts: int = 0
+    experts_per_token: int = 2
+    moe_ffn: Optional[int] = None
+    router_aux_loss_coef: float = 0.01
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def __post_init__(self) -> None:
@@ -47,6 +53,17 @@ class ModelConfig:
             self.head_dim = self.hidden // self.heads
         if self.heads % self.kv_heads:
             raise ValueError(f"heads={self.heads} not divisible by kv_heads={self.kv_heads}")
+        if self.num_experts:
+            if self.moe_ffn is None:
+                self.moe_ffn = self.ffn
+            if not (0 < self.experts_per_token <= self.num_experts):
+                raise ValueError("experts_per_token must be in [1, num_experts]")
+            if not self.gated_mlp:
+                raise ValueError("MoE layers use SwiGLU experts (activation silu)")
+
+    @property
+    def is_moe(self) -> bool:
+        return self.num_experts > 0
 
     # ------------------------------------------------------------------ derived sizes
     @property
@@ -66,6 +83,8 @@ class ModelConfig:
         h, f, L, V = self.hidden, self.ffn, self.layers, self.vocab_size
         attn = h * (self.q_size + 2 * self.kv_size) + self.q_size * h
         mlp = (3 if self.gated_mlp else 2) * h * f
+        if self.is_moe:  # router + every expert
+            mlp = self.num_experts * h + self.num_experts * 3 * h * self.moe_ffn
         norms = (2 * h) if self.norm == "rmsnorm" else (4 * h)
         biases = 0
         if self.norm == "layernorm":  # GPT-2 style linear biases
@@ -81,9 +100,17 @@ class ModelConfig:
                 n += self.max_position_embeddings * h
         return n
 
+    def active_parameters(self) -> int:
+        """Parameters a token touches (MoE: top-k experts of each layer, not all of them)."""
+        n = self.num_parameters(include_embedding=False)
+        if self.is_moe:
+            n -= self.layers * (self.num_experts - self.experts_per_token) * 3 * self.hidden * self.moe_ffn
+        return n
+
     def flops_per_token(self, seq_len: int, training: bool = True) -> float:
-        """Model FLOPs per token (6N + attention; PaLM-style MFU accounting, causal halved)."""
-        n = self.num_parameters(include_embedding=False) + self.vocab_size * self.hidden  # lm_head matmul
+        """Model FLOPs per token (6N + attention; PaLM-style MFU accounting, causal halved;
+        MoE counts the active experts only)."""
+        n = self.active_parameters() + self.vocab_size * self.hidden  # lm_head matmul
         attn = 2 * 2 * self.layers * self.q_size * seq_len / 2  # QK^T + PV, causal half
         fwd = 2 * n + attn
         return 3 * fwd if training else fwd
@@ -92,7 +119,8 @@ class ModelConfig:
     _KNOWN = {
         "name", "arch", "layers", "hidden", "ffn", "heads", "kv_heads", "vocab_size", "head_dim",
         "max_position_embeddings", "activation", "norm", "position", "layer_norm_eps",
-        "tie_word_embeddings", "rope", "attention",
+        "tie_word_embeddings", "rope", "attention", "num_experts", "experts_per_token", "moe_ffn",
+        "router_aux_loss_coef",
     }
 
     @classmethod
@@ -103,6 +131,8 @@ class ModelConfig:
         aliases = {
             "num_hidden_layers": "layers", "hidden_size": "hidden", "intermediate_size": "ffn",
             "num_attention_heads": "heads", "num_key_value_heads": "kv_heads", "rms_norm_eps": "layer_norm_eps",
+            "num_local_experts": "num_experts", "num_experts_per_tok": "experts_per_token",
+            "router_aux_loss_coef": "router_aux_loss_coef",
         }
         for a, k in aliases.items():
             if a in d and k not in kw:
@@ -125,7 +155,8 @@ class ModelConfig:
         return cls.from_dict(data)
 
     def to_dict(self) -> Dict[str, Any]:
-        d = {k: getattr(self, k) for k in sorted(self._KNOWN)}
+        moe = ("num_experts", "experts_per_token", "moe_ffn", "router_aux_loss_coef")
+        d = {k: getattr(self, k) for k in sorted(self._KNOWN) if self.is_moe or k not in moe}
         d.update(self.extra)
         d["estimated_params"] = self.num_parameters()
         return d
@@ -180,7 +211,20 @@ MODEL_TEMPLATES: Dict[str, Dict[str, Dict[str, Any]]] = {
             "rope": {"base": 500000, "scaling": "linear"},
         },
     },
+    "mixtral": {
+        "8x7b": {
+            "name": "mixtral-8x7b", "arch": "decoder-only", "layers": 32, "hidden": 4096, "ffn": 14336,
+            "heads": 32, "kv_heads": 8, "vocab_size": 32000, "max_position_embeddings": 32768,
+            "rope": {"base": 1000000, "scaling": "linear"}, "num_experts": 8, "experts_per_token": 2,
+        },
+    },
     "tiny": {
+        "moe": {
+            "name": "tiny-moe", "arch": "decoder-only", "layers": 2, "hidden": 256, "ffn": 704,
+            "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
+            "rope": {"base": 10000, "scaling": "linear"}, "num_experts": 4, "experts_per_token": 2,
+            "moe_ffn": 256,
+        },
         "test": {
             "name": "tiny-test", "arch": "decoder-only", "layers": 2, "hidden": 256, "ffn": 704,
             "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
@@ -194,6 +238,7 @@ ALIASES = {
     "gpt-7b": ("gpt", "7b"), "gpt-13b": ("gpt", "13b"), "llama-7b": ("llama", "7b"),
     "llama-13b": ("llama", "13b"), "llama-30b": ("llama", "30b"), "llama3-70b": ("llama", "70b"),
     "llama-70b": ("llama", "70b"), "tiny": ("tiny", "test"), "tiny-test": ("tiny", "test"),
+    "mixtral-8x7b": ("mixtral", "8x7b"), "tiny-moe": ("tiny", "moe"),
 }
 
 

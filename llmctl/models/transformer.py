@@ -28,6 +28,7 @@ from llmctl.exec.linear import linear, weight_grad
 from llmctl.parallel import context_parallel as cp
 from llmctl.parallel import tensor_parallel as tp
 from .config import ModelConfig
+from .moe import MoEMLP
 
 
 @dataclass
@@ -49,6 +50,10 @@ class ParallelContext:
     cp_size: int = 1
     cp_rank: int = 0
     cp_mode: str = "ulysses"
+    # expert parallel (MoE models; llmctl.models.moe): all-to-all group of ep_size DP ranks
+    ep_group: Optional[object] = None
+    ep_size: int = 1
+    ep_rank: int = 0
 
 
 def _init_linear(w: torch.Tensor, std: float) -> None:
@@ -110,8 +115,14 @@ class DecoderLayer(nn.Module):
         self.wqkv = nn.Parameter(torch.empty((self.nq + 2 * self.nkv) * self.D, h, **kw))
         self.wo = nn.Parameter(torch.empty(h, self.nq * self.D, **kw))
         gated = cfg.gated_mlp
-        self.w_up = nn.Parameter(torch.empty((2 if gated else 1) * self.f, h, **kw))
-        self.w_down = nn.Parameter(torch.empty(h, self.f, **kw))
+        self.moe = None
+        if cfg.is_moe:
+            if t > 1:
+                raise NotImplementedError("MoE layers with tensor parallelism (use expert parallelism)")
+            self.w_up = self.w_down = None
+        else:
+            self.w_up = nn.Parameter(torch.empty((2 if gated else 1) * self.f, h, **kw))
+            self.w_down = nn.Parameter(torch.empty(h, self.f, **kw))
         if ln:  # GPT-2 style biases (row-parallel biases are replicated, added after the reduce)
             self.bqkv = nn.Parameter(torch.zeros((self.nq + 2 * self.nkv) * self.D, **kw))
             self.bo = nn.Parameter(torch.zeros(h, **kw))
@@ -121,9 +132,13 @@ class DecoderLayer(nn.Module):
             self.bqkv = self.bo = self.b_up = self.b_down = None
         std = 0.02
         _init_linear(self.wqkv, std)
-        _init_linear(self.w_up, std)
+        if self.w_up is not None:
+            _init_linear(self.w_up, std)
         _init_linear(self.wo, std / math.sqrt(2 * cfg.layers))
-        _init_linear(self.w_down, std / math.sqrt(2 * cfg.layers))
+        if self.w_down is not None:
+            _init_linear(self.w_down, std / math.sqrt(2 * cfg.layers))
+        if cfg.is_moe:
+            self.moe = MoEMLP(cfg, cfg.layers, pc.ep_group, pc.ep_size, pc.ep_rank, **kw)
         for p in (self.attn_norm_w, self.mlp_norm_w, self.attn_norm_b, self.mlp_norm_b, self.bo, self.b_down):
             if p is not None:
                 p.tp_replicated = True  # identical on every TP rank (partial grads under SP)
@@ -176,6 +191,8 @@ class DecoderLayer(nn.Module):
         return out
 
     def mlp(self, xn):
+        if self.moe is not None:
+            return self.moe(xn)
         x = self._col_in(xn)
         if self.cfg.gated_mlp:
             gu = linear(x, self.w_up, self.b_up)
@@ -345,7 +362,15 @@ class DecoderLM(nn.Module):
         logits = self.head(x, residual)
         if labels is None:
             return logits
-        return self.loss(logits, labels, loss_denom)
+        loss = self.loss(logits, labels, loss_denom)
+        if self.cfg.is_moe and self.cfg.router_aux_loss_coef:
+            # load-balancing loss, averaged over layers; scaled like the CE term so gradient
+            # accumulation over micro-batches averages it
+            aux = [l.moe.aux_loss for l in self.layers if l.moe is not None and l.moe.aux_loss is not None]
+            if aux:
+                scale = labels.numel() / float(loss_denom if loss_denom is not None else labels.numel())
+                loss = loss + self.cfg.router_aux_loss_coef * scale * torch.stack(aux).mean().to(loss.dtype)
+        return loss
 
 
 def build_model(cfg: ModelConfig, device=None, dtype=torch.bfloat16, pc: Optional[ParallelContext] = None,

@@ -1,7 +1,7 @@
 """Process-group construction from a parallelism plan (TP × CP × DP × PP).
 
 Rank layout (global rank r): TP is the fastest-varying dimension, then CP (context
-parallel, Ulysses), then DP, then PP:
+parallel), then DP, then PP:
 
     r = pp_rank * (dp * cp * tp) + dp_rank * (cp * tp) + cp_rank * tp + tp_rank
 
@@ -11,6 +11,11 @@ collectives must live; the per-layer CP all-to-alls come next.  Gradients are re
 the combined DP×CP group (``dpcp``: every rank holding the same parameters).  The same
 function also produces the explicit rank lists that ``plan compute`` writes into the plan's
 ``[shard_map]`` section.
+
+Expert parallelism (MoE) lives inside DP: each DP group is cut into blocks of ``ep``
+consecutive DP ranks (an *EP group*, the all-to-all domain: on one node these are xGMI peers);
+rank ``j`` of every block holds the same expert shard, and those ranks form the *expert-DP*
+group over which the experts' gradients are reduced.
 """
 
 from __future__ import annotations
@@ -28,11 +33,14 @@ class ParallelLayout:
     pp: int = 1
     dp: int = 1
     cp: int = 1
+    ep: int = 1  # expert parallel degree (divides dp)
 
     def __post_init__(self):
         if self.tp * self.pp * self.dp * self.cp != self.world_size:
             raise ValueError(f"tp({self.tp})*cp({self.cp})*pp({self.pp})*dp({self.dp}) != "
                              f"world_size({self.world_size})")
+        if self.ep < 1 or self.dp % self.ep:
+            raise ValueError(f"expert_parallel={self.ep} must divide dp={self.dp}")
 
     def coords4(self, rank: int):
         tp_rank = rank % self.tp
@@ -73,10 +81,19 @@ class ParallelLayout:
     def pp_groups(self) -> List[List[int]]:
         return self._groups(lambda t, c, d, p: (t, c, d))
 
+    def ep_groups(self) -> List[List[int]]:
+        return self._groups(lambda t, c, d, p: (t, c, p, d // self.ep))
+
+    def edp_groups(self) -> List[List[int]]:
+        return self._groups(lambda t, c, d, p: (t, c, p, d % self.ep))
+
     def shard_map(self) -> Dict[str, List[List[int]]]:
         m = {"tp_groups": self.tp_groups(), "dp_groups": self.dp_groups(), "pp_groups": self.pp_groups()}
         if self.cp > 1:
             m["cp_groups"] = self.cp_groups()
+        if self.ep > 1:
+            m["ep_groups"] = self.ep_groups()
+            m["expert_dp_groups"] = self.edp_groups()
         return m
 
 
@@ -89,6 +106,8 @@ class ProcessGroups:
     pp_group: Optional[object] = None
     cp_group: Optional[object] = None
     dpcp_group: Optional[object] = None  # gradient-reduction group (== dp_group when cp == 1)
+    ep_group: Optional[object] = None  # MoE all-to-all group
+    edp_group: Optional[object] = None  # expert-gradient reduction group
     pp_ranks: List[int] = field(default_factory=list)
 
     @property
@@ -107,8 +126,13 @@ class ProcessGroups:
     def cp_rank(self):
         return self.layout.coords4(self.rank)[1]
 
+    @property
+    def ep_rank(self):
+        return self.dp_rank % self.layout.ep
 
-def build_process_groups(tp: int = 1, pp: int = 1, dp: Optional[int] = None, cp: int = 1) -> ProcessGroups:
+
+def build_process_groups(tp: int = 1, pp: int = 1, dp: Optional[int] = None, cp: int = 1,
+                         ep: int = 1) -> ProcessGroups:
     """Create TP/CP/DP/PP groups.  Every rank must call this with identical arguments (group
     creation is collective)."""
     if dist.is_initialized():
@@ -117,7 +141,7 @@ def build_process_groups(tp: int = 1, pp: int = 1, dp: Optional[int] = None, cp:
         world, rank = 1, 0
     if dp is None:
         dp = world // (tp * pp * cp)
-    layout = ParallelLayout(world, tp=tp, pp=pp, dp=dp, cp=cp)
+    layout = ParallelLayout(world, tp=tp, pp=pp, dp=dp, cp=cp, ep=ep)
     pg = ProcessGroups(layout=layout, rank=rank)
     if world == 1:
         pg.pp_ranks = [0]
@@ -139,6 +163,9 @@ def build_process_groups(tp: int = 1, pp: int = 1, dp: Optional[int] = None, cp:
         pg.dpcp_group = make(layout.dpcp_groups())
     else:
         pg.dpcp_group = pg.dp_group
+    if ep > 1:
+        pg.ep_group = make(layout.ep_groups())
+        pg.edp_group = make(layout.edp_groups())
     for ranks in layout.pp_groups():
         if rank in ranks:
             pg.pp_ranks = ranks

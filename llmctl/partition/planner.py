@@ -214,10 +214,27 @@ class ParallelismPlanner:
             replicated /= tp
         return 2.0 * (sharded + replicated) + 8  # + lse/rstd
 
+    def expert_parallel(self, dp: int) -> int:
+        """MoE: shard experts over the largest group of DP ranks that divides the expert count
+        and stays on one node (the per-layer token all-to-all rides the xGMI mesh); dense: 1."""
+        c = self.cfg
+        if not getattr(c, "is_moe", False):
+            return 1
+        return max(e for e in range(1, dp + 1)
+                   if dp % e == 0 and c.num_experts % e == 0 and e <= self.hw.gpus_per_node)
+
+    def _expert_params_stage(self, pp: int) -> float:
+        c = self.cfg
+        if not getattr(c, "is_moe", False):
+            return 0.0
+        return math.ceil(c.layers / pp) * c.num_experts * 3 * c.hidden * c.moe_ffn
+
     def compute_memory_requirement(self, tp: int, pp: int, dp: int, zero_stage: int, micro_batch: int,
                                    sp: bool = False, ac: str = "none", num_microbatches: int = 1) -> float:
         c = self.cfg
         P = self._stage_params(tp, pp)
+        ep = self.expert_parallel(dp)
+        P -= self._expert_params_stage(pp) * (1 - 1 / ep)  # each rank holds 1/ep of the experts
         w, g, opt = 2.0 * P, 2.0 * P, 12.0 * P
         if zero_stage >= 1:
             opt /= dp
@@ -289,7 +306,13 @@ class ParallelismPlanner:
         if zs >= 3:
             dp_time *= 1.5  # params gathered in fwd and bwd
         exposed_dp = max(dp_time - 0.8 * compute, 0.1 * dp_time)
-        total = compute_total + tp_time + pp_time + exposed_dp
+        # MoE token all-to-all: dispatch + combine, forward and backward, per layer (exposed)
+        ep_time = 0.0
+        ep = self.expert_parallel(dp)
+        if ep > 1:
+            a2a = mb * self.seq_len * c.experts_per_token * c.hidden * 2.0 * (ep - 1) / ep
+            ep_time = 4 * a2a / (self._link_bw(ep, tp) * 1e9) * math.ceil(c.layers / pp) * accum
+        total = compute_total + tp_time + pp_time + exposed_dp + ep_time
         return dict(compute_s=compute_total, tp_s=tp_time, pp_s=pp_time, dp_s=dp_time, total_s=total,
                     comm_gb=(grad_bytes * 2 * (dp > 1) + (4 * act_bytes * c.layers if tp > 1 else 0)) / GiB)
 
@@ -303,6 +326,8 @@ class ParallelismPlanner:
                 continue
             if c.heads % tp or c.kv_heads % tp or c.ffn % tp or c.vocab_size % tp or tp > self.hw.gpus_per_node:
                 continue
+            if getattr(c, "is_moe", False) and (tp > 1 or pp > 1):
+                continue  # MoE layers: expert parallelism inside DP (llmctl.models.moe)
             if pp > c.layers:
                 continue
             dp = n // (tp * pp)
@@ -327,6 +352,7 @@ class ParallelismPlanner:
         tps = gbs * self.seq_len / t["total_s"]
         return dict(tensor_parallel=tp, pipeline_parallel=pp, data_parallel=dp, zero_stage=zs,
                     sequence_parallel=sp, activation_checkpoint=ac, micro_batch_size=mb,
+                    expert_parallel=self.expert_parallel(dp),
                     global_batch_size=gbs, grad_accum=accum, num_microbatches=M,
                     estimated_memory_gb=round(mem, 3), estimated_comm_gb=round(t["comm_gb"], 3),
                     estimated_flops=self.estimate_flops(gbs), estimated_step_time_s=round(t["total_s"], 4),

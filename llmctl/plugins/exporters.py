@@ -46,6 +46,16 @@ def to_hf_llama(sd: Dict[str, torch.Tensor], cfg) -> Dict[str, torch.Tensor]:
                 out[f"{p}.mlp.up_proj.weight"] = v[f:]
             elif leaf == "w_down":
                 out[f"{p}.mlp.down_proj.weight"] = v
+            elif leaf == "moe.w_router":  # Mixtral naming
+                out[f"{p}.block_sparse_moe.gate.weight"] = v
+            elif leaf.startswith("moe.experts_up."):
+                e = leaf.rsplit(".", 1)[1]
+                f = v.shape[0] // 2
+                out[f"{p}.block_sparse_moe.experts.{e}.w1.weight"] = v[:f]
+                out[f"{p}.block_sparse_moe.experts.{e}.w3.weight"] = v[f:]
+            elif leaf.startswith("moe.experts_down."):
+                e = leaf.rsplit(".", 1)[1]
+                out[f"{p}.block_sparse_moe.experts.{e}.w2.weight"] = v
             elif leaf == "attn_norm_w":
                 out[f"{p}.input_layernorm.weight"] = v
             elif leaf == "mlp_norm_w":

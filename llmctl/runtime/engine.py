@@ -67,6 +67,7 @@ class TrainingConfig:
     pipeline_parallel: int = 1
     context_parallel: int = 1  # CP: sequence split over cp ranks (llmctl.parallel.context_parallel)
     context_parallel_mode: str = "ulysses"  # ulysses (all-to-all, xGMI-mesh friendly) | ring
+    expert_parallel: int = 1  # MoE: experts sharded over groups of this many DP ranks (llmctl.models.moe)
     pack_sequences: bool = False  # documents packed into sequences: attention/positions reset at separators
     doc_separator: int = 0  # token that ends a document (byte tokenizer / tokenize_to_bin use 0)
     sequence_parallel: bool = False
@@ -155,8 +156,11 @@ class TrainingEngine:
             raise NotImplementedError("context_parallel with pipeline_parallel is not supported")
         if c.pack_sequences and (c.context_parallel > 1 or c.pipeline_parallel > 1):
             raise NotImplementedError("pack_sequences with context / pipeline parallelism is not supported")
+        if c.expert_parallel > 1 and (c.tensor_parallel > 1 or c.pipeline_parallel > 1 or c.context_parallel > 1
+                                      or c.zero_stage >= 3):
+            raise NotImplementedError("expert_parallel composes with DP / ZeRO-1/2 only")
         self.pg: ProcessGroups = build_process_groups(tp=c.tensor_parallel, pp=c.pipeline_parallel,
-                                                      cp=c.context_parallel)
+                                                      cp=c.context_parallel, ep=c.expert_parallel)
         self.rank = self.pg.rank
         self.is_main = self.rank == 0
 
@@ -175,7 +179,8 @@ class TrainingEngine:
             sequence_parallel=c.sequence_parallel and pg.layout.tp > 1,
             layer_start=lo, layer_end=hi, has_embedding=pp_rank == 0, has_head=pp_rank == pp - 1,
             activation_checkpoint=c.activation_checkpoint,
-            cp_group=pg.cp_group, cp_size=pg.layout.cp, cp_rank=pg.cp_rank, cp_mode=c.context_parallel_mode)
+            cp_group=pg.cp_group, cp_size=pg.layout.cp, cp_rank=pg.cp_rank, cp_mode=c.context_parallel_mode,
+            ep_group=pg.ep_group, ep_size=pg.layout.ep, ep_rank=pg.ep_rank)
         # identical init on every DP replica (seeded; TP ranks get different shards, so
         # their seeds differ by tp_rank/pp_rank only)
         torch.manual_seed(c.seed + 1000 * pg.tp_rank + 100000 * pp_rank)
@@ -191,7 +196,10 @@ class TrainingEngine:
             self.flat = self.zero3.flat
         else:
             self.zero3 = None
-            self.flat = FlatParameters(list(self.model.named_parameters()), bucket_numel=bucket_numel, align=align)
+            named = list(self.model.named_parameters())
+            if pg.layout.ep > 1:  # expert shards: their own flat buffer, reduced over expert-DP
+                named = [(n, p) for n, p in named if not getattr(p, "expert", False)]
+            self.flat = FlatParameters(named, bucket_numel=bucket_numel, align=align)
             # GEMM-written weight gradients (no AccumulateGrad pass); tied embeddings excluded
             from llmctl.exec.linear import GradSink
 
@@ -214,6 +222,15 @@ class TrainingEngine:
                                        tp_group=pg.tp_group, sequence_parallel=pc.sequence_parallel)
         if self.zero3 is None and self.optimizer.zero_stage >= 1 and dp > 1:
             self._install_param_gather_hooks()
+        self.eflat = self.eopt = self.esync = None
+        if pg.layout.ep > 1:
+            experts = [(n, p) for n, p in self.model.named_parameters() if getattr(p, "expert", False)]
+            edp = dp // pg.layout.ep
+            self.eflat = FlatParameters(experts, bucket_numel=bucket_numel, align=64 * edp)
+            self.eopt = FlatAdamW(self.eflat, lr=c.learning_rate, betas=tuple(c.betas), eps=c.eps,
+                                  weight_decay=c.weight_decay, max_grad_norm=c.gradient_clipping,
+                                  dp_group=pg.edp_group, zero_stage=0)
+            self.esync = GradSyncEngine(self.eflat, group=pg.edp_group, mode="allreduce")
         total = c.max_steps if c.max_steps > 0 else 1000
         self.scheduler = LRSchedule(c.learning_rate, c.scheduler, c.warmup_steps, total)
         self.pipeline = None
@@ -271,6 +288,8 @@ class TrainingEngine:
         self.model.train()
         c = self.config
         self.flat.zero_grad()
+        if self.eflat is not None:
+            self.eflat.zero_grad()
         if self.zero3 is not None:
             self.zero3.begin_step()
         if self.pipeline is not None:
@@ -295,16 +314,26 @@ class TrainingEngine:
                     ctx = self.zero3.no_sync() if not last else _null()
                 else:
                     ctx = self.sync.no_sync() if not last else _null()
-                with ctx:
+                ectx = self.esync.no_sync() if (self.esync is not None and not last) else _null()
+                with ctx, ectx:
                     losses.append(self._forward_backward(x, y, denom))
             loss = torch.stack(losses).sum()
         if self.zero3 is not None:
             self.zero3.finish_grad_sync()
         elif self.sync is not None:
             self.sync.finish()
+        if self.esync is not None:
+            self.esync.finish()
         self.global_step += 1
         lr = self.scheduler(self.global_step)
-        gnorm = self.optimizer.step(lr=lr, grad_divisor=float(self.pg.layout.dp))
+        if self.eopt is not None:
+            # one global clip norm: the expert shards are distinct across the EP group
+            enorm = self.eopt.grad_norm_sq().clone()
+            dist.all_reduce(enorm, group=self.pg.ep_group)
+            gnorm = self.optimizer.step(lr=lr, grad_divisor=float(self.pg.layout.dp), extra_norm_sq=enorm)
+            self.eopt.step(lr=lr, grad_divisor=float(self.pg.layout.dp), coef=self.optimizer.last_coef)
+        else:
+            gnorm = self.optimizer.step(lr=lr, grad_divisor=float(self.pg.layout.dp))
         if self.zero3 is not None:
             self.zero3.after_step()
         self.consumed_samples += sum(b[0].shape[0] for b in batches) * self.pg.layout.dp
@@ -411,12 +440,25 @@ class TrainingEngine:
         named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
         with torch.no_grad():
             for n, p in named:
-                g = _global_name(n, self.pc.layer_start)
+                g = self._expert_global(_global_name(n, self.pc.layer_start))
                 t = shard_tp(g, full[g], self.pg.layout.tp, self.pg.tp_rank, self.model_config)
                 p.copy_(t.to(p.dtype))
         if self.zero3 is not None:
             self.zero3.reload_shards_from_full()
         _reinit_master_from_params(self)
+        if self.eopt is not None:
+            with torch.no_grad():
+                self.eopt.master.copy_(self.eflat.data.float())
+                self.eopt.exp_avg.zero_()
+                self.eopt.exp_avg_sq.zero_()
+
+    def _expert_global(self, name: str) -> str:
+        """Expert parameter names carry the rank-local expert index; checkpoints use global ids."""
+        if self.pg.layout.ep == 1 or (".experts_up." not in name and ".experts_down." not in name):
+            return name
+        from llmctl.models.moe import expert_param_global_name
+
+        return expert_param_global_name(name, self.pg.ep_rank * (self.model_config.num_experts // self.pg.layout.ep))
 
     def gather_full_state_dict(self) -> Dict[str, torch.Tensor]:
         """Collective: every rank returns the full unsharded model (CPU tensors)."""
@@ -424,7 +466,7 @@ class TrainingEngine:
 
         self.optimizer.wait_params()
         named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
-        local = {_global_name(n, self.pc.layer_start): p.detach().float().cpu() for n, p in named}
+        local = {self._expert_global(_global_name(n, self.pc.layer_start)): p.detach().float().cpu() for n, p in named}
         if self.zero3 is not None:
             self.zero3.release_all()
         if not dist.is_initialized():
@@ -432,10 +474,13 @@ class TrainingEngine:
         parts: List[Dict[str, torch.Tensor]] = [None] * dist.get_world_size()  # type: ignore
         dist.all_gather_object(parts, (self.pg.tp_rank, self.pg.dp_rank, local))
         by_name: Dict[str, Dict[int, torch.Tensor]] = {}
+        ep = self.pg.layout.ep
         for tp_rank, dp_rank, sd in parts:
-            if dp_rank != 0:
-                continue
             for k, v in sd.items():
+                # replicated parameters from DP rank 0; expert shards from each rank of EP block 0
+                is_expert = ep > 1 and (".experts_up." in k or ".experts_down." in k)
+                if dp_rank != 0 and not (is_expert and dp_rank < ep):
+                    continue
                 by_name.setdefault(k, {})[tp_rank] = v
         return {k: consolidate_tp(k, [s[i] for i in sorted(s)], self.model_config) for k, s in by_name.items()}
 

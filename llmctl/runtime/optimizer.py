@@ -99,6 +99,7 @@ class FlatAdamW:
         self._pending = {}  # bucket index -> (all-gather work, input buffer)
         self.overlap_param_gather = False  # engines with forward pre-hooks turn this on
         self.last_grad_norm: Optional[torch.Tensor] = None
+        self.last_coef: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ ZeRO helpers
     def shard_view(self, b: Bucket) -> torch.Tensor:
@@ -139,24 +140,33 @@ class FlatAdamW:
 
     # ------------------------------------------------------------------ step
     @torch.no_grad()
-    def step(self, lr: Optional[float] = None, grad_divisor: float = 1.0) -> torch.Tensor:
+    def step(self, lr: Optional[float] = None, grad_divisor: float = 1.0,
+             extra_norm_sq: Optional[torch.Tensor] = None, coef: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One update.  ``grad_divisor`` = DP world size × accumulation micro-steps when the
         gradients are still sums; returns the (pre-clip, averaged) global grad norm as a
-        device tensor."""
+        device tensor.  ``extra_norm_sq``: squared norm of parameters stepped by another
+        optimizer (MoE expert shards) that belongs in the same clip norm; ``coef``: apply a
+        scale computed by that other optimizer instead of computing one."""
         self.step_count += 1
         self.wait_params()  # defensive: never update a bucket whose previous gather is in flight
         lr = self.lr if lr is None else lr
-        nsq = self.grad_norm_sq()
-        norm = torch.sqrt(nsq) / grad_divisor
-        if self.max_grad_norm and self.max_grad_norm > 0:
-            coef = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0) / grad_divisor
+        if coef is None:
+            nsq = self.grad_norm_sq()
+            if extra_norm_sq is not None:
+                nsq = nsq + extra_norm_sq
+            norm = torch.sqrt(nsq) / grad_divisor
+            if self.max_grad_norm and self.max_grad_norm > 0:
+                coef = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0) / grad_divisor
+            else:
+                coef = torch.ones_like(norm) / grad_divisor
+            # skip-step policy: a non-finite global norm (identical on every rank) turns the scale
+            # into NaN, which the fused kernel treats as "leave everything untouched"
+            finite = torch.isfinite(norm)
+            coef = torch.where(finite, coef, torch.full_like(coef, float("nan")))
+            self.skipped_steps = self.skipped_steps + (~finite).to(torch.int32)
         else:
-            coef = torch.ones_like(norm) / grad_divisor
-        # skip-step policy: a non-finite global norm (identical on every rank) turns the scale
-        # into NaN, which the fused kernel treats as "leave everything untouched"
-        finite = torch.isfinite(norm)
-        coef = torch.where(finite, coef, torch.full_like(coef, float("nan")))
-        self.skipped_steps = self.skipped_steps + (~finite).to(torch.int32)
+            norm = self.last_grad_norm if self.last_grad_norm is not None else torch.zeros_like(coef)
+        self.last_coef = coef
         if self.zero_stage == 0:
             for pv, ms, g, m, v, decay, region in self._segments():
                 ops.adamw_step_(pv, ms, g, m, v, lr=lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,

@@ -22,7 +22,7 @@ DEFAULTS: Dict[str, Any] = dict(
     weight_decay=0.01, optimizer="adamw", scheduler="linear", gradient_clipping=1.0, mixed_precision="bf16",
     distributed_backend="auto", deepspeed_config=None, save_steps=500, eval_steps=500, save_total_limit=3,
     resume_from_checkpoint=None, logging_steps=10, log_level="info", seed=42, deterministic=False, config=None,
-    plan=None, seq_len=2048, tensor_parallel=1, pipeline_parallel=1, context_parallel=1, context_parallel_mode="ulysses", sequence_parallel=False, zero_stage=0,
+    plan=None, seq_len=2048, tensor_parallel=1, pipeline_parallel=1, context_parallel=1, context_parallel_mode="ulysses", expert_parallel=1, sequence_parallel=False, zero_stage=0,
     activation_checkpoint="none", num_microbatches=0, device="auto", metrics_jsonl=None, prometheus_port=0,
 )
 
@@ -64,6 +64,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--context-parallel", type=int, default=S, help="context-parallel degree")
     p.add_argument("--context-parallel-mode", type=str, choices=["ulysses", "ring"], default=S,
                    help="ulysses (all-to-all around attention) or ring attention")
+    p.add_argument("--expert-parallel", type=int, default=S, help="MoE: experts sharded over this many DP ranks")
     p.add_argument("--zero-stage", type=int, default=S)
     p.add_argument("--activation-checkpoint", type=str, choices=["none", "selective", "full"], default=S)
     p.add_argument("--num-microbatches", type=int, default=S)

@@ -87,7 +87,8 @@ class InferenceEngine:
                                                   scheduler, block_size)
         self.max_batch_size = max_batch_size
         self.rope = self.model.rope_tables(self.max_model_len, self.device)
-        self.use_graphs = use_graphs and self.device.type == "cuda"
+        # MoE routing sizes the expert segments on the host: decode runs eagerly
+        self.use_graphs = use_graphs and self.device.type == "cuda" and not cfg.is_moe
         self._graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, Dict[str, torch.Tensor]]] = {}
         self._rng = torch.Generator(device=self.device)
         self._rng.manual_seed(seed)
@@ -140,6 +141,8 @@ class InferenceEngine:
                 x[:, layer.nq + layer.nkv:].contiguous())
 
     def _mlp(self, layer, xn):
+        if layer.moe is not None:  # routed experts (host-side split sizes: eager, no graphs)
+            return layer.moe(xn)
         if self.cfg.gated_mlp:
             out = F.linear(ops.swiglu(F.linear(xn, layer.w_up, layer.b_up)), layer.w_down)
         else:

@@ -50,7 +50,8 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
                   activation_checkpoint=layout.get("ac", "none"),
                   num_microbatches=layout.get("microbatches", 0),
                   context_parallel=layout.get("cp", 1),
-                  context_parallel_mode=layout.get("cp_mode", "ulysses"))
+                  context_parallel_mode=layout.get("cp_mode", "ulysses"),
+                  expert_parallel=layout.get("ep", 1))
     eng = TrainingEngine(cfg)
     eng.load_full_state_dict(reference_state(model))
     vocab = eng.model_config.vocab_size

@@ -132,3 +132,25 @@ def test_ring_attention_matches_full_attention(world):
     for r in range(world):
         for name in ("o", "dq", "dk", "dv"):
             assert torch.allclose(out[r][name], out[r][name + "_ref"], atol=2e-5, rtol=1e-4), (r, name)
+
+
+@pytest.fixture(scope="module")
+def ref_moe_dp2():
+    return train_reference(STEPS, 2, model="tiny-moe")
+
+
+@pytest.mark.parametrize("ep,zero", [(1, 1), (2, 0), (2, 1)])
+def test_moe_expert_parallel_matches_single(ref_moe_dp2, ep, zero):
+    """Mixture of experts: DP=2 with the experts sharded over EP ranks (all-to-all token
+    dispatch, expert grads reduced over expert-DP) follows the single-process trajectory."""
+    out = run_ranks(train_layout, 2, STEPS, {"ep": ep, "zero": zero}, "tiny-moe")
+    _losses_close(out[0]["losses"], ref_moe_dp2["losses"])
+    _close(out[0]["state"], ref_moe_dp2["state"])
+
+
+def test_moe_dp4_ep2_zero1_matches_single():
+    """EP=2 inside DP=4: two EP blocks, expert gradients all-reduced over expert-DP pairs."""
+    ref = train_reference(STEPS, 4, model="tiny-moe")
+    out = run_ranks(train_layout, 4, STEPS, {"ep": 2, "zero": 1}, "tiny-moe")
+    _losses_close(out[0]["losses"], ref["losses"])
+    _close(out[0]["state"], ref["state"])
