@@ -9,11 +9,21 @@ GEMM writes the flat view itself: ``mm(..., out=view)`` on the first micro-step 
 beta = 1 epilogue, free accumulation) on later gradient-accumulation micro-steps.  The sink
 then notifies the DP overlap engine that the parameter's gradient is ready — the same
 signal ``register_post_accumulate_grad_hook`` gives for ordinary parameters.
+
+Data gradient through a transposed weight copy: ``dX = dY W`` (the "NN" GEMM) runs ~13 %
+slower on hipBLASLt than the forward's "TN" layout at the GPT-7B shapes
+(``profiles/gemm_tunable_dgradT_r1.log``: 7.27 -> 6.37 ms per layer).  Sinked weights therefore
+keep a bf16 ``W^T`` copy, refreshed by the transpose HIP kernel the first time the weight is
+used after an optimizer step (``GradSink.epoch``; under ZeRO-1/2 that is after the layer's
+all-gather has landed), and the backward computes ``dX = F.linear(dY, W^T)``.  Cost: one
+bf16 copy of the projection weights and ~2 x 13.5 GB of HBM transpose traffic per step.
 """
 
 from __future__ import annotations
 
 from typing import Callable, List, Optional
+
+import os
 
 import torch
 import torch.nn.functional as F
@@ -53,8 +63,30 @@ def wgrad_into(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate:
 
 
 class GradSink:
-    def __init__(self):
+    def __init__(self, transpose_dgrad: Optional[bool] = None):
         self.callbacks: List[Callable[[torch.nn.Parameter], None]] = []
+        if transpose_dgrad is None:
+            transpose_dgrad = os.environ.get("LLMCTL_DGRAD_TRANSPOSE", "1") != "0"
+        self.transpose_dgrad = transpose_dgrad
+        self.epoch = 0  # bumped by the engine after every optimizer step / weight load
+
+    def weight_t(self, w: torch.nn.Parameter) -> Optional[torch.Tensor]:
+        """The up-to-date ``W^T`` copy of a 2-D bf16 GPU weight (None if not applicable)."""
+        if not (self.transpose_dgrad and w.is_cuda and w.dim() == 2 and w.dtype == torch.bfloat16):
+            return None
+        from llmctl.ops._lib import native, use_native
+
+        if not use_native(w) or w.shape[0] % 8 or w.shape[1] % 8:
+            return None
+        wt = getattr(w, "_llmctl_wt", None)
+        if wt is None:
+            wt = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
+            w._llmctl_wt = wt
+            w._llmctl_wt_epoch = -1
+        if w._llmctl_wt_epoch != self.epoch:
+            native().transpose_(w.detach(), wt)
+            w._llmctl_wt_epoch = self.epoch
+        return wt
 
     def attach(self, p: torch.nn.Parameter) -> None:
         p._llmctl_grad_sink = self
@@ -81,6 +113,8 @@ class _Linear(torch.autograd.Function):
         # aliases (e.g. under activation checkpointing) that do not carry the sink
         ctx.wparam = w
         ctx.has_b = b is not None
+        sink = getattr(w, "_llmctl_grad_sink", None)
+        ctx.wt = sink.weight_t(w) if sink is not None and ctx.needs_input_grad[0] else None
         return F.linear(x, w, b)
 
     @staticmethod
@@ -95,7 +129,9 @@ class _Linear(torch.autograd.Function):
                 sink.write(ctx.wparam, dy2, x2)  # weight grad first: lets its bucket's comm start earlier
             else:
                 dw = dy2.t().matmul(x2)
-        dx = dy.matmul(w) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = F.linear(dy, ctx.wt) if ctx.wt is not None else dy.matmul(w)
         db = dy2.sum(0) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db
 
@@ -105,6 +141,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
     if getattr(w, "_llmctl_grad_sink", None) is None or not torch.is_grad_enabled():
         return F.linear(x, w, b)
     return _Linear.apply(x, w, b)
+
+
+def data_grad(dy: torch.Tensor, w: torch.nn.Parameter) -> torch.Tensor:
+    """``dy @ w`` for hand-written backward passes, through the weight's transposed copy when
+    its sink keeps one."""
+    sink = getattr(w, "_llmctl_grad_sink", None)
+    wt = sink.weight_t(w) if sink is not None else None
+    return F.linear(dy, wt) if wt is not None else dy.matmul(w)
 
 
 def weight_grad(w: torch.nn.Parameter, dy2: torch.Tensor, x2: torch.Tensor) -> Optional[torch.Tensor]:

@@ -254,6 +254,8 @@ class CheckpointManager:
         with torch.no_grad():
             for n, prm in named:
                 g = _global_name(n, e.pc.layer_start)
+                if hasattr(e, "_expert_global"):
+                    g = e._expert_global(g)
                 if g not in full:
                     raise KeyError(f"checkpoint {p} lacks tensor {g}")
                 t = shard_tp(g, full[g], e.pg.layout.tp, e.pg.tp_rank, e.model_config)
@@ -285,6 +287,8 @@ class CheckpointManager:
         e.global_step = int(state["global_step"])
         e.epoch = int(state.get("epoch", 0))
         e.consumed_samples = int(state.get("consumed_samples", 0))
+        if hasattr(e, "_weights_changed"):
+            e._weights_changed()
 
 
 def optimizer_index(e) -> Optional[Dict[str, Any]]:

@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from llmctl import ops
-from llmctl.exec.linear import linear, weight_grad
+from llmctl.exec.linear import data_grad, linear, weight_grad
 from llmctl.parallel import context_parallel as cp
 from llmctl.parallel import tensor_parallel as tp
 from .config import ModelConfig
@@ -86,7 +86,7 @@ class _SwiGLUDown(torch.autograd.Function):
         act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
         dout2 = dout.reshape(-1, dout.shape[-1])
         dw = weight_grad(ctx.wparam, dout2, act.reshape(-1, act.shape[-1]))
-        dact = dout.matmul(w_down)
+        dact = data_grad(dout, ctx.wparam)
         dgu = native().swiglu_bwd(dact, gu) if use_native(gu) else ref.swiglu_bwd(dact, gu)
         return dgu, dw
 

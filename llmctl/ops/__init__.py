@@ -22,10 +22,11 @@ from .functional import (
     rope_qkv,
     sample,
     swiglu,
+    transpose_,
 )
 
 __all__ = [
     "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy",
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
-    "rmsnorm", "rope_qkv", "sample", "swiglu",
+    "rmsnorm", "rope_qkv", "sample", "swiglu", "transpose_",
 ]

@@ -300,6 +300,15 @@ def l2norm_sq(t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 
 
 # =============================================================================== serving
+def transpose_(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """``dst[C, R] = src[R, C]`` (bf16, HIP kernel on GPU)."""
+    if use_native(src):
+        native().transpose_(src, dst)
+    else:
+        dst.copy_(src.t())
+    return dst
+
+
 def kv_cache_write(k, v, k_cache, v_cache, slot_mapping):
     if use_native(k):
         native().kv_cache_write(k, v, k_cache, v_cache, slot_mapping)
@@ -321,6 +330,7 @@ def sample(logits, temperature, top_k, top_p, uniform):
 
 
 __all__ = [
+    "transpose_",
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
     "sample",

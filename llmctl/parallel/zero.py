@@ -151,7 +151,7 @@ class Zero3Model:
     def _install_hooks(self, layers):
         from llmctl.exec.linear import GradSink
 
-        self.sink = GradSink()
+        self.sink = GradSink(transpose_dgrad=False)  # params are gathered / freed per layer
         self.flat.sink = None  # zero_grad of the shard buffer is a plain memset
         leafs = ("wqkv", "wo", "w_up", "w_down", "lm_head")
         tied = getattr(self.model.cfg, "tie_word_embeddings", False)

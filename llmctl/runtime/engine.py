@@ -189,6 +189,7 @@ class TrainingEngine:
         dp = pg.layout.dp
         align = 64 * max(dp, 1)
         bucket_numel = int(c.bucket_mb * 2**20 / torch.tensor([], dtype=c.dtype).element_size())
+        self.grad_sink = None
         if c.zero_stage >= 3 and dp > 1:
             from llmctl.parallel.zero import Zero3Model
 
@@ -205,7 +206,8 @@ class TrainingEngine:
 
             tied = mc.tie_word_embeddings
             leafs = ("wqkv", "wo", "w_up", "w_down") + (() if tied else ("lm_head",))
-            self.flat.install_sinks(GradSink(), lambda n, p: n.split(".")[-1] in leafs)
+            self.grad_sink = GradSink()
+            self.flat.install_sinks(self.grad_sink, lambda n, p: n.split(".")[-1] in leafs)
         norm_group = pg.pp_group if pp > 1 else None
         self.optimizer = FlatAdamW(self.flat, lr=c.learning_rate, betas=tuple(c.betas), eps=c.eps,
                                    weight_decay=c.weight_decay, max_grad_norm=c.gradient_clipping,
@@ -336,6 +338,7 @@ class TrainingEngine:
             gnorm = self.optimizer.step(lr=lr, grad_divisor=float(self.pg.layout.dp))
         if self.zero3 is not None:
             self.zero3.after_step()
+        self._weights_changed()
         self.consumed_samples += sum(b[0].shape[0] for b in batches) * self.pg.layout.dp
         return {"loss": loss, "grad_norm": gnorm, "lr": torch.tensor(lr)}
 
@@ -446,11 +449,18 @@ class TrainingEngine:
         if self.zero3 is not None:
             self.zero3.reload_shards_from_full()
         _reinit_master_from_params(self)
+        self._weights_changed()
         if self.eopt is not None:
             with torch.no_grad():
                 self.eopt.master.copy_(self.eflat.data.float())
                 self.eopt.exp_avg.zero_()
                 self.eopt.exp_avg_sq.zero_()
+
+    def _weights_changed(self) -> None:
+        """Parameters were rewritten (optimizer step, state load): derived copies (the
+        transposed dgrad weights) refresh on next use."""
+        if self.grad_sink is not None:
+            self.grad_sink.epoch += 1
 
     def _expert_global(self, name: str) -> str:
         """Expert parameter names carry the rank-local expert index; checkpoints use global ids."""

@@ -363,3 +363,35 @@ def test_moe_model_step_gpu(native_lib):
         if p.grad is not None:
             assert torch.isfinite(p.grad.float()).all(), n
     assert gpu.layers[0].moe.w_router.grad is not None
+
+
+@pytest.mark.parametrize("R,C", [(264, 136), (4096, 12288), (64, 8)])
+def test_transpose_kernel(native_lib, R, C):
+    x = _bf(R, C, seed=R + C)
+    y = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    native_lib.transpose_(x, y)
+    assert torch.equal(y, x.t())
+
+
+def test_linear_dgrad_through_transposed_weight(native_lib):
+    """Sinked weights compute dX = F.linear(dY, W^T) from a cached transposed copy; the copy
+    refreshes after the weights change (GradSink.epoch)."""
+    from llmctl.exec.linear import GradSink, linear
+
+    w = torch.nn.Parameter(_bf(512, 256, seed=5) * 0.05)
+    w.grad = torch.zeros_like(w)
+    sink = GradSink(transpose_dgrad=True)
+    sink.attach(w)
+    x = _bf(128, 256, seed=6).requires_grad_(True)
+    dy = _bf(128, 512, seed=7)
+    for step in range(2):
+        sink.reset(w)
+        y = linear(x, w)
+        y.backward(dy)
+        ref_dx = (dy.float() @ w.detach().float())
+        assert (x.grad.float() - ref_dx).abs().max().item() < 2e-2 * ref_dx.abs().max().item(), step
+        assert torch.equal(w._llmctl_wt, w.detach().t())
+        x.grad = None
+        with torch.no_grad():
+            w.mul_(1.5)  # an "optimizer step"
+        sink.epoch += 1

@@ -61,13 +61,22 @@ def main():
         w = (torch.randn(N, K, device=dev, generator=g) * 0.02).bfloat16()
         dy = (torch.randn(T, N, device=dev, generator=g) * 1e-2).bfloat16()
         data[name] = (x, w, dy, torch.empty(N, K, device=dev, dtype=torch.bfloat16))
+        if "wgradT" in want:  # K(=tokens)-contiguous copies: the wgrad as an NT GEMM
+            data[name] += (dy.t().contiguous(), x.t().contiguous())
+        if "dgradT" in want:  # a transposed weight copy: the dgrad in the forward's (TN) layout
+            data[name] += (None, None, w.t().contiguous())
 
     def ops_for(name):
-        x, w, dy, dw = data[name]
+        x, w, dy, dw = data[name][:4]
+        dyT, xT = data[name][4:6] if len(data[name]) > 4 else (None, None)
+        wT = data[name][6] if len(data[name]) > 6 else None
         return {k: f for k, f in {
             "fwd": lambda: F.linear(x, w),
             "dgrad": lambda: dy @ w,
             "wgrad": lambda: torch.mm(dy.t(), x, out=dw),
+            "wgradT": lambda: torch.mm(dyT, xT.t(), out=dw),
+            "dgradT": lambda: F.linear(dy, wT),
+            "transpose": lambda: (dy.t().contiguous(), x.t().contiguous()),
         }.items() if k in want}
 
     res = {}
@@ -84,7 +93,7 @@ def main():
     run("hipblaslt")
     for name in (SHAPES if "wgrad" in want else []):  # the llmctl MFMA wgrad kernel
         N, K = SHAPES[name]
-        x, w, dy, dw = data[name]
+        x, w, dy, dw = data[name][:4]
         ms = timeit(lambda: ops.gemm_ex(dy, x, dw, True, True, False))
         res[name]["wgrad_llmctl"] = {"ms": round(ms, 4), "tflops": round(2.0 * T * N * K / ms / 1e9, 1)}
         print(name, "wgrad llmctl", res[name]["wgrad_llmctl"], flush=True)
