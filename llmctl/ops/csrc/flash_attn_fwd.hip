@@ -18,7 +18,11 @@
 //     reuse of the K/V stream) when B*Hq % 8 == 0;
 //   * packed sequences (optional ``doc_start[B,S]``: position where each token's document
 //     begins, non-decreasing): key j is visible to query i iff doc_start[i] <= j <= i; the
-//     K/V loop starts at the block's first document start, so the work is sum(doc_len^2).
+//     K/V loop starts at the block's first document start, so the work is sum(doc_len^2);
+//   * small grids (e.g. a single 2k-token prefill: 1 x 32 heads x 16 q-blocks = 512 workgroups,
+//     all resident at once, so the run time is the heaviest block's): the K/V range of every
+//     q-block is split over two workgroups that write fp32 partial outputs + LSEs, merged by a
+//     combine kernel — halves the critical path of the causal tail.
 // Outputs O [B,S,Hq,HD] bf16 and LSE [B,Hq,S] fp32 (natural log) for the backward pass.
 #include "attn_common.h"
 
@@ -42,9 +46,11 @@ struct FwdArgs {
   long o_sb, o_ss, o_sh;
   float scale_log2;  // softmax_scale * log2(e)
   const int* doc;    // [B, S] document start per token, or nullptr
+  float* o_part;     // SPLIT: [2, B, S, Hq, HD] fp32 normalised partial outputs
+  float* lse_part;   // SPLIT: [2, B, Hq, S] natural-log partial LSEs
 };
 
-template <int HD, bool CAUSAL, bool DOC = false>
+template <int HD, bool CAUSAL, bool DOC = false, bool SPLIT = false>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
   constexpr int NKS = HD / 16;  // k-steps of QK^T
   constexpr int NDB = HD / 32;  // 32-wide d blocks of O
@@ -61,7 +67,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
   const int nqb = (a.S + QB - 1) / QB;
   const int BH = a.B * a.Hq;
   const int bh = blockIdx.x % BH;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (largest causal span) first
+  const int rest = blockIdx.x / BH;
+  const int part = SPLIT ? rest & 1 : 0;
+  const int qblk = nqb - 1 - (SPLIT ? rest >> 1 : rest);  // heaviest (largest causal span) first
   const int b = bh / a.Hq, hq = bh % a.Hq;
   const int hk = hq / (a.Hq / a.Hkv);
   const int q_row0 = qblk * QB + wave * 32;
@@ -88,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
   float m_i = -INFINITY, l_i = 0.f;
 
   const int kv_end = CAUSAL ? min(a.S, qblk * QB + QB) : a.S;
-  const int ntiles = (kv_end + KB - 1) / KB;
+  int ntiles = (kv_end + KB - 1) / KB;
   // packed documents: this lane's first visible key, the wave's min / max of it (doc_start is
   // non-decreasing) and the block's first tile
   int my_start = 0, w_min = 0, w_max = 0, t0 = 0;
@@ -98,6 +106,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     w_min = ds[min(q_row0, a.S - 1)];
     w_max = ds[min(q_row0 + 31, a.S - 1)];
     t0 = ds[min(qblk * QB, a.S - 1)] / KB;
+  }
+  if constexpr (SPLIT) {  // part 0: tiles [t0, mid), part 1: [mid, ntiles) (holds the diagonal)
+    const int mid = (t0 + ntiles) / 2;
+    if (part == 0) ntiles = mid;
+    else t0 = mid;
   }
 
   // ---- staging registers for one K and one V tile
@@ -201,6 +214,24 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
   }
 
   // ---- epilogue: O = O^T^T / l ; LSE
+  if constexpr (SPLIT) {
+    if (my_q < a.S) {
+      const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+      float* Op = a.o_part + ((((long)part * a.B + b) * a.S + my_q) * a.Hq + hq) * HD;
+#pragma unroll
+      for (int d = 0; d < NDB; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = d * 32 + 8 * g + 4 * hh;
+          *reinterpret_cast<float4*>(Op + col) =
+              make_float4(o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+        }
+      if (hh == 0)
+        a.lse_part[(((long)part * a.B + b) * a.Hq + hq) * a.S + my_q] =
+            (l_i > 0.f) ? (m_i + __log2f(l_i)) * 0.69314718055994531f : -INFINITY;
+    }
+    return;
+  }
   if (my_q < a.S) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
     unsigned short* Op = a.o + b * a.o_sb + (long)my_q * a.o_ss + hq * a.o_sh;
@@ -220,6 +251,48 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
       a.lse[((long)b * a.Hq + hq) * a.S + my_q] = lse;
     }
   }
+}
+
+// merge the two K/V-range halves: lse = logaddexp(l0, l1), o = o0 e^(l0-lse) + o1 e^(l1-lse)
+template <int HD>
+__global__ __launch_bounds__(256) void fa_combine_kernel(const float* __restrict__ o_part,
+                                                         const float* __restrict__ lse_part,
+                                                         unsigned short* __restrict__ o, float* __restrict__ lse,
+                                                         int B, int S, int Hq, long o_sb, long o_ss, long o_sh) {
+  constexpr int LPR = HD / 8;  // lanes per (b, s, h) row, 8 elements each
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long row = gid / LPR;  // (b, s, h) in [B, S, Hq] order
+  const int sub = gid % LPR;
+  if (row >= (long)B * S * Hq) return;
+  const int hq = row % Hq;
+  const long bs = row / Hq;
+  const int sq = bs % S;
+  const int b = bs / S;
+  const long li = ((long)b * Hq + hq) * S + sq;
+  const long plane = (long)B * Hq * S;
+  const float l0 = lse_part[li], l1 = lse_part[plane + li];
+  const float m = fmaxf(l0, l1);
+  float w0 = 0.f, w1 = 0.f, l = -INFINITY;
+  if (m != -INFINITY) {
+    const float e0 = __expf(l0 - m), e1 = __expf(l1 - m);
+    l = m + __logf(e0 + e1);
+    w0 = e0 / (e0 + e1);
+    w1 = e1 / (e0 + e1);
+  }
+  const long ob = row * HD + sub * 8;
+  const long osz = (long)B * S * Hq * HD;
+  float out[8];
+#pragma unroll
+  for (int j = 0; j < 8; j += 4) {
+    const float4 x0 = *reinterpret_cast<const float4*>(o_part + ob + j);
+    const float4 x1 = *reinterpret_cast<const float4*>(o_part + osz + ob + j);
+    out[j] = w0 * x0.x + w1 * x1.x;
+    out[j + 1] = w0 * x0.y + w1 * x1.y;
+    out[j + 2] = w0 * x0.z + w1 * x1.z;
+    out[j + 3] = w0 * x0.w + w1 * x1.w;
+  }
+  store8(o + b * o_sb + (long)sq * o_ss + (long)hq * o_sh + sub * 8, out);
+  if (sub == 0) lse[li] = l;
 }
 
 }  // namespace
@@ -250,10 +323,32 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   FwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_mut(o), lse.data_ptr<float>(), B, S, Hq, Hkv,
             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
-            (float)(scale * 1.4426950408889634), nullptr};
+            (float)(scale * 1.4426950408889634), nullptr, nullptr, nullptr};
   const int nqb = (S + QB - 1) / QB;
   dim3 grid((unsigned)(B * Hq * nqb)), block(256);
   auto s = stream();
+  // a grid that the CUs hold in one residency round (2 workgroups per CU) finishes when its
+  // heaviest causal block does: split every block's K/V range over two workgroups
+  const bool split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 4 &&
+                     (long)B * Hq * nqb <= 2L * num_cus();
+  if (split) {
+    auto o_part = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
+    auto lse_part = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));
+    a.o_part = o_part.data_ptr<float>();
+    a.lse_part = lse_part.data_ptr<float>();
+    dim3 g2((unsigned)(2 * B * Hq * nqb));
+    const long threads = (long)B * S * Hq * (D / 8);
+    if (D == 128) {
+      hipLaunchKernelGGL((fa_fwd_kernel<128, true, false, true>), g2, block, 0, s, a);
+      hipLaunchKernelGGL(fa_combine_kernel<128>, dim3((threads + 255) / 256), dim3(256), 0, s, a.o_part, a.lse_part,
+                         bf_mut(o), lse.data_ptr<float>(), B, S, Hq, o.stride(0), o.stride(1), o.stride(2));
+    } else {
+      hipLaunchKernelGGL((fa_fwd_kernel<64, true, false, true>), g2, block, 0, s, a);
+      hipLaunchKernelGGL(fa_combine_kernel<64>, dim3((threads + 255) / 256), dim3(256), 0, s, a.o_part, a.lse_part,
+                         bf_mut(o), lse.data_ptr<float>(), B, S, Hq, o.stride(0), o.stride(1), o.stride(2));
+    }
+    return {o, lse};
+  }
   if (doc_start.has_value() && doc_start->defined()) {
     const at::Tensor& ds = *doc_start;
     LLMCTL_CHECK(causal, "flash_attn_fwd: doc_start (packed sequences) needs causal attention");

@@ -160,6 +160,8 @@ ATTN_CASES = [
     (2, 320, 8, 2, 128, True),
     (1, 130, 4, 1, 64, True),
     (1, 300, 4, 1, 128, False),
+    (1, 512, 4, 2, 64, True),  # small grid: K/V-split forward + combine
+    (1, 2048, 8, 8, 128, True),
 ]
 
 
