@@ -224,6 +224,14 @@ class TrainingEngine:
                                        tp_group=pg.tp_group, sequence_parallel=pc.sequence_parallel)
         if self.zero3 is None and self.optimizer.zero_stage >= 1 and dp > 1:
             self._install_param_gather_hooks()
+        elif (self.zero3 is None and self.optimizer.zero_stage == 0 and self.device.type == "cuda" and pp == 1
+              and os.environ.get("LLMCTL_OVERLAP_OPTIMIZER", "0") == "1"):
+            # opt-in: measured neutral on GPT-7B mb 12 (27.7k vs 27.9k tok/s in one A/B,
+            # profiles/bench_r1_overlap_opt_ab.jsonl) — the concurrent AdamW slows the GEMMs
+            # about as much as it hides
+            self._install_param_gather_hooks()
+            self.optimizer.overlap_param_gather = False
+            self.optimizer.overlap_update = True
         self.eflat = self.eopt = self.esync = None
         if pg.layout.ep > 1:
             experts = [(n, p) for n, p in self.model.named_parameters() if getattr(p, "expert", False)]
@@ -247,7 +255,8 @@ class TrainingEngine:
     def _install_param_gather_hooks(self) -> None:
         """ZeRO-1/2: the post-step all-gather of updated parameter shards overlaps the next
         forward — each decoder layer (and the top-level module, for embedding / head / final
-        norm) waits only for the buckets holding its own parameters."""
+        norm) waits only for the buckets holding its own parameters.  ZeRO-0 on one GPU uses
+        the same hooks for the side-stream optimizer update (``FlatAdamW.overlap_update``)."""
         flat, opt = self.flat, self.optimizer
 
         def buckets_of(params):
@@ -270,7 +279,11 @@ class TrainingEngine:
                              device=self.device)
 
     # ------------------------------------------------------------------ step
-    def _forward_backward(self, input_ids, labels, denom):
+    def _late_zero_grad(self) -> None:
+        self.optimizer.wait_params()  # every bucket's update has been ordered before this point
+        self.flat.zero_grad()
+
+    def _forward_backward(self, input_ids, labels, denom, before_backward=None):
         doc_start = None
         if self.config.pack_sequences:
             from llmctl.ops.ref import document_starts
@@ -281,6 +294,8 @@ class TrainingEngine:
         loss = self.model(input_ids, labels, loss_denom=denom, doc_start=doc_start)
         if self.faults and self.faults.nan_loss(self.global_step + 1):
             loss = loss * float("nan")
+        if before_backward is not None:
+            before_backward()
         loss.backward()
         return loss.detach()
 
@@ -289,7 +304,11 @@ class TrainingEngine:
         device tensors (no host sync): mean loss and grad norm."""
         self.model.train()
         c = self.config
-        self.flat.zero_grad()
+        # with the side-stream update the previous step may still be reading the gradients:
+        # zero them only once the first forward has waited for every bucket (its pre-hooks)
+        late_zero = self.optimizer.overlap_update
+        if not late_zero:
+            self.flat.zero_grad()
         if self.eflat is not None:
             self.eflat.zero_grad()
         if self.zero3 is not None:
@@ -318,7 +337,8 @@ class TrainingEngine:
                     ctx = self.sync.no_sync() if not last else _null()
                 ectx = self.esync.no_sync() if (self.esync is not None and not last) else _null()
                 with ctx, ectx:
-                    losses.append(self._forward_backward(x, y, denom))
+                    losses.append(self._forward_backward(x, y, denom, before_backward=(
+                        self._late_zero_grad if late_zero and i == 0 else None)))
             loss = torch.stack(losses).sum()
         if self.zero3 is not None:
             self.zero3.finish_grad_sync()

@@ -25,6 +25,16 @@ from llmctl import ops
 from llmctl.runtime.flat import Bucket, FlatParameters
 
 
+class _StreamEvent:
+    """A pending side-stream update: ``wait()`` orders the current stream after it."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
 class LRSchedule:
     """``constant`` | ``linear`` (reference default, engine.py:246-253) | ``cosine``
     (declared by reference configs but unsupported there)."""
@@ -98,6 +108,8 @@ class FlatAdamW:
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=dev)
         self._pending = {}  # bucket index -> (all-gather work, input buffer)
         self.overlap_param_gather = False  # engines with forward pre-hooks turn this on
+        self.overlap_update = False  # ZeRO-0: per-bucket update on a side stream, waited per layer
+        self._update_stream = None
         self.last_grad_norm: Optional[torch.Tensor] = None
         self.last_coef: Optional[torch.Tensor] = None
 
@@ -167,7 +179,27 @@ class FlatAdamW:
         else:
             norm = self.last_grad_norm if self.last_grad_norm is not None else torch.zeros_like(coef)
         self.last_coef = coef
-        if self.zero_stage == 0:
+        if self.zero_stage == 0 and self.overlap_update:
+            # bucket by bucket, in forward order, on a side stream: the HBM-bound update of
+            # bucket i+1.. runs under the next forward's (MFMA-bound) GEMMs of the layers in
+            # bucket i; each layer's forward pre-hook waits only for its own buckets' events
+            f = self.flat
+            if self._update_stream is None:
+                self._update_stream = torch.cuda.Stream(device=f.device)
+            side = self._update_stream
+            coef.record_stream(side)  # (before the wait: record_stream counts as a main-stream access)
+            side.wait_stream(torch.cuda.current_stream(f.device))
+            with torch.cuda.stream(side):
+                for b in sorted(f.buckets, key=lambda b: b.start):
+                    s0, s1 = b.start, b.end
+                    ops.adamw_step_(f.data[s0:s1], self.master[s0:s1], f.grad[s0:s1], self.exp_avg[s0:s1],
+                                    self.exp_avg_sq[s0:s1], lr=lr, beta1=self.beta1, beta2=self.beta2,
+                                    eps=self.eps, weight_decay=self.weight_decay if b.decay else 0.0,
+                                    step=self.step_count, grad_scale=coef)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    self._pending[b.index] = (_StreamEvent(ev), None)
+        elif self.zero_stage == 0:
             for pv, ms, g, m, v, decay, region in self._segments():
                 ops.adamw_step_(pv, ms, g, m, v, lr=lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
                                 weight_decay=self.weight_decay if decay else 0.0, step=self.step_count,
