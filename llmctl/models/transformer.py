@@ -265,6 +265,9 @@ class DecoderLM(nn.Module):
             if p is not None:
                 p.tp_replicated = True
         self._rope_cache = {}
+        # called at the top of ``head()``: the engine's ZeRO-1/2 (and side-stream optimizer)
+        # overlap waits here for the final-norm / LM-head buckets, which are gathered last
+        self.pre_head_hook = None
 
     # ------------------------------------------------------------------ helpers
     def head_weight(self):
@@ -326,6 +329,8 @@ class DecoderLM(nn.Module):
 
     def head(self, x, residual):
         cfg = self.cfg
+        if self.pre_head_hook is not None:
+            self.pre_head_hook()
         if residual is None:
             xn = (ops.layernorm(x, self.final_norm_w, self.final_norm_b, cfg.layer_norm_eps)
                   if self.final_norm_b is not None else ops.rmsnorm(x, self.final_norm_w, cfg.layer_norm_eps))

@@ -265,10 +265,18 @@ class TrainingEngine:
         def hook_for(idx):
             return lambda module, args: opt.wait_params(idx)
 
-        top = [p for n, p in self.model.named_parameters() if not n.startswith("layers.")]
-        self._gather_hooks = [self.model.register_forward_pre_hook(hook_for(buckets_of(top)))]
+        # the embedding buckets are gathered first and the final-norm / LM-head buckets last
+        # (flat-offset order): the top-level pre-hook waits only for the former, the head for
+        # the latter — waiting for every top-level parameter up front would serialise the
+        # whole gather (or side-stream update) before the first layer
+        named = [(n, p) for n, p in self.model.named_parameters() if not n.startswith("layers.")]
+        front = [p for n, p in named if n in ("embed", "pos_embed")]
+        back = [p for n, p in named if n not in ("embed", "pos_embed")]
+        self._gather_hooks = [self.model.register_forward_pre_hook(hook_for(buckets_of(front)))]
         for layer in self.model.layers:
             self._gather_hooks.append(layer.register_forward_pre_hook(hook_for(buckets_of(layer.parameters()))))
+        back_idx = buckets_of(back)
+        self.model.pre_head_hook = lambda: opt.wait_params(back_idx)
         opt.overlap_param_gather = True
 
     # ------------------------------------------------------------------ data

@@ -25,6 +25,14 @@ from llmctl import ops
 from llmctl.runtime.flat import Bucket, FlatParameters
 
 
+def forward_order(buckets):
+    """Buckets in the order the next forward needs them: the small 1-D regions (norm weights /
+    biases of EVERY layer, incl. layer 0's) first, then the matrices in flat order (embedding,
+    layer 0, ..., LM head).  Flat-offset order would put the norm buckets last, and layer 0's
+    pre-hook would then wait for the whole gather / update."""
+    return sorted(buckets, key=lambda b: (b.region == "decay", b.start))
+
+
 class _StreamEvent:
     """A pending side-stream update: ``wait()`` orders the current stream after it."""
 
@@ -190,7 +198,7 @@ class FlatAdamW:
             coef.record_stream(side)  # (before the wait: record_stream counts as a main-stream access)
             side.wait_stream(torch.cuda.current_stream(f.device))
             with torch.cuda.stream(side):
-                for b in sorted(f.buckets, key=lambda b: b.start):
+                for b in forward_order(f.buckets):
                     s0, s1 = b.start, b.end
                     ops.adamw_step_(f.data[s0:s1], self.master[s0:s1], f.grad[s0:s1], self.exp_avg[s0:s1],
                                     self.exp_avg_sq[s0:s1], lr=lr, beta1=self.beta1, beta2=self.beta2,
@@ -209,7 +217,7 @@ class FlatAdamW:
             # RCCL gather of bucket i runs while AdamW updates bucket i+1, and with
             # ``overlap_param_gather`` the waits move to the next forward (per-module hooks)
             f = self.flat
-            for b in sorted(f.buckets, key=lambda b: b.start):
+            for b in forward_order(f.buckets):
                 off, c = self.shard_offsets[b.index]
                 s = b.start + self.dp_rank * c
                 ops.adamw_step_(f.data[s:s + c], self.master[off:off + c], self.grad_shard[off:off + c],

@@ -242,3 +242,40 @@ def test_scheduled_profiler_writes_trace(tmp_path):
     eng.train()
     traces = list((tmp_path / "prof").glob("trace_rank00000_step*.json"))
     assert len(traces) == 1 and "llmctl.train_step" in traces[0].read_text()
+
+
+# ---------------------------------------------------------------- ZeRO gather / side-stream update overlap order
+@pytest.mark.parametrize("tied", [False, True])
+def test_param_gather_waits_follow_forward_order(tied):
+    """The post-step parameter all-gather (ZeRO-1/2) is issued in ``forward_order``; each
+    forward pre-hook may only wait for buckets up to its own layer's position in that order.
+    Regression: the norm-weight bucket sat last in flat order and was waited by layer 0 (and
+    the LM-head bucket by the top-level hook), which serialised the whole gather before the
+    first layer."""
+    import dataclasses
+    from types import SimpleNamespace
+
+    from llmctl.models import build_model, get_model_config
+    from llmctl.runtime.engine import TrainingEngine
+    from llmctl.runtime.flat import FlatParameters
+    from llmctl.runtime.optimizer import forward_order
+
+    cfg = dataclasses.replace(get_model_config("tiny"), tie_word_embeddings=tied)
+    m = build_model(cfg, dtype=torch.float32)
+    flat = FlatParameters(list(m.named_parameters()), bucket_numel=4096)
+    order = {b.index: i for i, b in enumerate(forward_order(flat.buckets))}
+    assert len(order) > 2 * cfg.layers
+    waits = []
+    opt = SimpleNamespace(wait_params=lambda idx: waits.append([order[i] for i in idx]))
+    TrainingEngine._install_param_gather_hooks(SimpleNamespace(flat=flat, optimizer=opt, model=m))
+    ids = torch.randint(0, cfg.vocab_size, (1, 8))
+    m(ids, ids)
+    assert len(waits) == cfg.layers + 2  # top-level, every layer, head
+    # layer k may only need the buckets issued up to about its own share of the gather
+    per_layer = -(-len(order) // cfg.layers)
+    seen = -1
+    for k, w in enumerate(waits[:-1]):
+        seen = max([seen, *w])
+        assert seen <= (k + 1) * per_layer + 1, (k, seen, len(order), waits)
+    seen = max([seen, *waits[-1]])
+    assert seen == len(order) - 1  # everything is waited by the end of the forward
