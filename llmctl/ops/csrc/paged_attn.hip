@@ -4,12 +4,22 @@
 // contiguous (D*2 bytes), a block holds block_size consecutive tokens of one sequence.
 //
 // Decode (one new token per sequence) is HBM-bound: every cached K/V byte is read once.
-// Workgroup = one (sequence, kv-head) pair = 4 waves; the `group = Hq/Hkv` query heads that
-// share the kv head are handled together so GQA reads K/V once per group.  Inside a wave,
-// 16 lanes cooperate on one token (8 contiguous bf16 of D=128 per lane: 16-B loads), so a
-// wave-instruction covers 4 tokens; q·k is reduced over the 16 lanes with xor-shuffles.  Each
-// wave streams a contiguous slice of the context with an online softmax; the 4 waves (and
-// the 4 token groups within each wave) are merged through LDS at the end.
+// Workgroup = one (sequence, kv-head, context split) = 4 waves; the `group = Hq/Hkv` query
+// heads that share the kv head are handled together so GQA reads K/V once per group.  Inside a
+// wave, 16 lanes cooperate on one token (8 contiguous bf16 of D=128 per lane: 16-B loads), so
+// a wave-instruction covers 4 tokens; q·k is reduced over the 16 lanes with xor-shuffles.
+// Each wave streams a contiguous slice of its split with an online softmax, U tokens per lane
+// per iteration: all U block-table reads, then all 2U K/V loads are issued before the first
+// use (with one token per iteration the loop is latency-bound: one 16-B load pair in flight
+// per lane).  The 4 waves (and the 4 token groups within each wave) are merged through LDS.
+// Small batches (N·Hkv workgroups, far fewer than the ~2k that cover 256 CUs' HBM latency)
+// split the context over `nsplit` workgroups (flash-decoding): fp32 partials (O unnormalised,
+// running max m in the log2 domain, sum l) + a combine kernel.  nsplit depends only on
+// shapes (batch rounded up to the decode-graph bucket), so a captured hipGraph stays valid for
+// any context lengths and graph / eager decode agree bit for bit.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace llmctl {
@@ -30,19 +40,21 @@ __global__ __launch_bounds__(256) void kv_write_kernel(const unsigned short* __r
   reinterpret_cast<uint4*>(vc)[slot * row8 + c] = reinterpret_cast<const uint4*>(v)[(long)t * row8 + c];
 }
 
-template <int D, int G>
+template <int D, int G, int U>
 __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short* __restrict__ q,
                                                             const unsigned short* __restrict__ kc,
                                                             const unsigned short* __restrict__ vc,
                                                             const int* __restrict__ block_tables,
                                                             const int* __restrict__ ctx_lens,
-                                                            unsigned short* __restrict__ out, int Hq, int Hkv,
-                                                            int block_size, int max_blocks, float scale_log2) {
+                                                            unsigned short* __restrict__ out,
+                                                            float* __restrict__ part_o, float* __restrict__ part_ml,
+                                                            int Hq, int Hkv, int block_size, int max_blocks,
+                                                            float scale_log2, int nsplit) {
   constexpr int LPT = D / 8;          // lanes per token (16 for D=128, 8 for D=64)
   constexpr int TPW = 64 / LPT;       // tokens per wave-instruction
   __shared__ float sm_m[4 * TPW][G], sm_l[4 * TPW][G];
   __shared__ float sm_o[4 * TPW][G][D];
-  const int seq = blockIdx.x / Hkv, hk = blockIdx.x % Hkv;
+  const int seq = blockIdx.x / Hkv, hk = blockIdx.x % Hkv, split = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane % LPT;         // which 8-element slice of D
   const int tg = lane / LPT;          // token group inside the wave
@@ -60,30 +72,49 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
   }
-  // contiguous token slice per wave
-  const int per_wave = (L + 3) / 4;
-  const int t0 = wave * per_wave, t1 = min(L, t0 + per_wave);
+  // this workgroup's context split, then a contiguous token slice per wave
+  const int chunk = (L + nsplit - 1) / nsplit;
+  const int c0 = min(L, split * chunk), c1 = min(L, c0 + chunk);
+  const int per_wave = (c1 - c0 + 3) / 4;
+  const int t0 = c0 + wave * per_wave, t1 = min(c1, t0 + per_wave);
   const long kv_row = (long)Hkv * D;
-  for (int t = t0 + tg; t < t1; t += TPW) {
-    const int blk = bt[t / block_size];
-    const long base = ((long)blk * block_size + (t % block_size)) * kv_row + (long)hk * D + sub * 8;
-    float kf[8], vf[8];
-    load8(kc + base, kf);
-    load8(vc + base, vf);
+  for (int t = t0 + tg; t < t1; t += TPW * U) {
+    int blk[U];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float s = 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int tt = t + u * TPW;
+      blk[u] = tt < t1 ? bt[tt / block_size] : -1;
+    }
+    float kf[U][8], vf[U][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += qv[g][j] * kf[j];
+    for (int u = 0; u < U; ++u) {
+      const int tt = t + u * TPW;
+      if (blk[u] >= 0) {
+        const long base = ((long)blk[u] * block_size + (tt % block_size)) * kv_row + (long)hk * D + sub * 8;
+        load8(kc + base, kf[u]);
+        load8(vc + base, vf[u]);
+      }
+    }
 #pragma unroll
-      for (int off = LPT / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
-      s *= scale_log2;
-      const float mn = fmaxf(m[g], s);
-      const float a = exp2f(m[g] - mn), p = exp2f(s - mn);
-      l[g] = l[g] * a + p;
+    for (int u = 0; u < U; ++u) {
+      // validity is uniform over the LPT lanes of a token group, so the shuffles below only
+      // ever read lanes that take the same branch
+      if (blk[u] < 0) continue;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + p * vf[j];
-      m[g] = mn;
+      for (int g = 0; g < G; ++g) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += qv[g][j] * kf[u][j];
+#pragma unroll
+        for (int off = LPT / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        s *= scale_log2;
+        const float mn = fmaxf(m[g], s);
+        const float a = exp2f(m[g] - mn), p = exp2f(s - mn);
+        l[g] = l[g] * a + p;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + p * vf[u][j];
+        m[g] = mn;
+      }
     }
   }
   // publish per (wave, token-group) partials
@@ -111,8 +142,54 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
         O += sm_o[s][g][d] * w;
       }
     }
-    out[((long)seq * Hq + hk * G + g) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+    const long row = (long)seq * Hq + hk * G + g;
+    if (nsplit == 1) {
+      out[row * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+    } else {
+      const long p = row * nsplit + split;
+      part_o[p * D + d] = O;
+      if (d == 0) {
+        part_ml[2 * p] = M;
+        part_ml[2 * p + 1] = Ls;
+      }
+    }
   }
+}
+
+// out[row] = sum_s O_s 2^(m_s - M) / sum_s l_s 2^(m_s - M); empty splits carry m = -inf.
+template <int D>
+__global__ __launch_bounds__(D) void paged_combine_kernel(const float* __restrict__ part_o,
+                                                          const float* __restrict__ part_ml,
+                                                          unsigned short* __restrict__ out, int nsplit) {
+  const long row = blockIdx.x;
+  const int d = threadIdx.x;
+  const float* ml = part_ml + row * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  float Ls = 0.f, O = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < nsplit; ++s) {
+      const float w = exp2f(ml[2 * s] - M);
+      Ls += ml[2 * s + 1] * w;
+      O += part_o[(row * nsplit + s) * D + d] * w;
+    }
+  }
+  out[row * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+}
+
+// Context splits per (sequence, kv-head): enough workgroups for ~8 per CU, at least 128
+// context slots per split, at most 16.  The batch is rounded up to a power of two, as the
+// serving engine's decode-graph buckets are, so graph replay and eager decode pick the same
+// split.  LLMCTL_DECODE_SPLITS overrides (tests, A/B).
+int decode_splits(int N, int Hkv, int max_ctx) {
+  if (const char* e = std::getenv("LLMCTL_DECODE_SPLITS")) {
+    const int v = std::atoi(e);
+    if (v > 0) return std::min(v, 64);
+  }
+  int np = 1;
+  while (np < N) np *= 2;
+  const int wgs = std::max(1, np * Hkv);
+  return std::max(1, std::min({(2048 + wgs - 1) / wgs, max_ctx / 128, 16}));
 }
 
 }  // namespace
@@ -146,34 +223,51 @@ at::Tensor paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache
   const int N = q.size(0), Hq = q.size(1), D = q.size(2);
   const int bs = k_cache.size(1), Hkv = k_cache.size(2);
   LLMCTL_CHECK(k_cache.size(3) == D && Hq % Hkv == 0, "head shape mismatch");
+  LLMCTL_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= N && context_lens.numel() >= N,
+               "block_tables [N, max_blocks] / context_lens [N]");
   const int G = Hq / Hkv;
   const int max_blocks = block_tables.size(1);
   const c10::DeviceGuard g(q.device());
   auto out = at::empty_like(q);
   if (N == 0) return out;
   const float sl2 = (float)(scale * 1.4426950408889634);
-  dim3 grid(N * Hkv), block(256);
+  const int nsplit = decode_splits(N, Hkv, max_blocks * bs);
+  at::Tensor part_o, part_ml;
+  float *po = nullptr, *pml = nullptr;
+  if (nsplit > 1) {
+    part_o = at::empty({(long)N * Hq * nsplit * D}, q.options().dtype(at::kFloat));
+    part_ml = at::empty({(long)N * Hq * nsplit * 2}, q.options().dtype(at::kFloat));
+    po = part_o.data_ptr<float>();
+    pml = part_ml.data_ptr<float>();
+  }
+  dim3 grid(N * Hkv, nsplit), block(256);
   auto s = stream();
-#define LAUNCH(DD, GG)                                                                                            \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, GG>), grid, block, 0, s, bf_ptr(q), bf_ptr(k_cache), bf_ptr(v_cache), \
-                     block_tables.data_ptr<int>(), context_lens.data_ptr<int>(), bf_mut(out), Hq, Hkv, bs,         \
-                     max_blocks, sl2)
+#define LAUNCH(DD, GG, UU)                                                                                        \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU>), grid, block, 0, s, bf_ptr(q), bf_ptr(k_cache),           \
+                     bf_ptr(v_cache), block_tables.data_ptr<int>(), context_lens.data_ptr<int>(), bf_mut(out), po, \
+                     pml, Hq, Hkv, bs, max_blocks, sl2, nsplit)
   if (D == 128) {
-    if (G == 1) LAUNCH(128, 1);
-    else if (G == 2) LAUNCH(128, 2);
-    else if (G == 4) LAUNCH(128, 4);
-    else if (G == 8) LAUNCH(128, 8);
+    if (G == 1) LAUNCH(128, 1, 4);
+    else if (G == 2) LAUNCH(128, 2, 4);
+    else if (G == 4) LAUNCH(128, 4, 2);
+    else if (G == 8) LAUNCH(128, 8, 2);
     else LLMCTL_CHECK(false, "GQA group must be 1/2/4/8");
   } else if (D == 64) {
-    if (G == 1) LAUNCH(64, 1);
-    else if (G == 2) LAUNCH(64, 2);
-    else if (G == 4) LAUNCH(64, 4);
-    else if (G == 8) LAUNCH(64, 8);
+    if (G == 1) LAUNCH(64, 1, 4);
+    else if (G == 2) LAUNCH(64, 2, 4);
+    else if (G == 4) LAUNCH(64, 4, 2);
+    else if (G == 8) LAUNCH(64, 8, 2);
     else LLMCTL_CHECK(false, "GQA group must be 1/2/4/8");
   } else {
     LLMCTL_CHECK(false, "head_dim must be 64 or 128");
   }
 #undef LAUNCH
+  if (nsplit > 1) {
+    if (D == 128)
+      hipLaunchKernelGGL(paged_combine_kernel<128>, dim3(N * Hq), dim3(128), 0, s, po, pml, bf_mut(out), nsplit);
+    else
+      hipLaunchKernelGGL(paged_combine_kernel<64>, dim3(N * Hq), dim3(64), 0, s, po, pml, bf_mut(out), nsplit);
+  }
   return out;
 }
 

@@ -276,6 +276,26 @@ def test_paged_attention_decode(native_lib, Hq, Hkv, D):
     assert _rel(o, orf) < 2e-2, _rel(o, orf)
 
 
+@pytest.mark.parametrize("splits", ["1", "3", "8", "auto"])
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 32, 128), (32, 8, 128), (16, 2, 64)])
+def test_paged_attention_decode_context_splits(native_lib, monkeypatch, Hq, Hkv, D, splits):
+    """Split-context (flash-decoding) path: partials + combine, including splits that are
+    empty for short sequences, and the automatic choice."""
+    if splits == "auto":
+        monkeypatch.delenv("LLMCTL_DECODE_SPLITS", raising=False)
+    else:
+        monkeypatch.setenv("LLMCTL_DECODE_SPLITS", splits)
+    nb, bs, N, maxb = 400, 16, 3, 128
+    kc = _bf(nb, bs, Hkv, D, seed=61)
+    vc = _bf(nb, bs, Hkv, D, seed=62)
+    lens = torch.tensor([2, 700, 2048], dtype=torch.int32, device=DEV)
+    bt = torch.randperm(nb, device=DEV)[: N * maxb].view(N, maxb).to(torch.int32).contiguous()
+    q = _bf(N, Hq, D, seed=63)
+    o = native_lib.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+    orf = ref.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+    assert _rel(o, orf) < 2e-2, _rel(o, orf)
+
+
 def test_kv_cache_write(native_lib):
     nb, bs, H, D = 8, 16, 4, 128
     kc = torch.zeros(nb, bs, H, D, dtype=torch.bfloat16, device=DEV)
