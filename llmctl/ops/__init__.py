@@ -12,6 +12,7 @@ from .functional import (
     add_layernorm,
     add_rmsnorm,
     cross_entropy,
+    decode_linear,
     flash_attention,
     gelu,
     kv_cache_write,
@@ -26,7 +27,7 @@ from .functional import (
 )
 
 __all__ = [
-    "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy",
+    "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy", "decode_linear",
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
     "rmsnorm", "rope_qkv", "sample", "swiglu", "transpose_",
 ]

@@ -1,0 +1,163 @@
+// Decode-shaped GEMM (gfx950): y[M,N] = x[M,K] · W[N,K]^T (+ bias), M <= 32 tokens.
+//
+// A decode step reads every projection weight once for a handful of tokens: the op is an HBM
+// stream of W (13 GB per GPT-7B step); hipBLASLt's small-M kernels reach 3.6-3.8 TB/s on the
+// wide projections but only 1.8-2.4 TB/s on the 4096-row ones (too few workgroups).  Here:
+//   * MFMA 16x16x32 bf16 with the WEIGHT rows on the MFMA row axis and the tokens on the
+//     column axis: a wave owns 16 weight rows and MT x 16 token columns;
+//   * the K reduction order is free, so the lane group g = lane/16 of MFMA step s reads real
+//     k = kb + 32 g + 8 s + j: every lane streams 64 contiguous bytes of its weight row per
+//     128-deep K block (4 dwordx4 loads), the token operand uses the same permutation;
+//   * a workgroup = 8 waves on one 16-row tile, splitting K 8 ways; GB K blocks per wave are
+//     loaded before the first MFMA (16-32 KB of weight loads in flight per wave, the whole
+//     CU's share of the stream), the 8 partial tiles are reduced through LDS;
+//   * grid = N/16 workgroups (256 for a 4096-row projection: one per CU).
+// Measured (uncached weights, tools/decode_bench.py): 1.5-1.9x hipBLASLt on the narrow
+// projections (o-proj, down-proj), slower than it on the wide ones at M >= 8, which is why
+// ops.decode_linear routes only out_features <= 4096 here.
+// Weights are read with plain loads (they are not reused within a step; the L2/MALL decides).
+#include "attn_common.h"
+
+namespace llmctl {
+namespace {
+
+using attn::bf16x8_t;
+using f32x4_t = __attribute__((ext_vector_type(4))) float;
+
+constexpr int KBLK = 128;  // K per block: 4 MFMA steps of 32
+constexpr int NW = 8;      // waves per workgroup (K split)
+
+__device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8_t ld16(const unsigned short* p) {
+  return *reinterpret_cast<const bf16x8_t*>(p);
+}
+
+template <int NT, int MT, int GB>
+__global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned short* __restrict__ x,
+                                                              const unsigned short* __restrict__ w,
+                                                              const unsigned short* __restrict__ bias,
+                                                              unsigned short* __restrict__ y, int M, int N,
+                                                              int K) {
+  __shared__ f32x4_t red[NW][NT * MT][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16 * NT;
+  const int nblk = K / KBLK;
+  const int b0 = wave * nblk / NW, b1 = (wave + 1) * nblk / NW;
+  const unsigned short* wrow[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) wrow[i] = w + (long)(n0 + 16 * i + r) * K + 32 * g;
+  // token rows beyond M read row 0 (finite values) and are never stored
+  const unsigned short* xrow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = t * 16 + r;
+    xrow[t] = x + (long)(m < M ? m : 0) * K + 32 * g;
+  }
+  f32x4_t acc[NT][MT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[i][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  int b = b0;
+  for (; b + GB <= b1; b += GB) {
+    bf16x8_t a[GB][NT][4], xb[GB][MT][4];
+#pragma unroll
+    for (int u = 0; u < GB; ++u)
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[u][i][s] = ld16(wrow[i] + (long)(b + u) * KBLK + 8 * s);
+#pragma unroll
+    for (int u = 0; u < GB; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xb[u][t][s] = ld16(xrow[t] + (long)(b + u) * KBLK + 8 * s);
+#pragma unroll
+    for (int u = 0; u < GB; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[i][t] = mfma16(a[u][i][s], xb[u][t][s], acc[i][t]);
+  }
+  for (; b < b1; ++b) {
+    bf16x8_t a[NT][4], xb[MT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[i][s] = ld16(wrow[i] + (long)b * KBLK + 8 * s);
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xb[t][s] = ld16(xrow[t] + (long)b * KBLK + 8 * s);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[i][t] = mfma16(a[i][s], xb[t][s], acc[i][t]);
+  }
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) red[wave][i * MT + t][lane] = acc[i][t];
+  __syncthreads();
+  // D layout: lane l holds D[row = 4(l/16) + i][col = l%16] = y[token col][weight row]
+  for (int idx = threadIdx.x; idx < NT * MT * 64; idx += NW * 64) {
+    const int it = idx >> 6, l = idx & 63;
+    const int i = it / MT, t = it % MT;
+    f32x4_t s = red[0][it][l];
+#pragma unroll
+    for (int v = 1; v < NW; ++v) s += red[v][it][l];
+    const int m = t * 16 + (l & 15);
+    if (m >= M) continue;
+    const int n = n0 + 16 * i + 4 * (l >> 4);
+    float o[4] = {s[0], s[1], s[2], s[3]};
+    if (bias != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += bf2f(bias[n + j]);
+    }
+    ushort4 pk;
+    pk.x = f2bf(o[0]);
+    pk.y = f2bf(o[1]);
+    pk.z = f2bf(o[2]);
+    pk.w = f2bf(o[3]);
+    *reinterpret_cast<ushort4*>(y + (long)m * N + n) = pk;
+  }
+}
+
+}  // namespace
+
+at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+  LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(), "skinny_linear: 2-D contiguous");
+  LLMCTL_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "skinny_linear: bf16");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  LLMCTL_CHECK(w.size(1) == K, "skinny_linear: K mismatch");
+  LLMCTL_CHECK(M >= 1 && M <= 32 && N % 16 == 0 && K % KBLK == 0, "skinny_linear: needs M<=32, N%16==0, K%128==0");
+  const unsigned short* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    LLMCTL_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N, "bias [N] bf16");
+    bp = bf_ptr(*bias);
+  }
+  const c10::DeviceGuard guard(x.device());
+  auto y = at::empty({M, N}, x.options());
+  // (a two-row-tile variant for wide projections measured slower: 32.8 vs 23.9 us on the
+  // GPT-7B QKV at M=1 — more rows per wave cost more than the shared token fragment saves)
+  dim3 grid(N / 16), block(NW * 64);
+  auto st = stream();
+  if (M <= 16)
+    hipLaunchKernelGGL((skinny_gemm_kernel<1, 1, 4>), grid, block, 0, st, bf_ptr(x), bf_ptr(w), bp, bf_mut(y), M, N, K);
+  else
+    hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 2>), grid, block, 0, st, bf_ptr(x), bf_ptr(w), bp, bf_mut(y), M, N, K);
+  return y;
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("skinny_linear", &skinny_linear); }
+
+}  // namespace llmctl

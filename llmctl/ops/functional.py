@@ -12,6 +12,7 @@ copies are needed between kernels:
 
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -323,6 +324,22 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scal
     return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale)
 
 
+def decode_linear(x, w, b=None):
+    """``x @ w^T (+ b)`` for decode-shaped inputs: the weight-streaming MFMA kernel
+    (``csrc/skinny_gemm.hip``) for the NARROW projections (out features <= 4096: o-proj,
+    down-proj, TP shards) where hipBLASLt's small-M kernels launch too few workgroups
+    (GPT-7B o-proj at M=16: 9.6 vs 18.6 us, ``profiles/decode_bench_r1.jsonl``); wide ones
+    (QKV, up, LM head) and anything over 16 tokens x 11008 stay on hipBLASLt via ``F.linear``.
+    ``LLMCTL_SKINNY_GEMM=0`` / ``=all`` force the library / kernel path (A/B)."""
+    mode = os.environ.get("LLMCTL_SKINNY_GEMM", "1")
+    if (mode != "0" and use_native(x) and x.dim() == 2 and x.shape[0] <= 32 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.shape[0] % 16 == 0 and x.shape[1] % 128 == 0
+            and x.is_contiguous() and w.is_contiguous() and (b is None or b.is_contiguous())
+            and (mode == "all" or (w.shape[0] <= 4096 and x.shape[0] * x.shape[1] <= 16 * 11008))):
+        return native().skinny_linear(x, w, b)
+    return torch.nn.functional.linear(x, w, b)
+
+
 def sample(logits, temperature, top_k, top_p, uniform):
     if use_native(logits):
         return native().sample(logits, temperature, top_k, top_p, uniform)
@@ -333,5 +350,5 @@ __all__ = [
     "transpose_",
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample",
+    "sample", "decode_linear",
 ]

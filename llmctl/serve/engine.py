@@ -132,7 +132,7 @@ class InferenceEngine:
         return ops.add_layernorm(x, res, w, b, eps) if b is not None else ops.add_rmsnorm(x, res, w, eps)
 
     def _qkv(self, layer, xn, positions, seq_len):
-        qkv = F.linear(xn, layer.wqkv, layer.bqkv)
+        qkv = ops.decode_linear(xn, layer.wqkv, layer.bqkv)
         if self.rope is not None:
             return ops.rope_qkv(qkv, self.rope[0], self.rope[1], layer.nq, layer.nkv, seq_len, positions)
         T = qkv.shape[0]
@@ -144,9 +144,9 @@ class InferenceEngine:
         if layer.moe is not None:  # routed experts (host-side split sizes: eager, no graphs)
             return layer.moe(xn)
         if self.cfg.gated_mlp:
-            out = F.linear(ops.swiglu(F.linear(xn, layer.w_up, layer.b_up)), layer.w_down)
+            out = ops.decode_linear(ops.swiglu(ops.decode_linear(xn, layer.w_up, layer.b_up)), layer.w_down)
         else:
-            out = F.linear(ops.gelu(F.linear(xn, layer.w_up, layer.b_up)), layer.w_down)
+            out = ops.decode_linear(ops.gelu(ops.decode_linear(xn, layer.w_up, layer.b_up)), layer.w_down)
         out = self._reduce(out)  # row-parallel down projection
         if layer.b_down is not None:
             out = out + layer.b_down
@@ -159,7 +159,7 @@ class InferenceEngine:
             xn, _ = ops.add_layernorm(x, res, m.final_norm_w, m.final_norm_b, eps)
         else:
             xn, _ = ops.add_rmsnorm(x, res, m.final_norm_w, eps)
-        return self._gather_vocab(F.linear(xn, m.head_weight()))
+        return self._gather_vocab(ops.decode_linear(xn, m.head_weight()))
 
     # ------------------------------------------------------------------ prefill
     def prefill_plan(self, seqs: List[Sequence]) -> Dict:
@@ -196,7 +196,7 @@ class InferenceEngine:
             ops.kv_cache_write(k, v, kc[li], vc[li], slots)
             o = ops.flash_attention(q.view(B, S, layer.nq, layer.D), k.view(B, S, layer.nkv, layer.D),
                                     v.view(B, S, layer.nkv, layer.D), causal=True)
-            a = self._reduce(F.linear(o.view(B * S, -1), layer.wo))
+            a = self._reduce(ops.decode_linear(o.view(B * S, -1), layer.wo))
             if layer.bo is not None:
                 a = a + layer.bo
             xn, res = self._norm(layer, a, res, "mlp")
@@ -216,7 +216,7 @@ class InferenceEngine:
             q, k, v = self._qkv(layer, xn, positions, self.max_model_len)
             ops.kv_cache_write(k, v, kc[li], vc[li], slots)
             o = ops.paged_attention_decode(q, kc[li], vc[li], block_tables, ctx_lens)
-            a = self._reduce(F.linear(o.view(o.shape[0], -1), layer.wo))
+            a = self._reduce(ops.decode_linear(o.view(o.shape[0], -1), layer.wo))
             if layer.bo is not None:
                 a = a + layer.bo
             xn, res = self._norm(layer, a, res, "mlp")

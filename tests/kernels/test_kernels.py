@@ -451,3 +451,16 @@ def test_side_stream_optimizer_matches_inline(native_lib, monkeypatch):
     # bf16 ulps of the 1e-3-lr update as well)
     assert diff <= max(4 * noise, 2e-3), (diff, noise)
     assert (a.float() - b.float()).abs().mean().item() < 1e-5
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 32])
+@pytest.mark.parametrize("N,K,bias", [(256, 512, False), (4096, 11008, False), (1536, 4096, True)])
+def test_skinny_linear_decode_gemm(native_lib, M, N, K, bias):
+    """Decode-shaped weight-streaming GEMM vs the fp32 product (K split over 8 waves, LDS reduce)."""
+    x = _bf(M, K, seed=71)
+    w = _bf(N, K, scale=0.05, seed=72)
+    b = _bf(N, seed=73) if bias else None
+    y = native_lib.skinny_linear(x, w, b)
+    ref_y = x.float() @ w.float().t() + (b.float() if bias else 0.0)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert _rel(y, ref_y) < 1e-2, _rel(y, ref_y)

@@ -60,6 +60,34 @@ def main():
             print(json.dumps(row), flush=True)
         del kc, vc
     os.environ.pop("LLMCTL_DECODE_SPLITS", None)
+    # decode-shaped projection GEMMs (GPT-7B): weight-streaming MFMA kernel vs hipBLASLt
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "up": (22016, 4096), "down": (4096, 11008),
+              "lm_head": (32000, 4096)}
+    for M in (1, 8, 16, 32):
+        for name, (N, K) in shapes.items():
+            x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+            # cycle through > 256 MB of weight copies so the MALL does not serve repeats
+            nw = max(2, -(-768 * 2**20 // (N * K * 2)))
+            ws = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) for _ in range(nw)]
+            it = iter(range(1 << 30))
+            row = {"gemm": name, "M": M, "N": N, "K": K}
+            for impl, fn in (("skinny", lambda: nat.skinny_linear(x, ws[next(it) % nw], None)),
+                             ("hipblaslt", lambda: torch.nn.functional.linear(x, ws[next(it) % nw]))):
+                for _ in range(5):
+                    fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(50):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) / 50 * 1e3
+                row[f"{impl}_us"] = round(us, 1)
+                row[f"{impl}_tbps"] = round(N * K * 2 / (us * 1e-6) / 1e12, 2)
+            rows.append(row)
+            print(json.dumps(row), flush=True)
+            del ws
     if a.json_out:
         with open(a.json_out, "w") as f:
             for r in rows:
