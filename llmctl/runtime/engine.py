@@ -151,6 +151,10 @@ class TrainingEngine:
                 kw["device_id"] = self.device
                 # surface collective timeouts/errors as exceptions (torchrun then restarts)
                 os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+                # RCCL streams at high priority: the bucketed reduce-scatters / all-gathers
+                # overlapped with backward / forward get their workgroups dispatched ahead of
+                # the GEMM grids, so the last buckets are not left exposed after backward
+                os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
             dist.init_process_group(backend=backend, **kw)
         if c.context_parallel > 1 and c.pipeline_parallel > 1:
             raise NotImplementedError("context_parallel with pipeline_parallel is not supported")
