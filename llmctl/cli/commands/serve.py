@@ -23,7 +23,7 @@ def start(
     artifact: str = typer.Option(..., help="Checkpoint directory or model template name"),
     port: int = typer.Option(8080, help="Server port"),
     host: str = typer.Option("0.0.0.0", help="Server host"),
-    scheduler: str = typer.Option("dynamic", help="Scheduler (dynamic = continuous batching, static)"),
+    scheduler: str = typer.Option("dynamic", help="Scheduler (dynamic = continuous batching, prefill_first = TTFT-oriented continuous batching, static)"),
     max_batch_size: int = typer.Option(8, help="Maximum sequences per decode step"),
     max_batch_tokens: int = typer.Option(8192, help="Maximum tokens per engine step"),
     max_concurrent: int = typer.Option(128, help="Maximum concurrent requests"),

@@ -12,6 +12,10 @@ Here (``scheduler="dynamic"``), every engine step:
    (``max_batch_tokens`` minus the decode tokens), the batch-size cap and the free KV
    blocks (prompt + one block headroom) allow.
 ``scheduler="static"`` admits a new group only when the running group has fully finished.
+``scheduler="prefill_first"`` (TTFT-oriented): a step that can admit a waiting request runs
+only prefills — running sequences pause for that step — so a burst of arrivals gets its first
+tokens back-to-back; with a one-prompt token budget the i-th request's TTFT is about i prefill
+times instead of i x (prefill + decode step).
 """
 
 from __future__ import annotations
@@ -101,11 +105,18 @@ class ContinuousBatchScheduler:
         return len(self.running)
 
     # ------------------------------------------------------------------ step
+    def _can_admit(self) -> bool:
+        if not self.waiting or len(self.running) >= self.max_batch_size:
+            return False
+        return self.kv.can_allocate(self.waiting[0].num_tokens + self.kv_block_size())
+
     def schedule(self) -> SchedulerOutput:
         preempted: List[Sequence] = []
         decode: List[Sequence] = []
-        # 1) decodes for running sequences (each needs one more KV slot)
-        for seq in list(self.running):
+        # 1) decodes for running sequences (each needs one more KV slot); prefill_first skips
+        #    them while a waiting request can be admitted
+        running = [] if self.policy == "prefill_first" and self._can_admit() else list(self.running)
+        for seq in running:
             if len(decode) >= self.max_batch_size:
                 break
             if seq.status != "running":  # preempted earlier in this loop

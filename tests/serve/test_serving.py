@@ -74,6 +74,30 @@ def test_scheduler_token_budget():
     assert len(out.decode) == 1 and [len(q.prompt_ids) for q in out.prefill] == [20, 5]
 
 
+def test_scheduler_prefill_first_policy():
+    kv = PyKVManager(100, 16)
+    s = ContinuousBatchScheduler(kv, max_batch_size=8, max_batch_tokens=40, block_size=16, policy="prefill_first")
+    for n in (30, 20, 5):
+        s.add(Sequence(prompt_ids=[1] * n, params=SamplingParams()))
+    out = s.schedule()
+    assert [len(q.prompt_ids) for q in out.prefill] == [30] and not out.decode
+    out = s.schedule()  # admissions pending: the running sequence pauses
+    assert not out.decode and [len(q.prompt_ids) for q in out.prefill] == [20, 5]
+    out = s.schedule()  # queue drained: everyone decodes
+    assert len(out.decode) == 3 and not out.prefill
+
+
+def test_engine_prefill_first_matches_dynamic():
+    p = SamplingParams(max_tokens=6, temperature=0.0)
+    prompts = [[1, 2, 3], [4, 5, 6, 7, 8], [9] * 20]
+    outs = []
+    for pol in ("dynamic", "prefill_first"):
+        e = InferenceEngine("tiny", device="cpu", max_batch_size=2, num_kv_blocks=64, block_size=8,
+                            max_model_len=128, scheduler=pol)
+        outs.append([s.output_ids for s in e.generate(prompts, p)])
+    assert outs[0] == outs[1]
+
+
 @pytest.fixture(scope="module")
 def client():
     from fastapi.testclient import TestClient
