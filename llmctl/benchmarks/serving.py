@@ -31,9 +31,12 @@ def run_serving_benchmark(model: str = "gpt-7b", prompt_length: int = 2048, gen_
     V = eng.cfg.vocab_size
     rng = random.Random(seed)
     params = SamplingParams(max_tokens=gen_length, temperature=0.0, ignore_eos=True)
-    if warmup:  # compile graphs / warm allocator with a short request of each batch size
+    if warmup:  # capture decode graphs, warm the allocator and the GEMM / attention paths of the
+        # full-length prefill batches the timed run will form (first-use costs stay out of TTFT)
         eng.generate([[1] * 16 for _ in range(min(max_batch_size, num_requests))],
                      SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+        eng.generate([[2] * prompt_length for _ in range(min(max_batch_size, num_requests))],
+                     SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
     prompts = [[rng.randrange(V) for _ in range(prompt_length)] for _ in range(num_requests)]
     arrivals = [0.0] * num_requests
     if qps:
