@@ -1,0 +1,18 @@
+#!/bin/bash
+# gpurun: smoke, GPU tests, 1-GPU bench (driver default), rocprofv3 kernel stats of the bench,
+# Llama-3-70B layer-slice benchmark.
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONPATH=$PWD
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -30 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+timeout -k 10 600 python -u tools/slice_bench.py --model llama-70b --layers 2 6 --micro-batch 2 > gpurun_out/slice70b.jsonl 2> gpurun_out/slice70b.err || { tail -20 gpurun_out/slice70b.err; exit 1; }
+cat gpurun_out/slice70b.jsonl
+R=$PWD
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 > $R/gpurun_out/prof_bench.log 2>&1 || { tail -20 $R/gpurun_out/prof_bench.log; exit 1; }
+echo prof ok
