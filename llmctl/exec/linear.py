@@ -36,7 +36,7 @@ def _gemm_ex_ok(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
         return False
     from llmctl.ops._lib import use_native
 
-    if not use_native(g):
+    if not use_native(g) or os.environ.get("LLMCTL_WGRAD_KERNEL", "1") == "0":  # =0: hipBLASLt (A/B)
         return False
     M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
     if M % 256 or N % 256 or K % 32 or K == 0:
