@@ -47,12 +47,15 @@ def e2e(
     model: str = typer.Option("gpt-7b", help="Checkpoint dir or template"),
     max_batch_size: int = typer.Option(16, help="Max decode batch"),
     device: str = typer.Option("auto", help="auto | cuda | cpu"),
+    scheduler: str = typer.Option("dynamic", help="dynamic | prefill_first | static"),
+    max_batch_tokens: Optional[int] = typer.Option(None, help="Prefill token budget per step"),
 ) -> None:
     """End-to-end serving benchmark (TTFT p50/p99, TPOT, tokens/s)."""
     from llmctl.benchmarks.serving import run_serving_benchmark
 
     res = run_serving_benchmark(model=model, prompt_length=prompt_length, gen_length=gen_length, qps=qps,
-                                num_requests=num_requests, max_batch_size=max_batch_size, device=device)
+                                num_requests=num_requests, max_batch_size=max_batch_size, device=device,
+                                scheduler=scheduler, max_batch_tokens=max_batch_tokens)
     console.print_json(json.dumps(res))
 
 
