@@ -21,6 +21,7 @@ from .functional import (
     paged_attention_decode,
     rmsnorm,
     rope_qkv,
+    rope_qkv_cache,
     sample,
     swiglu,
     transpose_,
@@ -29,5 +30,5 @@ from .functional import (
 __all__ = [
     "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy", "decode_linear",
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
-    "rmsnorm", "rope_qkv", "sample", "swiglu", "transpose_",
+    "rmsnorm", "rope_qkv", "rope_qkv_cache", "sample", "swiglu", "transpose_",
 ]

@@ -16,7 +16,9 @@ __global__ __launch_bounds__(256) void rope_fwd_kernel(const unsigned short* __r
                                                         const PosT* __restrict__ pos, unsigned short* __restrict__ q,
                                                         unsigned short* __restrict__ k,
                                                         unsigned short* __restrict__ v, int nq, int nkv, int D,
-                                                        int S, long total) {
+                                                        int S, long total, unsigned short* __restrict__ kc = nullptr,
+                                                        unsigned short* __restrict__ vc = nullptr,
+                                                        const int64_t* __restrict__ slots = nullptr) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   const int CH = D >> 4;
@@ -56,6 +58,15 @@ __global__ __launch_bounds__(256) void rope_fwd_kernel(const unsigned short* __r
   }
   store8(dst + c * 8, o1);
   store8(dst + half + c * 8, o2);
+  if (slots != nullptr && h >= nq) {  // serving: K/V rows also go straight into the paged cache
+    const long sl = slots[t];
+    if (sl >= 0) {
+      const bool isk = h < nq + nkv;
+      unsigned short* cdst = (isk ? kc : vc) + (sl * nkv + (isk ? h - nq : h - nq - nkv)) * (long)D;
+      store8(cdst + c * 8, o1);
+      store8(cdst + half + c * 8, o2);
+    }
+  }
 }
 
 template <typename PosT>
@@ -197,9 +208,9 @@ void check_rope_tables(const at::Tensor& c, const at::Tensor& s, int D) {
 
 }  // namespace
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_qkv_fwd(const at::Tensor& qkv, const at::Tensor& cosT,
-                                                             const at::Tensor& sinT, int64_t nq, int64_t nkv,
-                                                             int64_t seq_len, const c10::optional<at::Tensor>& pos) {
+static std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_qkv_impl(
+    const at::Tensor& qkv, const at::Tensor& cosT, const at::Tensor& sinT, int64_t nq, int64_t nkv, int64_t seq_len,
+    const c10::optional<at::Tensor>& pos, at::Tensor* kc, at::Tensor* vc, const at::Tensor* slots) {
   LLMCTL_CHECK(qkv.is_cuda() && qkv.dim() == 2 && qkv.is_contiguous() && qkv.scalar_type() == at::kBFloat16,
                "qkv must be a contiguous 2-D bf16 GPU tensor");
   const long T = qkv.size(0);
@@ -220,16 +231,43 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_qkv_fwd(const at::Tensor& qk
   auto v = at::empty({T, nkv, D}, qkv.options());
   const long total = T * NH * (D / 16);
   if (total == 0) return {q, k, v};
+  unsigned short *kcp = nullptr, *vcp = nullptr;
+  const int64_t* sp = nullptr;
+  if (slots != nullptr) {
+    LLMCTL_CHECK(kc->is_contiguous() && vc->is_contiguous() && kc->scalar_type() == at::kBFloat16 &&
+                     vc->sizes() == kc->sizes() && kc->dim() == 4 && kc->size(2) == nkv && kc->size(3) == D,
+                 "k/v cache: contiguous bf16 [blocks, block_size, Hkv, D]");
+    LLMCTL_CHECK(slots->scalar_type() == at::kLong && slots->numel() == T && slots->is_contiguous(), "slots: int64 [T]");
+    kcp = bf_mut(*kc);
+    vcp = bf_mut(*vc);
+    sp = slots->data_ptr<int64_t>();
+  }
   if (has_pos && pos->scalar_type() == at::kLong)
     hipLaunchKernelGGL(rope_fwd_kernel<int64_t>, dim3(blocks_for(total)), dim3(256), 0, stream(), bf_ptr(qkv),
                        cosT.data_ptr<float>(), sinT.data_ptr<float>(), pos->data_ptr<int64_t>(), bf_mut(q), bf_mut(k),
-                       bf_mut(v), (int)nq, (int)nkv, D, (int)seq_len, total);
+                       bf_mut(v), (int)nq, (int)nkv, D, (int)seq_len, total, kcp, vcp, sp);
   else
     hipLaunchKernelGGL(rope_fwd_kernel<int32_t>, dim3(blocks_for(total)), dim3(256), 0, stream(), bf_ptr(qkv),
                        cosT.data_ptr<float>(), sinT.data_ptr<float>(),
                        has_pos ? pos->data_ptr<int32_t>() : nullptr, bf_mut(q), bf_mut(k), bf_mut(v), (int)nq,
-                       (int)nkv, D, (int)seq_len, total);
+                       (int)nkv, D, (int)seq_len, total, kcp, vcp, sp);
   return {q, k, v};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_qkv_fwd(const at::Tensor& qkv, const at::Tensor& cosT,
+                                                             const at::Tensor& sinT, int64_t nq, int64_t nkv,
+                                                             int64_t seq_len, const c10::optional<at::Tensor>& pos) {
+  return rope_qkv_impl(qkv, cosT, sinT, nq, nkv, seq_len, pos, nullptr, nullptr, nullptr);
+}
+
+// Serving: RoPE + split + paged-KV write in one pass (the separate kv_cache_write re-read K/V).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_qkv_cache_fwd(const at::Tensor& qkv, const at::Tensor& cosT,
+                                                                   const at::Tensor& sinT, int64_t nq, int64_t nkv,
+                                                                   int64_t seq_len,
+                                                                   const c10::optional<at::Tensor>& pos,
+                                                                   at::Tensor& k_cache, at::Tensor& v_cache,
+                                                                   const at::Tensor& slots) {
+  return rope_qkv_impl(qkv, cosT, sinT, nq, nkv, seq_len, pos, &k_cache, &v_cache, &slots);
 }
 
 at::Tensor rope_qkv_bwd(const at::Tensor& dq, const at::Tensor& dk, const at::Tensor& dv, const at::Tensor& cosT,
@@ -309,6 +347,7 @@ at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& x) {
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("rope_qkv_fwd", &rope_qkv_fwd);
+  m.impl("rope_qkv_cache_fwd", &rope_qkv_cache_fwd);
   m.impl("rope_qkv_bwd", &rope_qkv_bwd);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);

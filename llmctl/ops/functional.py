@@ -172,6 +172,16 @@ def rope_qkv(qkv, cos, sin, nq: int, nkv: int, seq_len: int, positions: Optional
     return _RopeQKV.apply(qkv, cos, sin, nq, nkv, seq_len, positions)
 
 
+def rope_qkv_cache(qkv, cos, sin, nq: int, nkv: int, seq_len: int, positions, k_cache, v_cache, slots):
+    """Inference: ``rope_qkv`` that also writes the rotated K and V rows into the paged cache at
+    ``slots`` (int64 [T], -1 = skip) in the same pass."""
+    if use_native(qkv):
+        return native().rope_qkv_cache_fwd(qkv, cos, sin, nq, nkv, seq_len, positions, k_cache, v_cache, slots)
+    q, k, v = ref.rope_qkv_fwd(qkv, cos, sin, nq, nkv, seq_len, positions)
+    ref.kv_cache_write(k, v, k_cache, v_cache, slots)
+    return q, k, v
+
+
 # =============================================================================== attention
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
@@ -350,5 +360,5 @@ __all__ = [
     "transpose_",
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample", "decode_linear",
+    "sample", "decode_linear", "rope_qkv_cache",
 ]

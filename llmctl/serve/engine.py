@@ -131,14 +131,19 @@ class InferenceEngine:
             return (ops.layernorm(x, w, b, eps) if b is not None else ops.rmsnorm(x, w, eps)), x
         return ops.add_layernorm(x, res, w, b, eps) if b is not None else ops.add_rmsnorm(x, res, w, eps)
 
-    def _qkv(self, layer, xn, positions, seq_len):
+    def _qkv(self, layer, xn, positions, seq_len, kc, vc, slots):
+        """QKV projection, RoPE and the paged-cache write of this step's K/V rows (one fused
+        pass with RoPE)."""
         qkv = ops.decode_linear(xn, layer.wqkv, layer.bqkv)
         if self.rope is not None:
-            return ops.rope_qkv(qkv, self.rope[0], self.rope[1], layer.nq, layer.nkv, seq_len, positions)
+            return ops.rope_qkv_cache(qkv, self.rope[0], self.rope[1], layer.nq, layer.nkv, seq_len, positions,
+                                      kc, vc, slots)
         T = qkv.shape[0]
         x = qkv.view(T, layer.nq + 2 * layer.nkv, layer.D)
-        return (x[:, :layer.nq].contiguous(), x[:, layer.nq:layer.nq + layer.nkv].contiguous(),
-                x[:, layer.nq + layer.nkv:].contiguous())
+        q, k, v = (x[:, :layer.nq].contiguous(), x[:, layer.nq:layer.nq + layer.nkv].contiguous(),
+                   x[:, layer.nq + layer.nkv:].contiguous())
+        ops.kv_cache_write(k, v, kc, vc, slots)
+        return q, k, v
 
     def _mlp(self, layer, xn):
         if layer.moe is not None:  # routed experts (host-side split sizes: eager, no graphs)
@@ -192,8 +197,7 @@ class InferenceEngine:
         kc, vc = self.kv_cache.k, self.kv_cache.v
         for li, layer in enumerate(self.model.layers):
             xn, res = self._norm(layer, x, res, "attn")
-            q, k, v = self._qkv(layer, xn, None, S)
-            ops.kv_cache_write(k, v, kc[li], vc[li], slots)
+            q, k, v = self._qkv(layer, xn, None, S, kc[li], vc[li], slots)
             o = ops.flash_attention(q.view(B, S, layer.nq, layer.D), k.view(B, S, layer.nkv, layer.D),
                                     v.view(B, S, layer.nkv, layer.D), causal=True)
             a = self._reduce(ops.decode_linear(o.view(B * S, -1), layer.wo))
@@ -213,8 +217,7 @@ class InferenceEngine:
         kc, vc = self.kv_cache.k, self.kv_cache.v
         for li, layer in enumerate(self.model.layers):
             xn, res = self._norm(layer, x, res, "attn")
-            q, k, v = self._qkv(layer, xn, positions, self.max_model_len)
-            ops.kv_cache_write(k, v, kc[li], vc[li], slots)
+            q, k, v = self._qkv(layer, xn, positions, self.max_model_len, kc[li], vc[li], slots)
             o = ops.paged_attention_decode(q, kc[li], vc[li], block_tables, ctx_lens)
             a = self._reduce(ops.decode_linear(o.view(o.shape[0], -1), layer.wo))
             if layer.bo is not None:

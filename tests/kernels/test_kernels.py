@@ -464,3 +464,23 @@ def test_skinny_linear_decode_gemm(native_lib, M, N, K, bias):
     ref_y = x.float() @ w.float().t() + (b.float() if bias else 0.0)
     assert y.shape == (M, N) and y.dtype == torch.bfloat16
     assert _rel(y, ref_y) < 1e-2, _rel(y, ref_y)
+
+
+@pytest.mark.parametrize("with_pos", [False, True])
+def test_rope_qkv_cache_fused_write(native_lib, with_pos):
+    """RoPE + paged-KV write in one pass == rope_qkv_fwd followed by kv_cache_write."""
+    nq, nkv, D, S, bs, nb = 8, 2, 128, 24, 16, 16
+    T = 2 * S
+    qkv = _bf(T, (nq + 2 * nkv) * D, seed=81)
+    cos, sin = ref.rope_tables(S + 8, D, base=10000.0, device=DEV)
+    pos = torch.randint(0, S + 8, (T,), device=DEV, dtype=torch.int32) if with_pos else None
+    slots = torch.randperm(nb * bs, device=DEV)[:T]
+    slots[3] = -1
+    kc = torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    q, k, v = native_lib.rope_qkv_cache_fwd(qkv, cos, sin, nq, nkv, S, pos, kc, vc, slots)
+    q2, k2, v2 = native_lib.rope_qkv_fwd(qkv, cos, sin, nq, nkv, S, pos)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(kc)
+    native_lib.kv_cache_write(k2, v2, kc2, vc2, slots)
+    assert torch.equal(q, q2) and torch.equal(k, k2) and torch.equal(v, v2)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
