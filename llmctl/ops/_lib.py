@@ -16,7 +16,7 @@ from pathlib import Path
 
 import torch
 
-LIB_PATH = Path(__file__).resolve().parent / "_llmctl_hip.so"
+LIB_PATH = Path(os.environ.get("LLMCTL_HIP_LIB") or Path(__file__).resolve().parent / "_llmctl_hip.so")  # override: A/B of two builds
 _loaded = False
 _error: str | None = None
 

@@ -32,6 +32,7 @@ namespace {
 
 constexpr int QB = 128;  // query rows per workgroup
 constexpr int KB = 64;   // keys per tile
+constexpr float kRescaleTh = 8.f;  // log2-domain headroom of the deferred softmax rescale
 
 struct FwdArgs {
   const unsigned short* q;
@@ -178,9 +179,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
         mx = fmaxf(mx, x);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float m_new = fmaxf(m_i, mx);
+    // deferred rescale: keep the running max while no row's max grew by more than kRescaleTh
+    // (p = 2^(s - m) then stays <= 2^kRescaleTh, exact in fp32 and well inside bf16 range); the
+    // decision is wave-uniform, and O, l and the LSE all use the same (possibly stale) m, so the
+    // result is the exact softmax.  Skips the 16*NDB O multiplies and the alpha exp per tile.
+    const bool grow = __builtin_amdgcn_ballot_w64(mx > m_i + kRescaleTh) != 0;
+    const float m_new = grow ? fmaxf(m_i, mx) : m_i;
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = fast_exp2(m_i - m_use);
     float rs = 0.f;
     bf16x8_t pb[2][2];
 #pragma unroll
@@ -195,12 +200,16 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
       pb[kb][1] = to_bf16x8(p + 8);
     }
     rs += __shfl_xor(rs, 32);
-    l_i = l_i * alpha + rs;
+    if (grow) {
+      const float alpha = fast_exp2(m_i - m_use);
+      l_i *= alpha;
+#pragma unroll
+      for (int d = 0; d < NDB; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+    }
+    l_i += rs;
     m_i = m_new;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
     // ---- O^T += V^T P^T
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
