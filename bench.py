@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--activation-checkpoint", default="none")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--backend", default="auto", help="auto (RCCL on GPU, gloo on CPU) | nccl | gloo")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -72,7 +73,8 @@ def main():
         tensor_parallel=args.tp, pipeline_parallel=args.pp, zero_stage=zero,
         sequence_parallel=args.sequence_parallel, activation_checkpoint=args.activation_checkpoint,
         context_parallel=args.cp, context_parallel_mode=args.cp_mode, expert_parallel=args.ep,
-        bucket_mb=args.bucket_mb, device=args.device, seed=1234, log_level="warning")
+        bucket_mb=args.bucket_mb, device=args.device, distributed_backend=args.backend, seed=1234,
+        log_level="warning")
     eng = TrainingEngine(cfg, mc)
     dev = eng.device
     data = SyntheticTokens(mc.vocab_size, args.seq_len, args.micro_batch, seed=1234, rank=eng.pg.dp_rank, device=dev)

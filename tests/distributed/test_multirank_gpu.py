@@ -1,0 +1,42 @@
+"""Multi-rank training on the GPU code paths (device tensors, HIP kernels, side streams, ZeRO
+gather hooks) on a one-GPU box: two ranks share cuda:0 and talk over gloo, because RCCL refuses
+two ranks on one device.  The 8-GPU RCCL runs are the driver's (``SCALE_rNN.json``)."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[2]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(*extra):
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"), "--gpus", "2", "--model", "gpt-125m",
+           "--seq-len", "256", "--micro-batch", "2", "--steps", "2", "--warmup", "1", "--device", "cuda:0",
+           "--backend", "gloo", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_two_rank_zero1_matches_zero0_on_gpu():
+    z0 = _bench("--zero", "0")
+    z1 = _bench("--zero", "1")
+    assert z0["config"]["parallelism"] == "dp2" and z1["config"]["parallelism"] == "dp2-zero1"
+    assert z0["n_gpus"] == 2 and z0["config"]["global_batch"] == 4
+    assert abs(z0["final_loss"] - z1["final_loss"]) < 2e-2, (z0["final_loss"], z1["final_loss"])
