@@ -108,6 +108,7 @@ class ProcessGroups:
     dpcp_group: Optional[object] = None  # gradient-reduction group (== dp_group when cp == 1)
     ep_group: Optional[object] = None  # MoE all-to-all group
     edp_group: Optional[object] = None  # expert-gradient reduction group
+    embed_group: Optional[object] = None  # {first, last} pipeline stage: tied-embedding grads
     pp_ranks: List[int] = field(default_factory=list)
 
     @property
@@ -169,4 +170,8 @@ def build_process_groups(tp: int = 1, pp: int = 1, dp: Optional[int] = None, cp:
     for ranks in layout.pp_groups():
         if rank in ranks:
             pg.pp_ranks = ranks
+    if pp > 1:
+        # Megatron-style embedding group: the first and last stage of each pipeline hold the
+        # two copies of a tied embedding / LM-head matrix and sum their gradients here
+        pg.embed_group = make([[r[0], r[-1]] for r in layout.pp_groups()])
     return pg

@@ -34,9 +34,51 @@ class PipelineSchedule:
         self.num_microbatches = max(int(num_microbatches), 1)
         self.prev = self.ranks[self.s - 1] if self.s > 0 else None
         self.next = self.ranks[self.s + 1] if self.s < self.P - 1 else None
-        if engine.model_config.tie_word_embeddings and self.P > 1:
-            raise NotImplementedError("tied word embeddings across pipeline stages are not supported; untie them")
+        # tied word embeddings: stage 0 owns ``embed``, stage P-1 an ``lm_head`` copy.  The copy
+        # starts equal (broadcast below) and stays equal because both receive the SUM of the
+        # two stages' gradients (``sync_tied_grads``) before identical optimizer updates.
+        self.tied = bool(engine.model_config.tie_word_embeddings and self.P > 1)
+        if self.tied:
+            self._broadcast_tied()
+            if self.is_last:
+                engine.optimizer.norm_exclude.append(self._tied_grad)
         self.last_loss: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------------ tied embeddings
+    def _tied_param(self):
+        m = self.e.model
+        return m.embed if self.is_first else (m.lm_head if self.is_last else None)
+
+    @torch.no_grad()
+    def _broadcast_tied(self):
+        p = self._tied_param()
+        if p is not None:
+            dist.broadcast(p.data, src=self.ranks[0], group=self.e.pg.embed_group)
+
+    def _tied_grad(self) -> Optional[torch.Tensor]:
+        """The DP-reduced gradient of the tied copy this rank holds: the whole ``p.grad`` under
+        ZeRO-0, else this DP rank's shard of its solo bucket (the same element range on both
+        stages: the engine gives each copy an equal-sized bucket of its own)."""
+        p = self._tied_param()
+        if p is None:
+            return None
+        opt = self.e.optimizer
+        if opt.zero_stage == 0:
+            return p.grad
+        b = self.e.flat.param_bucket[id(p)]
+        assert b.params == [p], "tied embedding copy must own its bucket"
+        off, c = opt.shard_offsets[b.index]
+        return opt.grad_shard[off:off + c]
+
+    @torch.no_grad()
+    def sync_tied_grads(self):
+        """Sum the tied matrix's gradient over the first and last stage (after DP reduction:
+        both are linear, so the order does not matter)."""
+        if not self.tied:
+            return
+        g = self._tied_grad()
+        if g is not None:
+            dist.all_reduce(g, group=self.e.pg.embed_group)
 
     # ------------------------------------------------------------------ helpers
     @property

@@ -204,7 +204,8 @@ class TrainingEngine:
             named = list(self.model.named_parameters())
             if pg.layout.ep > 1:  # expert shards: their own flat buffer, reduced over expert-DP
                 named = [(n, p) for n, p in named if not getattr(p, "expert", False)]
-            self.flat = FlatParameters(named, bucket_numel=bucket_numel, align=align)
+            solo = ("embed", "lm_head") if (pp > 1 and mc.tie_word_embeddings) else ()
+            self.flat = FlatParameters(named, bucket_numel=bucket_numel, align=align, solo=solo)
             # GEMM-written weight gradients (no AccumulateGrad pass); tied embeddings excluded
             from llmctl.exec.linear import GradSink
 
@@ -358,6 +359,8 @@ class TrainingEngine:
             self.sync.finish()
         if self.esync is not None:
             self.esync.finish()
+        if self.pipeline is not None:
+            self.pipeline.sync_tied_grads()
         self.global_step += 1
         lr = self.scheduler(self.global_step)
         if self.eopt is not None:
@@ -476,6 +479,8 @@ class TrainingEngine:
         with torch.no_grad():
             for n, p in named:
                 g = self._expert_global(_global_name(n, self.pc.layer_start))
+                if g == "lm_head" and g not in full and self.model_config.tie_word_embeddings:
+                    g = "embed"  # the last pipeline stage's copy of a tied matrix
                 t = shard_tp(g, full[g], self.pg.layout.tp, self.pg.tp_rank, self.model_config)
                 p.copy_(t.to(p.dtype))
         if self.zero3 is not None:
@@ -524,6 +529,8 @@ class TrainingEngine:
                 if dp_rank != 0 and not (is_expert and dp_rank < ep):
                     continue
                 by_name.setdefault(k, {})[tp_rank] = v
+        if self.model_config.tie_word_embeddings:
+            by_name.pop("lm_head", None)  # the pipeline's copy of ``embed``: not a model parameter
         return {k: consolidate_tp(k, [s[i] for i in sorted(s)], self.model_config) for k, s in by_name.items()}
 
     def _make_profiler(self):

@@ -62,7 +62,10 @@ class FlatParameters:
     """Re-home ``named_params`` into flat buffers (in place: ``p.data`` becomes a view)."""
 
     def __init__(self, named_params: Sequence[Tuple[str, nn.Parameter]], *, bucket_numel: int,
-                 align: int = 64, grad_dtype: Optional[torch.dtype] = None, allocate_grad: bool = True):
+                 align: int = 64, grad_dtype: Optional[torch.dtype] = None, allocate_grad: bool = True,
+                 solo: Sequence[str] = ()):
+        """``solo``: parameter names that get a bucket of their own (the tied embedding copies
+        of a pipeline: equal-sized solo buckets make their ZeRO shards line up across stages)."""
         named_params = [(n, p) for n, p in named_params if p.requires_grad]
         if not named_params:
             raise ValueError("no trainable parameters")
@@ -90,6 +93,12 @@ class FlatParameters:
             cur: List[Tuple[str, nn.Parameter]] = []
             cur_n = 0
             for n, p in reversed(plist):
+                if n in solo:
+                    if cur:
+                        groups.append(cur)
+                    groups.append([(n, p)])
+                    cur, cur_n = [], 0
+                    continue
                 cur.append((n, p))
                 cur_n += p.numel()
                 if cur_n >= bucket_numel:

@@ -114,6 +114,7 @@ class FlatAdamW:
             self.exp_avg_sq = torch.zeros_like(self.master)
             self.grad_shard = torch.zeros(n, dtype=flat.grad_dtype, device=dev)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.norm_exclude: List = []  # callables -> (this rank's part of) a grad the clip norm skips
         self._pending = {}  # bucket index -> (all-gather work, input buffer)
         self.overlap_param_gather = False  # engines with forward pre-hooks turn this on
         self.overlap_update = False  # ZeRO-0: per-bucket update on a side stream, waited per layer
@@ -150,6 +151,10 @@ class FlatAdamW:
             if region == "replicated" and self.tp > 1 and self.tp_rank != 0:
                 continue  # counted once per TP group
             ops.l2norm_sq(g, buf)
+        for get in self.norm_exclude:  # a second copy of a tied matrix counts once
+            g = get()
+            if g is not None:
+                buf.sub_(g.float().square().sum())
         if self.zero_stage > 0 or self.dp_sharded:
             dist.all_reduce(buf, group=self.dp_group)
         if self.tp > 1:

@@ -255,6 +255,15 @@ class InferenceEngine:
                                                bufs["ctx_lens"])
         self._graphs[nb] = (g, bufs)
 
+    def release_graphs(self) -> None:
+        """Drop the captured decode graphs (they hold the RCCL communicator's captured
+        collectives: release them before ``destroy_process_group``)."""
+        if self._graphs and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        for g, _ in self._graphs.values():
+            g.reset()
+        self._graphs.clear()
+
     def decode_plan(self, seqs: List[Sequence]) -> Dict:
         return {"op": "decode", "ids": [s.all_ids[-1] for s in seqs], "positions": [s.num_tokens - 1 for s in seqs],
                 "slots": [s._decode_slot for s in seqs], "ctx": [self.kv.num_tokens(s.seq_id) for s in seqs],

@@ -114,6 +114,7 @@ class TPInferenceEngine(InferenceEngine):
     def stop_workers(self) -> None:
         if self.tp_rank == 0:
             self._bcast({"op": "stop"})
+        self.release_graphs()
 
     @torch.inference_mode()
     def worker_loop(self) -> None:
@@ -122,6 +123,7 @@ class TPInferenceEngine(InferenceEngine):
             plan = self._bcast(None)
             op = plan["op"]
             if op == "stop":
+                self.release_graphs()
                 return
             if op == "prefill":
                 self.prefill_exec(plan)

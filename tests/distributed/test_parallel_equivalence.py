@@ -91,6 +91,23 @@ def test_pp2_dp2_zero1_matches_single(ref_dp2_m4):
     _close(out[0]["state"], ref_dp2_m4["state"])
 
 
+def test_pp2_tied_embeddings_matches_single():
+    """GPT-2 style tied LM head split over two stages: the last stage's copy gets the summed
+    gradient and the clip norm counts the matrix once."""
+    ref = train_reference(STEPS, dp=1, model="tiny-tied", micro_per_rank=4)
+    out = run_ranks(train_layout, 2, STEPS, {"pp": 2, "microbatches": 4}, "tiny-tied")
+    _losses_close(out[0]["losses"], ref["losses"])
+    _close(out[0]["state"], ref["state"])
+
+
+@pytest.mark.parametrize("zero", [0, 1, 2])
+def test_pp2_tied_dp2_matches_single(zero):
+    ref = train_reference(STEPS, dp=2, model="tiny-tied", micro_per_rank=4)
+    out = run_ranks(train_layout, 4, STEPS, {"pp": 2, "microbatches": 4, "zero": zero}, "tiny-tied")
+    _losses_close(out[0]["losses"], ref["losses"])
+    _close(out[0]["state"], ref["state"])
+
+
 def test_zero3_dp2_matches_single(ref_dp2):
     out = run_ranks(train_layout, 2, STEPS, {"zero": 3})
     _losses_close(out[0]["losses"], ref_dp2["losses"])

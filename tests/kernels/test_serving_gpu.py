@@ -68,4 +68,9 @@ def test_tp_engine_rccl_world1_with_graphs(native_lib):
         assert tpe.stats["graph_replays"] > 0
         assert [s.output_ids for s in a] == [s.output_ids for s in b]
     finally:
+        import gc
+
+        tpe = None
+        gc.collect()
+        torch.cuda.synchronize()
         dist.destroy_process_group()

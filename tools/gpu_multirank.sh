@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export PYTHONPATH=$PWD
 i=0
-for extra in "--zero 1" "--zero 0" "--tp 2 --zero 0" "--zero 2"; do
+for extra in ${CONFIGS:-"--zero 1" "--zero 0" "--tp 2 --zero 0" "--zero 2"}; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29650+i)) \
     bench.py --gpus 2 --model ${MODEL:-gpt-125m} --seq-len 1024 --micro-batch 4 --steps 3 --warmup 1 --device cuda:0 --backend gloo $extra \
     > gpurun_out/multirank_$i.json 2> gpurun_out/multirank_$i.err || { tail -30 gpurun_out/multirank_$i.err; exit 1; }
