@@ -133,7 +133,8 @@ class PipelineSchedule:
         M = len(batches)
         P, s = self.P, self.s
         B, S = batches[0][0].shape
-        denom = float(batches[0][1].numel() * M)
+        # loss = per-token mean over the whole micro-batch set; CP ranks hold 1/cp of each sequence
+        denom = float(batches[0][1].numel() * M * self.e.pg.layout.cp)
         warm = min(P - s - 1, M)
         inputs: List[Optional[torch.Tensor]] = []
         outputs: List[torch.Tensor] = []
@@ -220,22 +221,26 @@ class PipelineSchedule:
         if not self.is_last:
             t.zero_()
         dist.all_reduce(t, group=self.e.pg.pp_group)
+        if self.e.pg.cp_group is not None:  # CP ranks hold partial sums of one loss
+            dist.all_reduce(t, group=self.e.pg.cp_group)
         if self.e.pg.dp_group is not None:
             dist.all_reduce(t, group=self.e.pg.dp_group)
             t /= self.e.pg.layout.dp
         return float(t)
 
     @torch.no_grad()
-    def eval_loss(self, ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    def eval_loss(self, ids: torch.Tensor, labels: torch.Tensor, denom: Optional[float] = None) -> torch.Tensor:
         B, S = ids.shape
         x_in = None
         if not self.is_first:
             x_in = self._empty(B, S)
             self._p2p(recv=(x_in, self.prev))
-        out = self._forward(x_in, ids, labels, float(labels.numel()))
+        out = self._forward(x_in, ids, labels, float(denom if denom is not None else labels.numel()))
         if not self.is_last:
             self._p2p(send=(out, self.next))
             out = torch.zeros((), device=self.e.device)
         t = out.float().reshape(1).clone()
         dist.all_reduce(t, group=self.e.pg.pp_group)
+        if self.e.pg.cp_group is not None:
+            dist.all_reduce(t, group=self.e.pg.cp_group)
         return t[0]

@@ -243,6 +243,15 @@ class Zero3Model:
             self._gather(self.root)
             self._begin_backward(self.root)
 
+    def gather_root(self):
+        """Pipeline evaluation calls embed / head outside the hooked forward."""
+        if self.root is not None:
+            self._gather(self.root)
+
+    def release_root(self):
+        if self.root is not None and self.root.full is not None:
+            self._release(self.root)
+
     def set_sync(self, enabled: bool):
         self._sync_enabled = enabled
 

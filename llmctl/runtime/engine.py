@@ -156,8 +156,6 @@ class TrainingEngine:
                 # the GEMM grids, so the last buckets are not left exposed after backward
                 os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
             dist.init_process_group(backend=backend, **kw)
-        if c.context_parallel > 1 and c.pipeline_parallel > 1:
-            raise NotImplementedError("context_parallel with pipeline_parallel is not supported")
         if c.pack_sequences and (c.context_parallel > 1 or c.pipeline_parallel > 1):
             raise NotImplementedError("pack_sequences with context / pipeline parallelism is not supported")
         if c.expert_parallel > 1 and (c.tensor_parallel > 1 or c.pipeline_parallel > 1 or c.context_parallel > 1
@@ -326,17 +324,14 @@ class TrainingEngine:
             self.eflat.zero_grad()
         if self.zero3 is not None:
             self.zero3.begin_step()
+        cpn = self.pg.layout.cp
+        if cpn > 1:  # this rank's contiguous chunk of every sequence
+            batches = self._cp_split(batches)
         if self.pipeline is not None:
             self.optimizer.wait_params()  # stages call embed/head outside the hooked forward
             loss = self.pipeline.run(batches)
         else:
             n = len(batches)
-            cpn = self.pg.layout.cp
-            if cpn > 1:  # this rank's contiguous chunk of every sequence
-                from llmctl.parallel.context_parallel import split_sequence
-
-                batches = [(split_sequence(x, cpn, self.pg.cp_rank), split_sequence(y, cpn, self.pg.cp_rank))
-                           for x, y in batches]
             tokens = batches[0][1].numel() * cpn  # per replica: the CP ranks share one sequence
             # loss is a per-token mean inside each micro-batch; dividing the denominator
             # by n makes the accumulated gradient the mean over all n micro-batches
@@ -377,18 +372,36 @@ class TrainingEngine:
         self.consumed_samples += sum(b[0].shape[0] for b in batches) * self.pg.layout.dp
         return {"loss": loss, "grad_norm": gnorm, "lr": torch.tensor(lr)}
 
+    def _cp_split(self, batches):
+        from llmctl.parallel.context_parallel import split_sequence
+
+        cpn, r = self.pg.layout.cp, self.pg.cp_rank
+        return [(split_sequence(x, cpn, r), split_sequence(y, cpn, r)) for x, y in batches]
+
     @torch.no_grad()
     def evaluate(self, batches) -> float:
         self.optimizer.wait_params()
         self.model.eval()
         tot, n = 0.0, 0
+        cpn = self.pg.layout.cp
+        root = self.zero3 is not None and self.pipeline is not None
+        if root:
+            self.zero3.gather_root()
         for x, y in batches:
+            denom = float(y.numel())  # whole-sequence token count (CP ranks hold chunks)
+            if cpn > 1:
+                (x, y), = self._cp_split([(x, y)])
             if self.pipeline is not None:
-                l = self.pipeline.eval_loss(x, y)
+                l = self.pipeline.eval_loss(x, y, denom)
             else:
-                l = self.model(x, y)
+                l = self.model(x, y, loss_denom=denom)
+                if cpn > 1:  # partial sums of one mean
+                    l = l.detach().float().reshape(1).clone()
+                    dist.all_reduce(l, group=self.pg.cp_group)
             tot += float(l)
             n += 1
+        if root:
+            self.zero3.release_root()
         return tot / max(n, 1)
 
     # ------------------------------------------------------------------ loop

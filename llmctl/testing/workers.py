@@ -73,8 +73,9 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
                 torch.distributed.all_reduce(lt, group=eng.pg.dp_group)
                 lt /= eng.pg.layout.dp
             losses.append(float(lt))
+    ev = eng.evaluate([make_batch(vocab, cfg.seq_len, cfg.batch_size, 99, 0)])
     full = eng.gather_full_state_dict()
-    return {"losses": losses, "state": full if rank == 0 else None}
+    return {"losses": losses, "state": full if rank == 0 else None, "eval": ev}
 
 
 def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: int = 1) -> dict:
@@ -95,7 +96,8 @@ def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: in
                    for i in range(micro_per_rank)]
         out = eng.train_step(batches)
         losses.append(float(out["loss"]))  # already the mean over all micro-batches
-    return {"losses": losses, "state": eng.gather_full_state_dict()}
+    ev = eng.evaluate([make_batch(vocab, cfg.seq_len, cfg.batch_size, 99, 0)])
+    return {"losses": losses, "state": eng.gather_full_state_dict(), "eval": ev}
 
 
 PROMPTS = [[1, 2, 3, 4, 5], [9] * 13, [7, 7], [3, 1, 4, 1, 5, 9, 2, 6]]

@@ -108,6 +108,14 @@ def test_pp2_tied_dp2_matches_single(zero):
     _close(out[0]["state"], ref["state"])
 
 
+@pytest.mark.parametrize("cp_mode", ["ulysses", "ring"])
+def test_pp2_cp2_matches_single(ref_dp1_m4, cp_mode):
+    out = run_ranks(train_layout, 4, STEPS, {"pp": 2, "cp": 2, "cp_mode": cp_mode, "microbatches": 4})
+    _losses_close(out[0]["losses"], ref_dp1_m4["losses"])
+    _losses_close([out[0]["eval"]], [ref_dp1_m4["eval"]])  # CP-split, pipelined evaluation
+    _close(out[0]["state"], ref_dp1_m4["state"])
+
+
 def test_zero3_dp2_matches_single(ref_dp2):
     out = run_ranks(train_layout, 2, STEPS, {"zero": 3})
     _losses_close(out[0]["losses"], ref_dp2["losses"])
@@ -124,6 +132,7 @@ def test_cp2_ulysses_matches_single(ref_dp1):
     """Context parallel: each rank holds half of every sequence; all-to-all around attention."""
     out = run_ranks(train_layout, 2, STEPS, {"cp": 2})
     _losses_close(out[0]["losses"], ref_dp1["losses"])
+    _losses_close([out[0]["eval"]], [ref_dp1["eval"]])
     _close(out[0]["state"], ref_dp1["state"])
 
 
