@@ -114,8 +114,16 @@ class PipelineSchedule:
     def _forward(self, x_in: Optional[torch.Tensor], ids: torch.Tensor, labels: torch.Tensor, denom: float):
         m = self.e.model
         B, S = ids.shape
-        x = m.embed_tokens(ids) if self.is_first else x_in
-        x, res = m.run_layers(x, B, S)
+        positions = doc_start = None
+        c = self.e.config
+        if c.pack_sequences:  # every stage rebuilds the document map from the (shared) token ids
+            from llmctl.ops.ref import document_starts
+
+            doc_start = document_starts(ids, c.doc_separator)
+            labels = labels.masked_fill(ids == c.doc_separator, -100)
+            positions = (torch.arange(S, device=ids.device, dtype=torch.int32).view(1, S) - doc_start).reshape(-1)
+        x = m.embed_tokens(ids, positions) if self.is_first else x_in
+        x, res = m.run_layers(x, B, S, positions=positions, doc_start=doc_start)
         if self.is_last:
             logits = m.head(x, res)
             return m.loss(logits, labels, denom)

@@ -156,8 +156,8 @@ class TrainingEngine:
                 # the GEMM grids, so the last buckets are not left exposed after backward
                 os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
             dist.init_process_group(backend=backend, **kw)
-        if c.pack_sequences and (c.context_parallel > 1 or c.pipeline_parallel > 1):
-            raise NotImplementedError("pack_sequences with context / pipeline parallelism is not supported")
+        if c.pack_sequences and c.context_parallel > 1:
+            raise NotImplementedError("pack_sequences with context parallelism is not supported")
         if c.expert_parallel > 1 and (c.tensor_parallel > 1 or c.pipeline_parallel > 1 or c.context_parallel > 1
                                       or c.zero_stage >= 3):
             raise NotImplementedError("expert_parallel composes with DP / ZeRO-1/2 only")

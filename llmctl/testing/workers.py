@@ -12,10 +12,15 @@ from typing import Dict, List, Optional
 import torch
 
 
-def make_batch(vocab: int, seq: int, mb: int, step: int, dp_rank: int, micro: int = 0):
+PACK_SEP = 7  # document separator of the packed-sequence layouts
+
+
+def make_batch(vocab: int, seq: int, mb: int, step: int, dp_rank: int, micro: int = 0, pack: bool = False):
     g = torch.Generator()
     g.manual_seed(10007 * step + 101 * dp_rank + micro)
     t = torch.randint(0, vocab, (mb, seq + 1), generator=g)
+    if pack:  # several documents per row
+        t[:, 5::11] = PACK_SEP
     return t[:, :-1].contiguous(), t[:, 1:].contiguous()
 
 
@@ -51,7 +56,8 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
                   num_microbatches=layout.get("microbatches", 0),
                   context_parallel=layout.get("cp", 1),
                   context_parallel_mode=layout.get("cp_mode", "ulysses"),
-                  expert_parallel=layout.get("ep", 1))
+                  expert_parallel=layout.get("ep", 1),
+                  pack_sequences=layout.get("pack", False), doc_separator=PACK_SEP)
     eng = TrainingEngine(cfg)
     eng.load_full_state_dict(reference_state(model))
     vocab = eng.model_config.vocab_size
@@ -59,7 +65,8 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
     dp_rank = eng.pg.dp_rank
     nmb = eng.pipeline.num_microbatches if eng.pipeline is not None else micro_per_rank
     for s in range(steps):
-        batches = [make_batch(vocab, cfg.seq_len, cfg.batch_size, s, dp_rank, i) for i in range(nmb)]
+        batches = [make_batch(vocab, cfg.seq_len, cfg.batch_size, s, dp_rank, i, cfg.pack_sequences)
+                   for i in range(nmb)]
         out = eng.train_step(batches)
         loss = out["loss"]
         if eng.pipeline is not None:
@@ -78,7 +85,8 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
     return {"losses": losses, "state": full if rank == 0 else None, "eval": ev}
 
 
-def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: int = 1) -> dict:
+def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: int = 1,
+                    pack: bool = False) -> dict:
     """Single process; the DP ranks' batches are accumulation micro-steps."""
     import os
 
@@ -86,13 +94,13 @@ def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: in
 
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         os.environ.pop(k, None)
-    cfg = _config(model_name_or_path=model)
+    cfg = _config(model_name_or_path=model, pack_sequences=pack, doc_separator=PACK_SEP)
     eng = TrainingEngine(cfg)
     eng.load_full_state_dict(reference_state(model))
     vocab = eng.model_config.vocab_size
     losses = []
     for s in range(steps):
-        batches = [make_batch(vocab, cfg.seq_len, cfg.batch_size, s, r, i) for r in range(dp)
+        batches = [make_batch(vocab, cfg.seq_len, cfg.batch_size, s, r, i, pack) for r in range(dp)
                    for i in range(micro_per_rank)]
         out = eng.train_step(batches)
         losses.append(float(out["loss"]))  # already the mean over all micro-batches

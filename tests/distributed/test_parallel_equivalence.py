@@ -116,6 +116,14 @@ def test_pp2_cp2_matches_single(ref_dp1_m4, cp_mode):
     _close(out[0]["state"], ref_dp1_m4["state"])
 
 
+def test_pp2_packed_sequences_matches_single():
+    """Packed documents: every stage rebuilds the document map, the last masks separators."""
+    ref = train_reference(STEPS, dp=1, micro_per_rank=4, pack=True)
+    out = run_ranks(train_layout, 2, STEPS, {"pp": 2, "microbatches": 4, "pack": True})
+    _losses_close(out[0]["losses"], ref["losses"])
+    _close(out[0]["state"], ref["state"])
+
+
 def test_zero3_dp2_matches_single(ref_dp2):
     out = run_ranks(train_layout, 2, STEPS, {"zero": 3})
     _losses_close(out[0]["losses"], ref_dp2["losses"])
