@@ -17,6 +17,12 @@ keep a bf16 ``W^T`` copy, refreshed by the transpose HIP kernel the first time t
 used after an optimizer step (``GradSink.epoch``; under ZeRO-1/2 that is after the layer's
 all-gather has landed), and the backward computes ``dX = F.linear(dY, W^T)``.  Cost: one
 bf16 copy of the projection weights and ~2 x 13.5 GB of HBM transpose traffic per step.
+
+Round 2: where the shapes fit (tokens a multiple of 256, in/out features of 256/128), the data
+gradient runs on the in-house 64-deep MFMA kernel (``gemm64_ex``, llmctl/ops/csrc/gemm64.hip),
+which reads ``W`` K-major through ``ds_read_b64_tr_b16`` — faster than hipBLASLt's NN and TN
+kernels on the GPT-7B shapes, and no ``W^T`` copy is kept (the copy remains the fallback for
+other shapes).  Weight gradients go to the same kernel family.
 """
 
 from __future__ import annotations
@@ -27,6 +33,55 @@ import os
 
 import torch
 import torch.nn.functional as F
+
+
+# gemm64_ex config: tile-order group 4, schedule variant 1 (DMA issued in the read section)
+# — the fastest of the A/B in profiles/gemm64_variants_r2.jsonl on every GPT-7B shape
+GEMM64_CONFIG = int(os.environ.get("LLMCTL_GEMM64_CONFIG", "104"))
+
+
+def _gemm64_enabled() -> bool:
+    return os.environ.get("LLMCTL_GEMM64", "1") != "0"  # =0: A/B against the older paths
+
+
+def _rows_ok(*ts: torch.Tensor) -> bool:
+    for t in ts:
+        if t.stride(1) != 1 or t.stride(0) % 8 or t.data_ptr() % 16:
+            return False
+    return True
+
+
+def _gemm64_ok(M: int, N: int, K: int, *ts: torch.Tensor) -> bool:
+    """Shapes the 64-deep MFMA kernel (llmctl/ops/csrc/gemm64.hip) takes: M, N multiples of
+    256, K of 128, bf16 GPU operands with 16-byte aligned unit-stride rows."""
+    if not _gemm64_enabled() or M % 256 or N % 256 or K % 128 or K == 0:
+        return False
+    if not all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts):
+        return False
+    from llmctl.ops._lib import use_native
+
+    return use_native(ts[0]) and _rows_ok(*ts)
+
+
+def dgrad64_shape_ok(tokens: int, w: torch.Tensor) -> bool:
+    """Will ``dx = dy W`` for ``tokens`` rows run on gemm64?  (Decided at forward time: the
+    weight's W^T copy is only kept for layers whose data gradient cannot.)"""
+    out, inn = w.shape
+    return _gemm64_ok(tokens, inn, out, w) and out * w.stride(0) * 2 < 2**31
+
+
+def dgrad64_ok(dy2: torch.Tensor, w: torch.Tensor) -> bool:
+    """``dx = dy W`` on gemm64 (W read K-major through ds_read_b64_tr_b16: no W^T copy)."""
+    return (dy2.dim() == 2 and dy2.shape[1] == w.shape[0] and dgrad64_shape_ok(dy2.shape[0], w)
+            and dy2.is_cuda and dy2.dtype == torch.bfloat16 and _rows_ok(dy2))
+
+
+def dgrad64(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    from llmctl.ops._lib import native
+
+    dx = torch.empty(dy2.shape[0], w.shape[1], dtype=dy2.dtype, device=dy2.device)
+    native().gemm64_ex(dy2, w, dx, False, True, False, GEMM64_CONFIG)
+    return dx
 
 
 def _gemm_ex_ok(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
@@ -49,10 +104,16 @@ def _gemm_ex_ok(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
 
 
 def wgrad_into(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> None:
-    """``g (+)= dy2^T @ x2``: the MFMA kernel reads both K-major operands through
-    ds_read_b64_tr_b16 (+12-26 % over hipBLASLt on the GPT-7B shapes, profiles/gemm_bench_r1.json);
+    """``g (+)= dy2^T @ x2``: the MFMA kernels read both K-major operands through
+    ds_read_b64_tr_b16 (gemm64: +20-40 % over hipBLASLt on the GPT-7B shapes,
+    profiles/gemm64_variants_r2.jsonl; the 32-deep gemm_ex where K is not a multiple of 128);
     other shapes go to hipBLASLt."""
-    if _gemm_ex_ok(g, dy2, x2):
+    M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
+    if (_gemm64_ok(M, N, K, g, dy2, x2) and K * dy2.stride(0) * 2 < 2**31 and K * x2.stride(0) * 2 < 2**31):
+        from llmctl.ops._lib import native
+
+        native().gemm64_ex(dy2, x2, g, True, True, accumulate, GEMM64_CONFIG)
+    elif _gemm_ex_ok(g, dy2, x2):
         from llmctl.ops._lib import native
 
         native().gemm_ex(dy2, x2, g, True, True, accumulate)
@@ -114,7 +175,9 @@ class _Linear(torch.autograd.Function):
         ctx.wparam = w
         ctx.has_b = b is not None
         sink = getattr(w, "_llmctl_grad_sink", None)
-        ctx.wt = sink.weight_t(w) if sink is not None and ctx.needs_input_grad[0] else None
+        ctx.wt = None
+        if sink is not None and ctx.needs_input_grad[0] and not dgrad64_shape_ok(x.numel() // x.shape[-1], w):
+            ctx.wt = sink.weight_t(w)
         return F.linear(x, w, b)
 
     @staticmethod
@@ -131,7 +194,10 @@ class _Linear(torch.autograd.Function):
                 dw = dy2.t().matmul(x2)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = F.linear(dy, ctx.wt) if ctx.wt is not None else dy.matmul(w)
+            if dgrad64_ok(dy2, w):
+                dx = dgrad64(dy2, w).view(*dy.shape[:-1], w.shape[1])
+            else:
+                dx = F.linear(dy, ctx.wt) if ctx.wt is not None else dy.matmul(w)
         db = dy2.sum(0) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db
 
@@ -144,8 +210,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
 
 
 def data_grad(dy: torch.Tensor, w: torch.nn.Parameter) -> torch.Tensor:
-    """``dy @ w`` for hand-written backward passes, through the weight's transposed copy when
-    its sink keeps one."""
+    """``dy @ w`` for hand-written backward passes: gemm64 when the shape fits, else through
+    the weight's transposed copy when its sink keeps one."""
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    if dgrad64_ok(dy2, w):
+        return dgrad64(dy2, w).view(*dy.shape[:-1], w.shape[1])
     sink = getattr(w, "_llmctl_grad_sink", None)
     wt = sink.weight_t(w) if sink is not None else None
     return F.linear(dy, wt) if wt is not None else dy.matmul(w)

@@ -256,6 +256,8 @@ class CheckpointManager:
                 g = _global_name(n, e.pc.layer_start)
                 if hasattr(e, "_expert_global"):
                     g = e._expert_global(g)
+                if g == "lm_head" and g not in full and e.model_config.tie_word_embeddings:
+                    g = "embed"  # PP>1 last-stage copy of a tied matrix saved under PP=1 / HF
                 if g not in full:
                     raise KeyError(f"checkpoint {p} lacks tensor {g}")
                 t = shard_tp(g, full[g], e.pg.layout.tp, e.pg.tp_rank, e.model_config)
@@ -343,6 +345,8 @@ def reshard_optimizer(e, path: Path, state: Dict[str, Any]) -> None:
     new_tp, new_tr = e.pg.layout.tp, e.pg.tp_rank
     for q in flat.params:
         g = _global_name(flat.names[id(q)], start)
+        if g == "lm_head" and g not in where and cfg.tie_word_embeddings:
+            g = "embed"  # tied matrix: the PP>1 last-stage copy restarts from embed's state
         if g not in where:
             raise KeyError(f"optimizer state for {g} missing in {path}")
         per_tp = where[g]

@@ -1,8 +1,8 @@
 """Build the in-tree HIP kernel library ``llmctl/ops/_llmctl_hip.so`` for gfx950.
 
 Plain ``hipcc`` invocations (no hipify, no torch JIT cache): every ``csrc/*.hip`` /
-``csrc/*.cpp`` compiles to an object under ``build/ops`` (rebuilt only when the source or a
-header is newer), then one link step produces the shared library next to this file, so it
+``csrc/*.cpp`` compiles to an object under ``build/ops`` (rebuilt when the content hash of the
+source, the headers or the flags changes), then one link step produces the shared library next to this file, so it
 travels with the repository snapshot to the GPU box.
 
     python -m llmctl.ops.build [-j N] [--force] [--arch gfx950] [--save-temps]
@@ -47,12 +47,22 @@ def compile_flags(arch: str, save_temps: bool = False):
     return flags
 
 
-def _needs(src: Path, obj: Path) -> bool:
-    if not obj.exists():
-        return True
-    t = obj.stat().st_mtime
-    deps = [src] + list(CSRC.glob("*.h"))
-    return any(d.stat().st_mtime > t for d in deps)
+def _digest(src: Path, flags) -> str:
+    """Content key of one object: the source, every csrc header and the compile flags (not
+    mtimes: a restored or copied tree can carry stale objects with newer timestamps)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for d in [src] + sorted(CSRC.glob("*.h")):
+        h.update(d.name.encode())
+        h.update(d.read_bytes())
+    h.update("\0".join(flags).encode())
+    return h.hexdigest()
+
+
+def _needs(src: Path, obj: Path, flags) -> bool:
+    key = obj.with_suffix(obj.suffix + ".key")
+    return not (obj.exists() and key.exists() and key.read_text() == _digest(src, flags))
 
 
 def build(arch: str = "gfx950", jobs: int = 0, force: bool = False, save_temps: bool = False, verbose: bool = True) -> Path:
@@ -64,7 +74,7 @@ def build(arch: str = "gfx950", jobs: int = 0, force: bool = False, save_temps: 
     for s in srcs:
         o = BUILD / (s.name + ".o")
         objs.append(o)
-        if force or _needs(s, o):
+        if force or _needs(s, o, flags):
             todo.append((s, o))
 
     def _one(so):
@@ -73,6 +83,7 @@ def build(arch: str = "gfx950", jobs: int = 0, force: bool = False, save_temps: 
         r = subprocess.run(cmd, capture_output=True, text=True, cwd=str(BUILD))
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {s.name}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        o.with_suffix(o.suffix + ".key").write_text(_digest(s, flags))
         return s.name
 
     jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))

@@ -56,5 +56,6 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("car_error(int sig_ptr) -> int", &llmctl::car_error);
   m.def("gemm_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int variant=-1) -> ()");
   m.def("hbm_copy(Tensor src, Tensor(a!) dst) -> ()");
+  m.def("gemm64_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int config=4) -> ()");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
 }

@@ -1,0 +1,409 @@
+// bf16 MFMA GEMM, 256x256 tile, 64-deep K-tiles, half-tile LDS-DMA pipeline (gfx950).
+//
+//   C[M,N] (+)= sum_k A(m,k) * B(n,k)        fp32 accumulate, bf16 in/out
+//
+// Operand storage per template flag, as in gemm_bf16.hip: "K-contiguous" (A [M][K], B [N][K])
+// or "K-major" (A [K][M], B [K][N]); the three products of a linear layer map to
+//   forward  y  = x  W^T :  A = x [T][in], B = W [out][in]                  (AT=0, BT=0)
+//   dgrad    dx = dy W   :  A = dy [T][out], B(n=in,k=out) = W [out][in]     (AT=0, BT=1)
+//   wgrad    dW = dy^T x :  A(m=out,k=t) = dy [t][out], B(n=in,k=t) = x [t][in] (AT=1, BT=1)
+//
+// Why a second kernel family: gemm_bf16.hip stages 32-deep K-tiles, so a K-contiguous operand
+// row contributes 64 B per tile — every 128-B line is fetched in two halves by two tiles, and
+// that layout ran at 1.17-1.21 PF where the K-major (full 512-B rows) layouts reached 1.23-1.36
+// (profiles/gemm_bench_r1.json).  Here a K-tile is 64 deep: a K-contiguous row is one full
+// 128-B line per tile, a K-major image row is 256 B.
+//
+// Structure (CDNA guide §5 "256² 8-phase template", re-derived for this tile):
+//   * 8 waves = 2 (M) x 4 (N); wave (wr, wc) owns the 128x64 output block at rows wr*128,
+//     cols wc*64 = 8x4 tiles of mfma_f32_16x16x32_bf16 (128 accumulator registers), computed
+//     transposed (B fragment as the MFMA row operand) so a lane holds 4 consecutive columns.
+//   * A K-tile is staged as four 16-KB half-tiles, each filled by 2 LDS-DMA instructions per
+//     thread (buffer_load_dwordx4 ... lds, lane-linear image, swizzle applied to the SOURCE):
+//        A_lo = rows {0..63, 128..191}   (m-tiles 0-3 of both wave rows)
+//        A_hi = rows {64..127, 192..255} (m-tiles 4-7)
+//        B_h0 = cols 0..127 (waves wc 0,1), B_h1 = cols 128..255 (waves wc 2,3)
+//     Two K-tile buffers (128 KB of LDS).
+//   * 4 phases per K-tile, 16 MFMAs each (one 64x32 quadrant x K=64):
+//        j=0  read A_lo frags (m 0-3) + B frags n 0-1 -> quadrant (m 0-3, n 0-1)
+//        j=1  read B frags n 2-3                      -> (m 0-3, n 2-3)
+//        j=2  read A_hi frags (m 4-7)                 -> (m 4-7, n 2-3)
+//        j=3  (no reads)                              -> (m 4-7, n 0-1)
+//     Each phase issues ONE half-tile of the stream (2 DMA instructions) right after its first
+//     barrier:  j=0: B_h1(t+1)  j=1: A_hi(t+1)  j=2: A_lo(t+2)  j=3: B_h0(t+2).
+//     Every slot is restaged >= 2 phases after its last read (WAR); the counted waits
+//        j=1: vmcnt(6)  (retires A_hi(t), read at j=2)
+//        j=3: vmcnt(4)  (retires A_lo/B_h0/B_h1 of t+1, read at j=0 of t+1)
+//     sit before the first barrier of the phase BEFORE the read (RAW across waves), so at
+//     least 2-3 half-tiles stay in flight across every barrier; raw s_barrier only.
+//   * Two wave groups (wr = 0 / 1, one wave of each per SIMD) run one barrier apart: one
+//     group's LDS fragment reads overlap the other group's MFMAs (ping-pong).
+//   * Stream items past the last K-tile re-load the last K-tile (clamped source) into slots
+//     nobody reads again, so the wait counts never change in the tail.
+//   * XCD-aware bijective block remap + grouped tile order (GROUP tile-rows).
+#include "attn_common.h"
+
+namespace llmctl {
+using namespace attn;
+namespace {
+
+using f32x4_t = __attribute__((ext_vector_type(4))) float;
+using s2_t = __attribute__((ext_vector_type(2))) unsigned int;
+using i32x4_t = __attribute__((ext_vector_type(4))) int;
+
+constexpr int TM = 256, TN = 256, TK = 64;
+constexpr int HALF = 16384;       // bytes per half-tile image
+constexpr int BUF = 4 * HALF;     // one K-tile: A_lo, A_hi, B_h0, B_h1
+constexpr int NTHR = 512;
+enum : int { A_LO = 0, A_HI = 1, B_H0 = 2, B_H1 = 3 };
+
+// epilogues
+enum : int { EPI_STORE = 0, EPI_ACC = 1 };
+template <int V>
+using K_ = std::integral_constant<int, V>;
+
+struct G64Args {
+  const unsigned short* a;
+  const unsigned short* b;
+  unsigned short* c;
+  long lda, ldb, ldc;
+  int M, N, K;
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ i32x4_t make_rsrc(const void* base) {
+  const unsigned long a = (unsigned long)base;
+  i32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));
+  r[2] = -1;          // num_records: no clamping (offsets validated on the host)
+  r[3] = 0x00020000;  // raw buffer, 32-bit data format
+  return r;
+}
+// one LDS-DMA piece: 64 lanes x 16 B -> LDS [lds_byte, +1024), lane-linear
+__device__ __forceinline__ void bdma16(i32x4_t rsrc, unsigned voff, unsigned soff, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
+               "s"(soff), "s"(lds_byte)
+               : "memory");
+}
+
+__device__ __forceinline__ void bar() { __builtin_amdgcn_s_barrier(); }
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "add the immediate");
+}
+
+// ---- half-tile images -----------------------------------------------------------------------
+// row image (K-contiguous operand): [128 image rows][64 k], 128-B rows, 16-B chunk c stored at
+//   c ^ ((row >> 1) & 7): each ds_read_b128 lane group (16 lanes: rows r..r+15 at two chunks)
+//   lands on 16 distinct 16-B bank slots.
+// tr image (K-major operand): [64 k][128 image cols], 256-B rows, 32-B segment s stored at
+//   s ^ h(k), h(k) = (k & 3) | ((k >> 3) & 1) << 2: the 8 k-rows of a 32-lane
+//   ds_read_b64_tr_b16 half hit 8 distinct segments (conflict-free).
+__device__ __forceinline__ int swr(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int swt(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+// image row/col -> tile row/col of each half-tile kind (both image kinds have 128 positions)
+template <int KIND>
+__device__ __forceinline__ int tile_pos(int ip) {
+  if constexpr (KIND == A_LO) return (ip >> 6) * 128 + (ip & 63);
+  else if constexpr (KIND == A_HI) return (ip >> 6) * 128 + 64 + (ip & 63);
+  else if constexpr (KIND == B_H0) return ip;
+  else return 128 + ip;
+}
+
+// per-thread byte offset (relative to the operand's tile origin at k = 0) of DMA piece i
+template <bool T, int KIND>
+__device__ __forceinline__ unsigned stage_voff(int i, int tid, long ld) {
+  const int c = i * NTHR + tid;  // 16-B chunk index in the half-tile image
+  if constexpr (!T) {
+    const int ir = c >> 3, pc = c & 7;
+    const int row = tile_pos<KIND>(ir);
+    return (unsigned)(((long)row * ld + ((pc ^ swr(ir)) << 3)) * 2);
+  } else {
+    const int k = c >> 4, pc = c & 15;
+    const int seg = (pc >> 1) ^ swt(k);
+    const int col = tile_pos<KIND>(seg * 16 + (pc & 1) * 8);
+    return (unsigned)(((long)k * ld + col) * 2);
+  }
+}
+
+// MFMA operand fragment (16 positions x 32 k): lane l holds X(p0 + (l & 15), 32 ks + 8 (l >> 4) + j)
+template <bool T>
+__device__ __forceinline__ bf16x8_t frag(const unsigned char* img, int p0, int ks, int lane) {
+  const int g = lane >> 4, i16 = lane & 15;
+  if constexpr (!T) {
+    const int ir = p0 + i16;
+    const int c = ks * 4 + g;
+    return *reinterpret_cast<const bf16x8_t*>(img + ir * 128 + ((c ^ swr(ir)) << 4));
+  } else {
+    const int q = i16 >> 2, p = i16 & 3;
+    const int k = ks * 32 + 8 * g + q;
+    const int seg = (p0 >> 4) ^ swt(k);
+    const int off = k * 256 + seg * 32 + p * 8;
+    s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + off));
+    s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + off + 4 * 256));
+    s8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+template <bool AT, bool BT, int EPI, int GROUP, int V>
+__global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // ---- tile selection: XCD-bijective remap, then grouped (GROUP tile-rows) order
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  int wg;
+  {
+    const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
+    wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
+  }
+  const int per_group = GROUP * args.tiles_n;
+  const int grp = wg / per_group;
+  const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
+  const int inner = wg - grp * per_group;
+  const int tm = grp * GROUP + inner % gsz;
+  const int tn = inner / gsz;
+
+  const long lda = args.lda, ldb = args.ldb;
+  const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
+  const unsigned short* Bb = BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
+  const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
+  // byte step of one K-tile in each operand
+  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
+  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
+  const int KT = args.K / TK;
+
+  unsigned vo[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    vo[A_LO][i] = stage_voff<AT, A_LO>(i, tid, lda);
+    vo[A_HI][i] = stage_voff<AT, A_HI>(i, tid, lda);
+    vo[B_H0][i] = stage_voff<BT, B_H0>(i, tid, ldb);
+    vo[B_H1][i] = stage_voff<BT, B_H1>(i, tid, ldb);
+  }
+  const unsigned lds0 = lds_addr(smem) + wave * 1024;
+
+  // stream item: half-tile KIND of K-tile t (clamped: past-the-end items re-load the last tile)
+  auto issue = [&](auto kind_c, int t) {
+    constexpr int kind = decltype(kind_c)::value;
+    const int tc = t < KT ? t : KT - 1;
+    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
+    if constexpr (kind <= A_HI) {
+      const unsigned so = __builtin_amdgcn_readfirstlane(tc * a_kstep);
+      bdma16(ra, vo[kind][0], so, l);
+      bdma16(ra, vo[kind][1], so, l + 8192);
+    } else {
+      const unsigned so = __builtin_amdgcn_readfirstlane(tc * b_kstep);
+      bdma16(rb, vo[kind][0], so, l);
+      bdma16(rb, vo[kind][1], so, l + 8192);
+    }
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: the stream up to B_h0(1) in flight; retire A_lo/B_h0/B_h1 of K-tile 0
+  issue(K_<A_LO>{}, 0);
+  issue(K_<B_H0>{}, 0);
+  issue(K_<B_H1>{}, 0);
+  issue(K_<A_HI>{}, 0);
+  issue(K_<A_LO>{}, 1);
+  issue(K_<B_H0>{}, 1);
+  wait_vm<6>();
+  bar();
+  if (wr == 1) bar();  // wave group 1 runs one barrier behind group 0
+
+  const int ap = wr * 64;              // this wave's first image row/col in an A half-tile
+  const int bh = (wc >> 1) * HALF;     // this wave's B half-tile
+  const int bp = (wc & 1) * 64;        // ... and its first position in it
+  bf16x8_t af[4][2], bfr[4][2];
+
+  // V bits (A/B'd by tools/gemm64_bench.py): 1 = issue the phase's DMA in the read section
+  // (before the wait and the first barrier, where the wave otherwise idles at the barrier)
+  // instead of right before the MFMAs; 2 = no s_setprio around the MFMA cluster
+  constexpr bool EARLY = V & 1, PRIO = !(V & 2);
+  auto mfma_quadrant = [&](auto m0_c, auto n0_c) {
+    constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[m0 + i][n0 + j] = mfma16(bfr[n0 + j][ks], af[i][ks], acc[m0 + i][n0 + j]);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+  // EARLY moves each issue ahead of its phase's wait: the waits then count 2 more pieces
+  auto ktile = [&](int t, const unsigned char* buf) {
+    // j = 0
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_LO * HALF, ap + 16 * i, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
+    if constexpr (EARLY) issue(K_<B_H1>{}, t + 1);
+    bar();
+    if constexpr (!EARLY) issue(K_<B_H1>{}, t + 1);
+    mfma_quadrant(K_<0>{}, K_<0>{});
+    bar();
+    // j = 1
+#pragma unroll
+    for (int j = 2; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
+    if constexpr (EARLY) {
+      issue(K_<A_HI>{}, t + 1);
+      wait_vm<8>();
+      bar();
+    } else {
+      wait_vm<6>();
+      bar();
+      issue(K_<A_HI>{}, t + 1);
+    }
+    mfma_quadrant(K_<0>{}, K_<2>{});
+    bar();
+    // j = 2
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_HI * HALF, ap + 16 * i, ks, lane);
+    if constexpr (EARLY) issue(K_<A_LO>{}, t + 2);
+    bar();
+    if constexpr (!EARLY) issue(K_<A_LO>{}, t + 2);
+    mfma_quadrant(K_<4>{}, K_<2>{});
+    bar();
+    // j = 3
+    if constexpr (EARLY) {
+      issue(K_<B_H0>{}, t + 2);
+      wait_vm<6>();
+      bar();
+    } else {
+      wait_vm<4>();
+      bar();
+      issue(K_<B_H0>{}, t + 2);
+    }
+    mfma_quadrant(K_<4>{}, K_<0>{});
+    bar();
+  };
+
+  for (int t = 0; t < KT; t += 2) {
+    ktile(t, smem);
+    ktile(t + 1, smem + BUF);
+  }
+  if (wr == 0) bar();  // re-align the barrier count of the two groups
+  wait_vm<0>();        // the clamped tail items are still landing
+
+  // ---- epilogue: lane holds C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3
+  const int g = lane >> 4, i16 = lane & 15;
+  unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 64 + 4 * g;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      unsigned short* p = Cb + (long)(16 * i) * args.ldc + 16 * j;
+      f32x4_t v = acc[i][j];
+      if constexpr (EPI == EPI_ACC) {
+        const s2_t old = *reinterpret_cast<const s2_t*>(p);
+        v[0] += bf2f(old[0] & 0xffff);
+        v[1] += bf2f(old[0] >> 16);
+        v[2] += bf2f(old[1] & 0xffff);
+        v[3] += bf2f(old[1] >> 16);
+      }
+      s2_t o;
+      o[0] = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+      o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      *reinterpret_cast<s2_t*>(p) = o;
+    }
+  }
+}
+
+template <bool AT, bool BT, int EPI, int GROUP>
+void launch_g(const G64Args& g, int variant) {
+  const dim3 grid(g.tiles_m * g.tiles_n), block(NTHR);
+  switch (variant) {
+    case 1: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g); break;
+    case 2: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 2>), grid, block, 0, stream(), g); break;
+    case 3: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 3>), grid, block, 0, stream(), g); break;
+    default: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 0>), grid, block, 0, stream(), g); break;
+  }
+}
+
+// config = group (tile-rows per tile-order group: 4 / 8) + 100 * schedule variant
+template <bool AT, bool BT, int EPI>
+void launch(const G64Args& g, int config) {
+  const int group = config % 100, variant = config / 100;
+  if (group == 8) launch_g<AT, BT, EPI, 8>(g, variant);
+  else launch_g<AT, BT, EPI, 4>(g, variant);
+}
+
+}  // namespace
+
+bool gemm64_supported(long M, long N, long K) { return M % TM == 0 && N % TN == 0 && K % (2 * TK) == 0 && K > 0; }
+
+// out[M,N] (+)= A·B^T, operand storage by at / bt; M, N multiples of 256, K of 128.
+void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool at_, bool bt_, bool accumulate,
+               int64_t config) {
+  LLMCTL_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm64_ex: 2-D operands");
+  LLMCTL_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+                   out.scalar_type() == at::kBFloat16, "gemm64_ex: bf16 operands");
+  LLMCTL_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm64_ex: GPU tensors");
+  LLMCTL_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1, "gemm64_ex: unit inner stride");
+  const long M = at_ ? a.size(1) : a.size(0);
+  const long K = at_ ? a.size(0) : a.size(1);
+  const long N = bt_ ? b.size(1) : b.size(0);
+  const long Kb = bt_ ? b.size(0) : b.size(1);
+  LLMCTL_CHECK(K == Kb, "gemm64_ex: K mismatch (", K, " vs ", Kb, ")");
+  LLMCTL_CHECK(out.size(0) == M && out.size(1) == N, "gemm64_ex: out must be [M,N]");
+  LLMCTL_CHECK(gemm64_supported(M, N, K), "gemm64_ex: M,N multiples of 256, K of 128 (got ", M, "x", N, "x", K, ")");
+  LLMCTL_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(out.data_ptr()) & 7) == 0,
+               "gemm64_ex: 16-byte aligned operand rows");
+  // 32-bit buffer offsets: the farthest byte any tile's DMA addresses from its tile origin
+  const long a_span = at_ ? K * a.stride(0) * 2 : (long)TM * a.stride(0) * 2;
+  const long b_span = bt_ ? K * b.stride(0) * 2 : (long)TN * b.stride(0) * 2;
+  LLMCTL_CHECK(a_span < (1L << 31) && b_span < (1L << 31), "gemm64_ex: operand too large for 32-bit offsets");
+  const c10::DeviceGuard dg(a.device());
+  G64Args g{reinterpret_cast<const unsigned short*>(a.data_ptr()), reinterpret_cast<const unsigned short*>(b.data_ptr()),
+            reinterpret_cast<unsigned short*>(out.data_ptr()), a.stride(0), b.stride(0), out.stride(0),
+            (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN)};
+  const int grp = (int)config;
+  const int sel = (at_ ? 4 : 0) | (bt_ ? 2 : 0) | (accumulate ? 1 : 0);
+  switch (sel) {
+    case 0: launch<false, false, EPI_STORE>(g, grp); break;
+    case 1: launch<false, false, EPI_ACC>(g, grp); break;
+    case 2: launch<false, true, EPI_STORE>(g, grp); break;
+    case 3: launch<false, true, EPI_ACC>(g, grp); break;
+    case 4: launch<true, false, EPI_STORE>(g, grp); break;
+    case 5: launch<true, false, EPI_ACC>(g, grp); break;
+    case 6: launch<true, true, EPI_STORE>(g, grp); break;
+    default: launch<true, true, EPI_ACC>(g, grp); break;
+  }
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("gemm64_ex", &gemm64_ex); }
+
+}  // namespace llmctl

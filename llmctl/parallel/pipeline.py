@@ -24,6 +24,18 @@ import torch
 import torch.distributed as dist
 
 
+@torch.no_grad()
+def broadcast_tied_embedding(model, pg) -> None:
+    """Copy stage 0's ``embed`` into the last stage's ``lm_head`` (tied word embeddings).
+    Must run before the optimizer is built: ``FlatAdamW`` snapshots the fp32 master weights
+    from the parameters at construction, and the first update writes ``param = master``."""
+    if pg.layout.pp <= 1 or pg.embed_group is None:
+        return
+    p = model.embed if pg.pp_rank == 0 else (model.lm_head if pg.pp_rank == pg.layout.pp - 1 else None)
+    if p is not None:
+        dist.broadcast(p.data, src=pg.pp_ranks[0], group=pg.embed_group)
+
+
 class PipelineSchedule:
     def __init__(self, engine, num_microbatches: int):
         self.e = engine
@@ -35,25 +47,18 @@ class PipelineSchedule:
         self.prev = self.ranks[self.s - 1] if self.s > 0 else None
         self.next = self.ranks[self.s + 1] if self.s < self.P - 1 else None
         # tied word embeddings: stage 0 owns ``embed``, stage P-1 an ``lm_head`` copy.  The copy
-        # starts equal (broadcast below) and stays equal because both receive the SUM of the
-        # two stages' gradients (``sync_tied_grads``) before identical optimizer updates.
+        # starts equal (``broadcast_tied_embedding``, called by the engine BEFORE the optimizer
+        # snapshots its fp32 master weights) and stays equal because both receive the SUM of
+        # the two stages' gradients (``sync_tied_grads``) before identical optimizer updates.
         self.tied = bool(engine.model_config.tie_word_embeddings and self.P > 1)
-        if self.tied:
-            self._broadcast_tied()
-            if self.is_last:
-                engine.optimizer.norm_exclude.append(self._tied_grad)
+        if self.tied and self.is_last:
+            engine.optimizer.norm_exclude.append(self._tied_grad)
         self.last_loss: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ tied embeddings
     def _tied_param(self):
         m = self.e.model
         return m.embed if self.is_first else (m.lm_head if self.is_last else None)
-
-    @torch.no_grad()
-    def _broadcast_tied(self):
-        p = self._tied_param()
-        if p is not None:
-            dist.broadcast(p.data, src=self.ranks[0], group=self.e.pg.embed_group)
 
     def _tied_grad(self) -> Optional[torch.Tensor]:
         """The DP-reduced gradient of the tied copy this rank holds: the whole ``p.grad`` under

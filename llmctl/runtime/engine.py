@@ -176,6 +176,9 @@ class TrainingEngine:
         from llmctl.partition.shard_map import split_layers
 
         lo, hi = split_layers(L, pp)[pp_rank]
+        if mc.is_moe and pp > 1:
+            # the pipeline stages compute only the LM loss: the router aux loss would be dropped
+            raise NotImplementedError("MoE models with pipeline parallelism are not supported")
         pc = ParallelContext(
             tp_group=pg.tp_group, tp_size=pg.layout.tp, tp_rank=pg.tp_rank,
             sequence_parallel=c.sequence_parallel and pg.layout.tp > 1,
@@ -193,6 +196,10 @@ class TrainingEngine:
         bucket_numel = int(c.bucket_mb * 2**20 / torch.tensor([], dtype=c.dtype).element_size())
         self.grad_sink = None
         if c.zero_stage >= 3 and dp > 1:
+            if pp > 1 and mc.tie_word_embeddings:
+                # the tied copy would need its ZeRO-3 unit gathered for the broadcast and its
+                # grad reduced from the unit's flat shard: not implemented, so refuse loudly
+                raise NotImplementedError("ZeRO-3 with pipeline parallelism and tied word embeddings is not supported")
             from llmctl.parallel.zero import Zero3Model
 
             self.zero3 = Zero3Model(self.model, dp_group=pg.dpcp_group, dtype=c.dtype)
@@ -211,6 +218,10 @@ class TrainingEngine:
             leafs = ("wqkv", "wo", "w_up", "w_down") + (() if tied else ("lm_head",))
             self.grad_sink = GradSink()
             self.flat.install_sinks(self.grad_sink, lambda n, p: n.split(".")[-1] in leafs)
+        if pp > 1 and mc.tie_word_embeddings:
+            from llmctl.parallel.pipeline import broadcast_tied_embedding
+
+            broadcast_tied_embedding(self.model, pg)  # before FlatAdamW snapshots the masters
         norm_group = pg.pp_group if pp > 1 else None
         self.optimizer = FlatAdamW(self.flat, lr=c.learning_rate, betas=tuple(c.betas), eps=c.eps,
                                    weight_decay=c.weight_decay, max_grad_norm=c.gradient_clipping,
@@ -294,14 +305,18 @@ class TrainingEngine:
         self.optimizer.wait_params()  # every bucket's update has been ordered before this point
         self.flat.zero_grad()
 
-    def _forward_backward(self, input_ids, labels, denom, before_backward=None):
-        doc_start = None
-        if self.config.pack_sequences:
-            from llmctl.ops.ref import document_starts
+    def _packing(self, input_ids, labels):
+        """Packed sequences: the per-row document map and the labels with separator targets
+        masked (a separator's next-token label belongs to the next document)."""
+        if not self.config.pack_sequences:
+            return labels, None
+        from llmctl.ops.ref import document_starts
 
-            doc_start = document_starts(input_ids, self.config.doc_separator)
-            # a separator's next-token label belongs to the next document: not a target
-            labels = labels.masked_fill(input_ids == self.config.doc_separator, -100)
+        doc_start = document_starts(input_ids, self.config.doc_separator)
+        return labels.masked_fill(input_ids == self.config.doc_separator, -100), doc_start
+
+    def _forward_backward(self, input_ids, labels, denom, before_backward=None):
+        labels, doc_start = self._packing(input_ids, labels)
         loss = self.model(input_ids, labels, loss_denom=denom, doc_start=doc_start)
         if self.faults and self.faults.nan_loss(self.global_step + 1):
             loss = loss * float("nan")
@@ -356,8 +371,8 @@ class TrainingEngine:
             self.esync.finish()
         if self.pipeline is not None:
             self.pipeline.sync_tied_grads()
+        lr = self.scheduler(self.global_step)  # 0-based index of the step being applied (HF)
         self.global_step += 1
-        lr = self.scheduler(self.global_step)
         if self.eopt is not None:
             # one global clip norm: the expert shards are distinct across the EP group
             enorm = self.eopt.grad_norm_sq().clone()
@@ -394,7 +409,8 @@ class TrainingEngine:
             if self.pipeline is not None:
                 l = self.pipeline.eval_loss(x, y, denom)
             else:
-                l = self.model(x, y, loss_denom=denom)
+                y, doc_start = self._packing(x, y)
+                l = self.model(x, y, loss_denom=denom, doc_start=doc_start)
                 if cpn > 1:  # partial sums of one mean
                     l = l.detach().float().reshape(1).clone()
                     dist.all_reduce(l, group=self.pg.cp_group)

@@ -45,15 +45,21 @@ class _StreamEvent:
 
 class LRSchedule:
     """``constant`` | ``linear`` (reference default, engine.py:246-253) | ``cosine``
-    (declared by reference configs but unsupported there)."""
+    (declared by reference configs but unsupported there).
+
+    ``step`` is the 0-based index of the optimizer step being applied, as in HF's
+    ``get_linear_schedule_with_warmup`` (which the reference uses): warmup ramps
+    ``step / warmup`` (0 on the very first step when warmup > 0), the first post-warmup step
+    runs at the base LR, and the last step of a ``total``-step linear schedule runs at
+    ``base / (total - warmup)`` — never 0."""
 
     def __init__(self, base_lr: float, kind: str = "cosine", warmup_steps: int = 0, total_steps: int = 0,
                  min_lr_ratio: float = 0.1):
         self.base_lr, self.kind = base_lr, kind
         self.warmup, self.total, self.min_ratio = warmup_steps, max(total_steps, 1), min_lr_ratio
 
-    def __call__(self, step: int) -> float:  # step is 1-based
-        if self.warmup and step <= self.warmup:
+    def __call__(self, step: int) -> float:  # step: 0-based index of the step being applied
+        if self.warmup and step < self.warmup:
             return self.base_lr * step / self.warmup
         if self.kind == "constant":
             return self.base_lr

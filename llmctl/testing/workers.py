@@ -206,13 +206,13 @@ def _layout_config(layout: dict, model: str = "tiny"):
                    async_checkpoint=False)
 
 
-def ckpt_save_phase(rank: int, world: int, layout: dict, steps: int, out_dir: str) -> dict:
+def ckpt_save_phase(rank: int, world: int, layout: dict, steps: int, out_dir: str, model: str = "tiny") -> dict:
     """Train ``steps`` steps under ``layout`` from the reference init, then checkpoint."""
     from llmctl.io.checkpoint import CheckpointManager
     from llmctl.runtime.engine import TrainingEngine
 
-    eng = TrainingEngine(_layout_config(layout))
-    eng.load_full_state_dict(reference_state("tiny"))
+    eng = TrainingEngine(_layout_config(layout, model))
+    eng.load_full_state_dict(reference_state(model))
     vocab, cfg = eng.model_config.vocab_size, eng.config
     for s in range(steps):
         eng.train_step([make_batch(vocab, cfg.seq_len, cfg.batch_size, s, eng.pg.dp_rank, 0)])
@@ -222,12 +222,13 @@ def ckpt_save_phase(rank: int, world: int, layout: dict, steps: int, out_dir: st
     return {}
 
 
-def ckpt_resume_phase(rank: int, world: int, layout: dict, start: int, steps: int, out_dir: str) -> dict:
+def ckpt_resume_phase(rank: int, world: int, layout: dict, start: int, steps: int, out_dir: str,
+                      model: str = "tiny") -> dict:
     """Resume the checkpoint under a (possibly different) ``layout`` and train more steps."""
     from llmctl.io.checkpoint import CheckpointManager
     from llmctl.runtime.engine import TrainingEngine
 
-    eng = TrainingEngine(_layout_config(layout))
+    eng = TrainingEngine(_layout_config(layout, model))
     CheckpointManager(eng, out_dir).load(out_dir + "/ckpt")
     vocab, cfg = eng.model_config.vocab_size, eng.config
     assert eng.global_step == start and eng.optimizer.step_count == start
@@ -237,7 +238,7 @@ def ckpt_resume_phase(rank: int, world: int, layout: dict, start: int, steps: in
     return {"state": full if rank == 0 else None}
 
 
-def train_reference_schedule(schedule) -> dict:
+def train_reference_schedule(schedule, model: str = "tiny") -> dict:
     """Single process; ``schedule[s]`` = number of DP ranks whose micro-batches form step s."""
     import os
 
@@ -245,12 +246,37 @@ def train_reference_schedule(schedule) -> dict:
 
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         os.environ.pop(k, None)
-    eng = TrainingEngine(_config(model_name_or_path="tiny"))
-    eng.load_full_state_dict(reference_state("tiny"))
+    eng = TrainingEngine(_config(model_name_or_path=model))
+    eng.load_full_state_dict(reference_state(model))
     vocab, cfg = eng.model_config.vocab_size, eng.config
     for s, dp in enumerate(schedule):
         eng.train_step([make_batch(vocab, cfg.seq_len, cfg.batch_size, s, r, 0) for r in range(dp)])
     return {"state": eng.gather_full_state_dict()}
+
+
+def pp_tied_fresh(rank: int, world: int, steps: int = 2) -> dict:
+    """PP=world tied-embedding model from its OWN init (no load_full_state_dict): return the
+    first stage's ``embed`` and the last stage's ``lm_head`` after ``steps`` updates."""
+    from llmctl.runtime.engine import TrainingEngine
+
+    eng = TrainingEngine(_config(model_name_or_path="tiny-tied", pipeline_parallel=world, num_microbatches=2))
+    vocab, cfg = eng.model_config.vocab_size, eng.config
+    for s in range(steps):
+        eng.train_step([make_batch(vocab, cfg.seq_len, cfg.batch_size, s, 0, i) for i in range(2)])
+    m = eng.model
+    t = m.embed if eng.pipeline.is_first else (m.lm_head if eng.pipeline.is_last else None)
+    return {"tied": t.detach().clone() if t is not None else None}
+
+
+def zero3_pp_tied_error(rank: int, world: int) -> dict:
+    """ZeRO-3 x PP x tied embeddings must be refused, not silently untied."""
+    from llmctl.runtime.engine import TrainingEngine
+
+    try:
+        TrainingEngine(_config(model_name_or_path="tiny-tied", pipeline_parallel=2, zero_stage=3))
+    except NotImplementedError as e:
+        return {"error": str(e)}
+    return {"error": ""}
 
 
 def ring_attention_check(rank: int, world: int, B: int = 2, S: int = 48, Hq: int = 4, Hkv: int = 2,

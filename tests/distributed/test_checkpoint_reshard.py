@@ -29,3 +29,12 @@ def test_resume_across_layouts(tmp_path, src, dst):
     dp = lambda L: 2 // (L.get("tp", 1) * L.get("pp", 1))  # noqa: E731
     ref = train_reference_schedule([dp(src), dp(src), dp(dst)])
     _close(out[0]["state"], ref["state"])
+
+
+def test_resume_tied_pp1_checkpoint_under_pp2(tmp_path):
+    """A tied model saved under PP=1 (only ``embed`` on disk) resumes under PP=2: the last
+    stage's lm_head copy and its optimizer state come from ``embed``."""
+    run_ranks(ckpt_save_phase, 2, {"tp": 1, "zero": 1}, 2, str(tmp_path), "tiny-tied")
+    out = run_ranks(ckpt_resume_phase, 2, {"tp": 1, "pp": 2, "microbatches": 1}, 2, 1, str(tmp_path), "tiny-tied")
+    ref = train_reference_schedule([2, 2, 1], model="tiny-tied")
+    _close(out[0]["state"], ref["state"])

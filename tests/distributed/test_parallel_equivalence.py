@@ -4,7 +4,7 @@ import pytest
 import torch
 
 from llmctl.testing.harness import run_ranks
-from llmctl.testing.workers import train_layout, train_reference
+from llmctl.testing.workers import pp_tied_fresh, train_layout, train_reference, zero3_pp_tied_error
 
 STEPS = 3
 
@@ -100,6 +100,18 @@ def test_pp2_tied_embeddings_matches_single():
     _close(out[0]["state"], ref["state"])
 
 
+def test_pp2_tied_fresh_init_stays_tied():
+    """From the engine's own init (no load_full_state_dict re-seeding the fp32 masters), the
+    last stage's lm_head copy equals stage 0's embed after optimizer steps."""
+    out = run_ranks(pp_tied_fresh, 2, 2)
+    assert torch.equal(out[0]["tied"], out[1]["tied"])
+
+
+def test_zero3_pp_tied_rejected():
+    out = run_ranks(zero3_pp_tied_error, 4)
+    assert all("ZeRO-3" in o["error"] for o in out), out
+
+
 @pytest.mark.parametrize("zero", [0, 1, 2])
 def test_pp2_tied_dp2_matches_single(zero):
     ref = train_reference(STEPS, dp=2, model="tiny-tied", micro_per_rank=4)
@@ -121,6 +133,7 @@ def test_pp2_packed_sequences_matches_single():
     ref = train_reference(STEPS, dp=1, micro_per_rank=4, pack=True)
     out = run_ranks(train_layout, 2, STEPS, {"pp": 2, "microbatches": 4, "pack": True})
     _losses_close(out[0]["losses"], ref["losses"])
+    _losses_close([out[0]["eval"]], [ref["eval"]])
     _close(out[0]["state"], ref["state"])
 
 
@@ -133,6 +146,7 @@ def test_zero3_dp2_matches_single(ref_dp2):
 def test_zero3_pp2_dp2_matches_single(ref_dp2_m4):
     out = run_ranks(train_layout, 4, STEPS, {"zero": 3, "pp": 2, "microbatches": 4})
     _losses_close(out[0]["losses"], ref_dp2_m4["losses"])
+    _losses_close([out[0]["eval"]], [ref_dp2_m4["eval"]])  # gathered root unit on both stages
     _close(out[0]["state"], ref_dp2_m4["state"])
 
 

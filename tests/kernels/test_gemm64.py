@@ -1,0 +1,105 @@
+"""gemm64_ex (llmctl/ops/csrc/gemm64.hip) vs an fp32 PyTorch reference, every operand layout,
+store and accumulate epilogues, every schedule variant; checked per ROW (max error of the row
+over the row's max magnitude), so one wrong 16x16 tile fails the test even when a Frobenius
+norm over the whole output would hide it (the self-check below proves that)."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _bf(*shape, seed=0):
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    return torch.randn(*shape, generator=g, device=DEV).to(torch.bfloat16)
+
+
+def row_err(got: torch.Tensor, want: torch.Tensor) -> float:
+    d = (got.float() - want.float()).abs().amax(dim=1)
+    s = want.float().abs().amax(dim=1).clamp_min(1e-6)
+    return (d / s).max().item()
+
+
+TOL = 1.2e-2  # bf16 output rounding is <= 2^-8 of the row max; fp32 accumulation order adds ~1e-5
+
+
+def test_row_check_catches_one_bad_tile():
+    """Self-check of the oracle: a single corrupted 16x16 tile in a 2048x2048 output passes a
+    Frobenius-norm criterion (< 8e-3) but fails the per-row criterion."""
+    want = torch.randn(2048, 2048, generator=torch.Generator().manual_seed(1))
+    got = want.clone()
+    got[256:272, 512:528] += 0.15 * want.abs().amax()  # one tile off by 15 % of the range
+    frob = ((got - want).norm() / want.norm()).item()
+    assert frob < 8e-3
+    assert row_err(got, want) > 0.1
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (768, 512, 1024), (2304, 1280, 256)])
+@pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_gemm64_ex(native_lib, M, N, K, at, bt, acc):
+    A = _bf(M, K, seed=71)
+    B = _bf(N, K, seed=72)
+    a = A.t().contiguous() if at else A
+    b = B.t().contiguous() if bt else B
+    c0 = _bf(M, N, seed=73)
+    out = c0.clone() if acc else torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    native_lib.gemm64_ex(a, b, out, at, bt, acc, 104)
+    want = A.float() @ B.float().t() + (c0.float() if acc else 0.0)
+    assert torch.isfinite(out.float()).all()
+    assert row_err(out, want) < TOL
+
+
+@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304])
+def test_gemm64_configs(native_lib, config):
+    """Every tile-order group / schedule variant computes the same product (fwd and wgrad)."""
+    M, N, K = 1536, 1024, 2048  # 24 tiles: more tiles than one group, several K-tile pairs
+    A, B = _bf(M, K, seed=3), _bf(N, K, seed=4)
+    want = A.float() @ B.float().t()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    native_lib.gemm64_ex(A, B, out, False, False, False, config)
+    assert row_err(out, want) < TOL
+    native_lib.gemm64_ex(A.t().contiguous(), B.t().contiguous(), out, True, True, False, config)
+    assert row_err(out, want) < TOL
+
+
+def test_gemm64_strided_views(native_lib):
+    """Row-strided operand / output views (flat-buffer gradient views, column slices)."""
+    big = _bf(1024, 640, seed=81)
+    a = big[:, 64:576]           # K-major A [K=1024][M=512], row stride 640
+    b = _bf(1024, 512, seed=82)  # K-major B [K=1024][N=512]
+    out_buf = torch.zeros(512, 768, device=DEV, dtype=torch.bfloat16)
+    out = out_buf[:, 256:768]
+    native_lib.gemm64_ex(a, b, out, True, True, False, 104)
+    assert row_err(out, a.float().t() @ b.float()) < TOL
+    assert (out_buf[:, :256] == 0).all()
+
+
+def test_gemm64_rejects_bad_shapes(native_lib):
+    a, b = _bf(256, 96, seed=1), _bf(256, 96, seed=2)
+    out = torch.empty(256, 256, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="multiples"):
+        native_lib.gemm64_ex(a, b, out, False, False, False, 104)
+
+
+def test_linear_backward_on_gemm64(native_lib):
+    """exec.linear routes dgrad (no W^T copy) and wgrad (into the sink's flat view) through
+    gemm64 at eligible shapes; both match the fp32 reference."""
+    from llmctl.exec.linear import GradSink, dgrad64_ok, linear
+
+    T, inn, out = 512, 768, 1024
+    x = _bf(T, inn, seed=5).requires_grad_(True)
+    w = torch.nn.Parameter(_bf(out, inn, seed=6))
+    w.grad = torch.zeros_like(w)
+    sink = GradSink()
+    sink.attach(w)
+    y = linear(x, w)
+    assert getattr(w, "_llmctl_wt", None) is None  # gemm64 dgrad: no transposed copy kept
+    dy = _bf(T, out, seed=7)
+    assert dgrad64_ok(dy, w)
+    y.backward(dy)
+    assert row_err(x.grad, dy.float() @ w.detach().float()) < TOL
+    assert row_err(w.grad, dy.float().t() @ x.detach().float()) < TOL

@@ -45,6 +45,42 @@ def test_lr_schedules():
     assert LRSchedule(3e-4, "constant")(1000) == 3e-4
 
 
+def test_lr_schedule_matches_hf_linear():
+    """0-based step index, as HF get_linear_schedule_with_warmup (the reference's scheduler,
+    llmctl/runtime/engine.py:246-253): no warmup -> step 0 runs at the base LR; the last of
+    ``total`` steps runs at base/(total-warmup) > 0; warmup ramps step/warmup."""
+    from llmctl.runtime.optimizer import LRSchedule
+
+    def hf(step, warmup, total):  # transformers.optimization._get_linear_schedule_with_warmup_lr_lambda
+        if step < warmup:
+            return step / max(1, warmup)
+        return max(0.0, (total - step) / max(1, total - warmup))
+
+    for warmup, total in ((0, 5), (3, 12), (10, 110)):
+        s = LRSchedule(1.0, "linear", warmup_steps=warmup, total_steps=total)
+        for step in range(total):
+            assert s(step) == pytest.approx(hf(step, warmup, total)), (warmup, total, step)
+        assert s(total - 1) > 0
+    assert LRSchedule(2.0, "linear", warmup_steps=0, total_steps=4)(0) == 2.0
+
+
+def test_engine_lr_first_and_last_step():
+    """The engine applies scheduler(i) on its i-th (0-based) step: a 4-step linear run with
+    warmup 0 uses the base LR first and a positive LR last."""
+    import torch
+
+    from llmctl.models import get_model_config
+    from llmctl.runtime.engine import TrainingConfig, TrainingEngine
+
+    cfg = TrainingConfig(model_name_or_path="tiny", batch_size=2, seq_len=16, device="cpu", log_level="warning",
+                         learning_rate=1e-3, max_steps=4, warmup_steps=0, scheduler="linear")
+    eng = TrainingEngine(cfg, get_model_config("tiny"))
+    ids = torch.randint(0, eng.model_config.vocab_size, (2, 17))
+    lrs = [float(eng.train_step([(ids[:, :-1], ids[:, 1:])])["lr"]) for _ in range(4)]
+    eng.shutdown()
+    assert lrs[0] == pytest.approx(1e-3) and lrs[-1] == pytest.approx(2.5e-4), lrs
+
+
 # ---------------------------------------------------------------- data loader
 @pytest.fixture()
 def token_file(tmp_path):
