@@ -107,6 +107,30 @@ class KVManager {
     return true;
   }
 
+  // new sequence of `tokens` tokens whose first blocks are the (already cached, shared) `prefix`
+  // blocks: each gets one more reference, the rest are allocated; false (nothing changed) if OOM
+  bool add_sequence_shared(int64_t seq, int64_t tokens, const std::vector<int64_t>& prefix) {
+    if (tables_.count(seq)) throw std::runtime_error("sequence already registered");
+    const int64_t need = blocks_needed(std::max<int64_t>(tokens, 1));
+    if ((int64_t)prefix.size() > need) throw std::invalid_argument("prefix longer than the sequence");
+    const int64_t fresh = need - (int64_t)prefix.size();
+    if (fresh > alloc_.num_free()) return false;
+    Table t;
+    t.tokens = tokens;
+    for (auto b : prefix) {
+      alloc_.incref(b);
+      t.blocks.push_back(b);
+    }
+    for (int64_t i = 0; i < fresh; ++i) t.blocks.push_back(alloc_.allocate());
+    tables_[seq] = std::move(t);
+    return true;
+  }
+
+  // a reference held outside any sequence (the prefix cache); decref returns true when freed
+  void incref_block(int64_t b) { alloc_.incref(b); }
+  bool decref_block(int64_t b) { return alloc_.free(b); }
+  int32_t refcount(int64_t b) const { return alloc_.refcount(b); }
+
   // make room for one more token; returns its flat slot (block*bs + offset) or -1 if OOM
   int64_t append_token(int64_t seq) {
     auto& t = get(seq);
@@ -415,6 +439,10 @@ PYBIND11_MODULE(_llmctl_native, m) {
       .def("append_token", &KVManager::append_token)
       .def("slot", &KVManager::slot)
       .def("fork", &KVManager::fork)
+      .def("add_sequence_shared", &KVManager::add_sequence_shared)
+      .def("incref_block", &KVManager::incref_block)
+      .def("decref_block", &KVManager::decref_block)
+      .def("refcount", &KVManager::refcount)
       .def("free_sequence", &KVManager::free_sequence)
       .def("num_tokens", &KVManager::num_tokens)
       .def("block_table", &KVManager::block_table)

@@ -13,7 +13,7 @@ copies are needed between kernels:
 from __future__ import annotations
 
 import os
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -334,6 +334,31 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scal
     return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale)
 
 
+def prefill_work_list(cu_q, q_block: int = 128) -> List[int]:
+    """(sequence << 16) | q-block items for ``paged_prefill_attention``, heaviest (longest
+    causal span: the last q-blocks of long chunks) first."""
+    items = []
+    for n in range(len(cu_q) - 1):
+        qlen = int(cu_q[n + 1]) - int(cu_q[n])
+        for b in range((qlen + q_block - 1) // q_block):
+            items.append((b * q_block, (n << 16) | b))
+    items.sort(key=lambda t: -t[0])
+    return [w for _, w in items]
+
+
+def paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale: Optional[float] = None,
+                            work=None):
+    """Chunked / prefix-reusing prefill attention over the paged KV cache (see
+    ``csrc/paged_prefill.hip``).  ``cu_q`` / ``ctx_lens`` / ``block_tables`` int32; ``work``
+    (optional) is the precomputed :func:`prefill_work_list` as an int32 tensor."""
+    scale = scale if scale is not None else q.shape[-1] ** -0.5
+    if use_native(q):
+        if work is None:
+            work = torch.tensor(prefill_work_list(cu_q.tolist()), dtype=torch.int32, device=q.device)
+        return native().paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, work, scale)
+    return ref.paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale)
+
+
 def decode_linear(x, w, b=None):
     """``x @ w^T (+ b)`` for decode-shaped inputs: the weight-streaming MFMA kernel
     (``csrc/skinny_gemm.hip``) for the NARROW projections (out features <= 4096: o-proj,
@@ -360,5 +385,5 @@ __all__ = [
     "transpose_",
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample", "decode_linear", "rope_qkv_cache",
+    "sample", "decode_linear", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list",
 ]

@@ -212,6 +212,32 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scal
     return out
 
 
+def paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale: float):
+    """Packed new tokens q [T, Hq, D] of N sequences (rows cu_q[n]:cu_q[n+1]) attending, causally,
+    every cached key of their sequence: after the chunk's cache write sequence n holds
+    ctx_lens[n] tokens and its new tokens sit at positions ctx - qlen .. ctx - 1."""
+    T, Hq, D = q.shape
+    bs, Hkv = k_cache.shape[1], k_cache.shape[2]
+    rep = Hq // Hkv
+    out = torch.empty_like(q)
+    cu = [int(x) for x in cu_q]
+    for n in range(len(cu) - 1):
+        q0, q1 = cu[n], cu[n + 1]
+        qlen, L = q1 - q0, int(ctx_lens[n])
+        if qlen == 0:
+            continue
+        nb = (L + bs - 1) // bs
+        blocks = block_tables[n, :nb].long()
+        kk = k_cache[blocks].reshape(nb * bs, Hkv, D)[:L].float().repeat_interleave(rep, dim=1)
+        vv = v_cache[blocks].reshape(nb * bs, Hkv, D)[:L].float().repeat_interleave(rep, dim=1)
+        s = torch.einsum("qhd,lhd->hql", q[q0:q1].float(), kk) * scale
+        pos = torch.arange(L - qlen, L, device=q.device).view(1, qlen, 1)
+        keys = torch.arange(L, device=q.device).view(1, 1, L)
+        s = s.masked_fill(keys > pos, float("-inf"))
+        out[q0:q1] = torch.einsum("hql,lhd->qhd", torch.softmax(s, dim=-1), vv).to(q.dtype)
+    return out
+
+
 def kv_cache_write(k, v, k_cache, v_cache, slot_mapping):
     """k/v [N, Hkv, D] written at flat slots (block*block_size + offset) of the caches."""
     nb, bs = k_cache.shape[:2]

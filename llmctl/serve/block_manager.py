@@ -46,6 +46,35 @@ class PyKVManager:
         self.tokens[seq] = tokens
         return True
 
+    def add_sequence_shared(self, seq: int, tokens: int, prefix: List[int]) -> bool:
+        need = self.blocks_needed(max(tokens, 1))
+        if len(prefix) > need:
+            raise ValueError("prefix longer than the sequence")
+        if need - len(prefix) > len(self.free_list):
+            return False
+        for b in prefix:
+            self.incref_block(b)
+        self.tables[seq] = list(prefix) + [self._alloc() for _ in range(need - len(prefix))]
+        self.tokens[seq] = tokens
+        return True
+
+    def incref_block(self, b: int) -> None:
+        if self.ref[b] <= 0:
+            raise RuntimeError("incref of a free block")
+        self.ref[b] += 1
+
+    def decref_block(self, b: int) -> bool:
+        if self.ref[b] <= 0:
+            raise RuntimeError(f"double free of KV block {b}")
+        self.ref[b] -= 1
+        if self.ref[b] == 0:
+            self.free_list.append(b)
+            return True
+        return False
+
+    def refcount(self, b: int) -> int:
+        return self.ref[b]
+
     def append_token(self, seq: int) -> int:
         t = self.tables[seq]
         pos = self.tokens[seq]
@@ -68,9 +97,7 @@ class PyKVManager:
 
     def free_sequence(self, seq: int) -> None:
         for b in self.tables.pop(seq, []):
-            self.ref[b] -= 1
-            if self.ref[b] == 0:
-                self.free_list.append(b)
+            self.decref_block(b)
         self.tokens.pop(seq, None)
 
     def num_tokens(self, seq: int) -> int:

@@ -6,10 +6,13 @@ every generated token with ``use_cache=True`` but discarded the cache, right-pad
 batches and read the logits of the padded last position (wrong tokens for shorter
 prompts), and sampled with a host sync per request per token.  Here:
 
-* prefill: prompts are right-padded into one ``[B, S]`` batch (causal attention makes the
-  padding invisible to real tokens) through the flash-attention kernel; K/V of the real
-  tokens are scattered into the paged cache by ``kv_cache_write``; logits are taken at
-  each sequence's own last position;
+* prefill (round 2): CHUNKED and prefix-aware.  The scheduler hands out chunks (sequence,
+  first position, count) under a per-step token budget; the chunks of all sequences are packed
+  back to back (no padding), RoPE'd and written into the paged cache in one fused pass, and
+  attend through ``paged_prefill_attention`` (csrc/paged_prefill.hip): every query reads its
+  keys from the block table, so a cached prefix (earlier chunk, prefix-cache hit, resumed
+  sequence) and the chunk itself are one key range.  Logits are taken only at the last token
+  of chunks that complete a sequence's known tokens;
 * decode: one token per running sequence; per layer ``rope_qkv`` (explicit positions) ->
   ``kv_cache_write`` -> ``paged_attention_decode`` (block tables, GQA) -> o-proj -> MLP;
   the whole decode step (embedding .. lm_head) is captured once per batch-size bucket in
@@ -34,7 +37,8 @@ from llmctl.io.artifact import load_model
 from llmctl.models import DecoderLM
 
 from .block_manager import PagedKVCache, make_kv_manager
-from .scheduler import ContinuousBatchScheduler, SamplingParams, Sequence
+from .prefix_cache import PrefixCache
+from .scheduler import ContinuousBatchScheduler, PrefillChunk, SamplingParams, Sequence
 from .tokenizer import load_tokenizer
 
 log = logging.getLogger("llmctl.serve")
@@ -44,7 +48,7 @@ class InferenceEngine:
     def __init__(self, model_path: str = "tiny", device: str = "auto", dtype=torch.bfloat16, max_batch_size: int = 8,
                  max_batch_tokens: int = 8192, max_model_len: Optional[int] = None, kv_cache_fraction: float = 0.85,
                  block_size: int = 16, num_kv_blocks: Optional[int] = None, scheduler: str = "dynamic",
-                 use_graphs: bool = True, seed: int = 0, pc=None):
+                 use_graphs: bool = True, seed: int = 0, pc=None, prefix_caching: bool = True):
         if device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -83,8 +87,9 @@ class InferenceEngine:
         self.kv_cache = PagedKVCache(cfg.layers, num_kv_blocks, block_size, cfg.kv_heads // self.tp, cfg.head_dim,
                                      dtype, self.device)
         self.kv = make_kv_manager(num_kv_blocks, block_size)
+        self.prefix_cache = PrefixCache(self.kv, block_size) if prefix_caching else None
         self.scheduler = ContinuousBatchScheduler(self.kv, max_batch_size, max_batch_tokens, self.max_model_len,
-                                                  scheduler, block_size)
+                                                  scheduler, block_size, prefix_cache=self.prefix_cache)
         self.max_batch_size = max_batch_size
         self.rope = self.model.rope_tables(self.max_model_len, self.device)
         # MoE routing sizes the expert segments on the host: decode runs eagerly
@@ -167,48 +172,59 @@ class InferenceEngine:
         return self._gather_vocab(ops.decode_linear(xn, m.head_weight()))
 
     # ------------------------------------------------------------------ prefill
-    def prefill_plan(self, seqs: List[Sequence]) -> Dict:
-        """Host-side description of a prefill step (what TP ranks receive from rank 0)."""
-        lens = [s.num_tokens for s in seqs]
-        B, S = len(seqs), max(lens)
-        ids = np.zeros((B, S), dtype=np.int64)
-        slots = np.full((B, S), -1, dtype=np.int64)
-        for i, s in enumerate(seqs):
-            toks = s.all_ids
-            ids[i, :len(toks)] = toks
-            slots[i, :len(toks)] = np.asarray(self.kv.slots(s.seq_id, 0, len(toks)), dtype=np.int64)
-        return {"op": "prefill", "ids": ids, "slots": slots, "lens": lens}
+    def prefill_plan(self, chunks: List[PrefillChunk]) -> Dict:
+        """Host-side description of a (chunked, packed) prefill step — what TP ranks receive."""
+        ids, pos, slots, cu, ctx, last = [], [], [], [0], [], []
+        for i, c in enumerate(chunks):
+            toks = c.seq.all_ids
+            ids.extend(toks[c.start:c.start + c.count])
+            pos.extend(range(c.start, c.start + c.count))
+            slots.append(np.asarray(self.kv.slots(c.seq.seq_id, c.start, c.count), dtype=np.int64))
+            cu.append(cu[-1] + c.count)
+            ctx.append(c.start + c.count)
+            if c.final:
+                last.append(cu[-1] - 1)
+        bt = np.asarray(self.kv.block_tables([c.seq.seq_id for c in chunks], self.max_blocks_per_seq))
+        return {"op": "prefill", "ids": np.asarray(ids, dtype=np.int64), "pos": np.asarray(pos, dtype=np.int32),
+                "slots": np.concatenate(slots) if slots else np.zeros(0, dtype=np.int64), "cu": cu, "ctx": ctx,
+                "bt": bt, "last": last, "work": ops.prefill_work_list(cu)}
 
     @torch.inference_mode()
-    def prefill(self, seqs: List[Sequence]) -> torch.Tensor:
-        """Run the prompts (all known tokens) of ``seqs``; returns last-position logits [n, V]."""
-        return self.prefill_exec(self.prefill_plan(seqs))
+    def prefill(self, chunks) -> torch.Tensor:
+        """Run prefill chunks (``PrefillChunk`` list, or sequences: whole prompts); returns the
+        logits [n_final, V] of the chunks that complete their sequence, in chunk order."""
+        if chunks and isinstance(chunks[0], Sequence):
+            chunks = [PrefillChunk(s, 0, s.num_tokens) for s in chunks]
+        return self.prefill_exec(self.prefill_plan(chunks))
 
     @torch.inference_mode()
     def prefill_exec(self, plan: Dict) -> torch.Tensor:
-        lens = plan["lens"]
-        B, S = plan["ids"].shape
-        ids = torch.from_numpy(plan["ids"]).to(self.device, non_blocking=True)
-        slots = torch.from_numpy(plan["slots"])
-        slots = slots.to(self.device, non_blocking=True).view(-1)
-        pos = torch.arange(S, device=self.device).repeat(B)
-        x = self._embed(ids.view(-1), pos)
+        d = self.device
+        T = len(plan["ids"])
+        ids = torch.from_numpy(plan["ids"]).to(d, non_blocking=True)
+        pos = torch.from_numpy(plan["pos"]).to(d, non_blocking=True)
+        slots = torch.from_numpy(plan["slots"]).to(d, non_blocking=True)
+        bt = torch.from_numpy(plan["bt"]).to(d, non_blocking=True)
+        cu = torch.tensor(plan["cu"], dtype=torch.int32).to(d, non_blocking=True)
+        ctx = torch.tensor(plan["ctx"], dtype=torch.int32).to(d, non_blocking=True)
+        work = torch.tensor(plan["work"], dtype=torch.int32).to(d, non_blocking=True)
+        x = self._embed(ids, pos.long())
         res = None
         kc, vc = self.kv_cache.k, self.kv_cache.v
         for li, layer in enumerate(self.model.layers):
             xn, res = self._norm(layer, x, res, "attn")
-            q, k, v = self._qkv(layer, xn, None, S, kc[li], vc[li], slots)
-            o = ops.flash_attention(q.view(B, S, layer.nq, layer.D), k.view(B, S, layer.nkv, layer.D),
-                                    v.view(B, S, layer.nkv, layer.D), causal=True)
-            a = self._reduce(ops.decode_linear(o.view(B * S, -1), layer.wo))
+            q, k, v = self._qkv(layer, xn, pos, self.max_model_len, kc[li], vc[li], slots)
+            o = ops.paged_prefill_attention(q.view(T, layer.nq, layer.D), kc[li], vc[li], bt, cu, ctx, work=work)
+            a = self._reduce(ops.decode_linear(o.view(T, -1), layer.wo))
             if layer.bo is not None:
                 a = a + layer.bo
             xn, res = self._norm(layer, a, res, "mlp")
             x = self._mlp(layer, xn)
-        last = torch.tensor([i * S + n - 1 for i, n in enumerate(lens)], device=self.device)
-        x_last, res_last = x.index_select(0, last), res.index_select(0, last)
-        self.stats["prefill_tokens"] += sum(lens)
-        return self._final(x_last, res_last)
+        self.stats["prefill_tokens"] += T
+        if not plan["last"]:
+            return torch.empty(0, self.cfg.vocab_size, device=d, dtype=x.dtype)
+        last = torch.tensor(plan["last"], device=d)
+        return self._final(x.index_select(0, last), res.index_select(0, last))
 
     # ------------------------------------------------------------------ decode
     def _decode_body(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
@@ -344,14 +360,20 @@ class InferenceEngine:
         if out.decode:
             logits = self.decode(out.decode)
             for seq, tok in zip(out.decode, self.sample(logits, out.decode)):
+                self.scheduler.computed(seq, 1)
                 self._append(seq, tok)
                 produced += 1
         if out.prefill:
-            # cap the padded prefill batch by the token budget (padding is real compute)
             logits = self.prefill(out.prefill)
-            for seq, tok in zip(out.prefill, self.sample(logits, out.prefill)):
-                self._append(seq, tok)
-                produced += 1
+            final = [c.seq for c in out.prefill if c.final]
+            for c in out.prefill:
+                self.scheduler.computed(c.seq, c.count)
+                self.stats["prefix_hit_tokens"] = self.stats.get("prefix_hit_tokens", 0) + (
+                    c.seq.cached_tokens if c.start == c.seq.cached_tokens else 0)
+            if final:
+                for seq, tok in zip(final, self.sample(logits, final)):
+                    self._append(seq, tok)
+                    produced += 1
         self.stats["steps"] += 1
         return produced
 

@@ -1,0 +1,96 @@
+"""Prefix cache: full KV blocks indexed by the token prefix they hold.
+
+The reference's ``KVCacheManager`` (``llmctl/serve/server.py:57-87``) stored per-request tensors
+that were never read back; every request (and every generated token) re-ran its whole prefix.
+Here a KV block becomes reusable once all of its ``block_size`` positions are computed: its key
+is a hash chained over the token ids of every block up to and including it, so two sequences
+share a block only if their whole prefixes match.  The cache holds ONE reference on every block
+it indexes (through the KV manager's ``incref_block``), so a finished or preempted sequence's
+blocks stay resident until space is needed; eviction is LRU over blocks that nothing but the
+cache still references.
+
+Used for (a) requests that share a system prompt / few-shot prefix and (b) sequences resumed
+after preemption, which re-attach their computed blocks instead of recomputing them.
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List, Sequence
+
+
+def _block_hash(parent: int, tokens: Sequence[int]) -> int:
+    return hash((parent, tuple(tokens)))
+
+
+class PrefixCache:
+    def __init__(self, kv, block_size: int):
+        self.kv = kv
+        self.bs = block_size
+        self._blocks: "OrderedDict[int, int]" = OrderedDict()  # chain hash -> block id (LRU order)
+        self._owner: Dict[int, int] = {}  # block id -> chain hash
+        self.stats = {"lookups": 0, "hit_tokens": 0, "inserted": 0, "evicted": 0}
+
+    def __len__(self) -> int:
+        return len(self._blocks)
+
+    def _hashes(self, ids: Sequence[int], nblocks: int) -> List[int]:
+        out, h = [], 0
+        for i in range(nblocks):
+            h = _block_hash(h, ids[i * self.bs:(i + 1) * self.bs])
+            out.append(h)
+        return out
+
+    def match(self, ids: Sequence[int]) -> List[int]:
+        """Block ids of the longest cached prefix of ``ids`` in whole blocks, leaving at least one
+        token of ``ids`` uncached (its logits are what the prefill must produce)."""
+        self.stats["lookups"] += 1
+        nfull = (len(ids) - 1) // self.bs
+        blocks: List[int] = []
+        for h in self._hashes(ids, nfull):
+            b = self._blocks.get(h)
+            if b is None:
+                break
+            self._blocks.move_to_end(h)
+            blocks.append(b)
+        self.stats["hit_tokens"] += len(blocks) * self.bs
+        return blocks
+
+    def insert(self, ids: Sequence[int], table: Sequence[int], num_computed: int) -> None:
+        """Index every fully computed block of a sequence (``ids`` its tokens, ``table`` its block
+        table, ``num_computed`` the positions whose K/V are in the cache)."""
+        nfull = min(num_computed // self.bs, len(table))
+        for i, h in enumerate(self._hashes(ids, nfull)):
+            b = table[i]
+            if h in self._blocks:
+                self._blocks.move_to_end(h)
+                continue
+            if b in self._owner:  # block already indexed under another chain (cannot happen
+                continue           # for blocks shared through match(); kept as a guard)
+            self.kv.incref_block(b)
+            self._blocks[h] = b
+            self._owner[b] = h
+            self.stats["inserted"] += 1
+
+    def evict(self, blocks_needed: int) -> int:
+        """Release LRU cached blocks that no sequence uses until ``blocks_needed`` free blocks
+        exist (or nothing evictable is left); returns how many blocks were freed."""
+        freed = 0
+        for h in list(self._blocks):
+            if self.kv.num_free_blocks >= blocks_needed:
+                break
+            b = self._blocks[h]
+            if self.kv.refcount(b) > 1:  # still part of a live sequence
+                continue
+            del self._blocks[h]
+            del self._owner[b]
+            if self.kv.decref_block(b):
+                freed += 1
+            self.stats["evicted"] += 1
+        return freed
+
+    def clear(self) -> None:
+        for h, b in list(self._blocks.items()):
+            self.kv.decref_block(b)
+        self._blocks.clear()
+        self._owner.clear()

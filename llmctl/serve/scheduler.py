@@ -11,6 +11,13 @@ Here (``scheduler="dynamic"``), every engine step:
 2. WAITING sequences are admitted FIFO for prefill while the step's token budget
    (``max_batch_tokens`` minus the decode tokens), the batch-size cap and the free KV
    blocks (prompt + one block headroom) allow.
+Prefills are CHUNKED: a sequence whose known tokens are not all in the KV cache gets a chunk
+of them per step (at most the step's remaining token budget), so a long prompt no longer
+stalls the decodes of the running batch for a whole prefill, and prefill chunks of several
+sequences pack into one varlen batch with no padding.  With a :class:`PrefixCache`, admission
+first re-attaches the longest cached block prefix of the prompt (shared system prompts; a
+sequence resumed after preemption gets its own computed blocks back) and only the rest is
+computed.
 ``scheduler="static"`` admits a new group only when the running group has fully finished.
 ``scheduler="prefill_first"`` (TTFT-oriented): a step that can admit a waiting request runs
 only prefills — running sequences pause for that step — so a burst of arrivals gets its first
@@ -56,6 +63,9 @@ class Sequence:
     preemptions: int = 0
     on_token: Optional[Callable[["Sequence", int], None]] = None
     on_finish: Optional[Callable[["Sequence"], None]] = None
+    num_computed: int = 0  # leading positions whose K/V are in the paged cache
+    cached_tokens: int = 0  # of those, re-attached from the prefix cache (not computed)
+    kv_len: int = 0  # positions reserved in the block table (prefill target; +1 per decode)
 
     @property
     def all_ids(self) -> List[int]:
@@ -67,16 +77,29 @@ class Sequence:
 
 
 @dataclass
+class PrefillChunk:
+    """Positions [start, start + count) of ``seq`` computed in this step."""
+    seq: Sequence
+    start: int
+    count: int
+
+    @property
+    def final(self) -> bool:  # the chunk reaches the sequence's last known token: sample after it
+        return self.start + self.count == self.seq.num_tokens
+
+
+@dataclass
 class SchedulerOutput:
-    prefill: List[Sequence]
+    prefill: List[PrefillChunk]
     decode: List[Sequence]
     preempted: List[Sequence]
 
 
 class ContinuousBatchScheduler:
     def __init__(self, kv, max_batch_size: int = 8, max_batch_tokens: int = 8192, max_model_len: int = 4096,
-                 policy: str = "dynamic", block_size: int = 16):
+                 policy: str = "dynamic", block_size: int = 16, prefix_cache=None):
         self.kv = kv
+        self.prefix_cache = prefix_cache
         self.block_size = block_size
         self.max_batch_size = max_batch_size
         self.max_batch_tokens = max_batch_tokens
@@ -110,19 +133,43 @@ class ContinuousBatchScheduler:
             return False
         return self.kv.can_allocate(self.waiting[0].num_tokens + self.kv_block_size())
 
+    def _reserve(self, blocks: int) -> bool:
+        """``blocks`` free KV blocks, evicting unused prefix-cache blocks if needed."""
+        if self.kv.num_free_blocks >= blocks:
+            return True
+        if self.prefix_cache is not None:
+            self.prefix_cache.evict(blocks)
+        return self.kv.num_free_blocks >= blocks
+
+    def _admit(self, seq: Sequence) -> bool:
+        """Reserve blocks for all known tokens of ``seq`` (re-attaching its cached prefix)."""
+        n = seq.num_tokens  # a resumed sequence also re-covers its generated tokens
+        prefix = self.prefix_cache.match(seq.all_ids) if self.prefix_cache is not None else []
+        need = self.kv.blocks_needed(n + self.kv_block_size()) - len(prefix)
+        if not self._reserve(need):
+            return False
+        if not self.kv.add_sequence_shared(seq.seq_id, n, prefix):
+            return False
+        seq.num_computed = seq.cached_tokens = len(prefix) * self.block_size
+        seq.kv_len = n
+        return True
+
     def schedule(self) -> SchedulerOutput:
         preempted: List[Sequence] = []
         decode: List[Sequence] = []
-        # 1) decodes for running sequences (each needs one more KV slot); prefill_first skips
-        #    them while a waiting request can be admitted
+        # 1) decodes: running sequences whose known tokens are all cached but the newest (each
+        #    needs one more KV slot); prefill_first skips them while a request can be admitted
         running = [] if self.policy == "prefill_first" and self._can_admit() else list(self.running)
         for seq in running:
             if len(decode) >= self.max_batch_size:
                 break
-            if seq.status != "running":  # preempted earlier in this loop
+            if seq.status != "running" or seq.num_computed < seq.kv_len:  # preempted / still prefilling
                 continue
             slot = self.kv.append_token(seq.seq_id)
             while slot < 0:
+                if self.prefix_cache is not None and self._reserve(1):
+                    slot = self.kv.append_token(seq.seq_id)
+                    continue
                 victim = self._preempt_newest(exclude=seq)
                 if victim is None:
                     break
@@ -133,29 +180,41 @@ class ContinuousBatchScheduler:
                 preempted.append(seq)
                 continue
             seq._decode_slot = slot
+            seq.kv_len += 1
             decode.append(seq)
-        # 2) admissions (prefill)
-        prefill: List[Sequence] = []
+        decode = [s for s in decode if s.status == "running"]  # a later victim may have been listed
+        # 2) prefill chunks: sequences already admitted but not fully computed, then admissions
+        prefill: List[PrefillChunk] = []
+        budget = self.max_batch_tokens - len(decode)
+        decoding = {id(q) for q in decode}
+        for seq in self.running:
+            if budget <= 0:
+                break
+            if seq.status == "running" and id(seq) not in decoding and seq.num_computed < seq.kv_len:
+                c = min(seq.kv_len - seq.num_computed, budget)
+                prefill.append(PrefillChunk(seq, seq.num_computed, c))
+                budget -= c
         if self.policy == "static" and self.running:
             return SchedulerOutput(prefill, decode, preempted)
-        budget = self.max_batch_tokens - len(decode)
-        while self.waiting and len(self.running) + len(prefill) < self.max_batch_size:
+        admitted: List[Sequence] = []
+        while self.waiting and budget > 0 and len(self.running) + len(admitted) < self.max_batch_size:
             seq = self.waiting[0]
-            n = seq.num_tokens  # recompute generated tokens after a preemption
-            if n > budget and (prefill or decode):
-                break
-            if not self.kv.can_allocate(n + self.kv_block_size()):
+            if not self._admit(seq):
                 break
             self.waiting.popleft()
-            ok = self.kv.add_sequence(seq.seq_id, n)
-            if not ok:
-                self.waiting.appendleft(seq)
-                break
             seq.status = "running"
-            prefill.append(seq)
-            budget -= n
-        self.running.extend(prefill)
+            admitted.append(seq)
+            c = min(seq.kv_len - seq.num_computed, budget)
+            prefill.append(PrefillChunk(seq, seq.num_computed, c))
+            budget -= c
+        self.running.extend(admitted)
         return SchedulerOutput(prefill, decode, preempted)
+
+    def computed(self, seq: Sequence, count: int) -> None:
+        """The engine ran ``count`` more positions of ``seq``: index its newly full blocks."""
+        seq.num_computed += count
+        if self.prefix_cache is not None and seq.status == "running":
+            self.prefix_cache.insert(seq.all_ids, self.kv.block_table(seq.seq_id), seq.num_computed)
 
     def kv_block_size(self) -> int:
         return self.block_size
@@ -168,18 +227,31 @@ class ContinuousBatchScheduler:
         return None
 
     def _preempt(self, seq: Sequence) -> None:
-        self.kv.free_sequence(seq.seq_id)
+        self._release(seq)
         if seq in self.running:
             self.running.remove(seq)
         seq.status = "waiting"
+        seq.num_computed = seq.kv_len = 0
         seq.preemptions += 1
         self.waiting.appendleft(seq)
+
+    def _release(self, seq: Sequence) -> None:
+        """Free a sequence's blocks; with a prefix cache its computed full blocks stay indexed
+        (resumption after preemption and requests sharing the prefix re-attach them)."""
+        if self.prefix_cache is not None and seq.num_computed > 0:
+            try:
+                table = self.kv.block_table(seq.seq_id)
+            except (KeyError, IndexError, RuntimeError):
+                table = []
+            if table:
+                self.prefix_cache.insert(seq.all_ids, table, seq.num_computed)
+        self.kv.free_sequence(seq.seq_id)
 
     def finish(self, seq: Sequence, reason: str) -> None:
         seq.status = "finished"
         seq.finish_reason = reason
         seq.finish_time = time.time()
-        self.kv.free_sequence(seq.seq_id)
+        self._release(seq)
         if seq in self.running:
             self.running.remove(seq)
         if seq.on_finish:

@@ -104,8 +104,10 @@ class TPInferenceEngine(InferenceEngine):
         return box[0]
 
     @torch.inference_mode()
-    def prefill(self, seqs: List[Sequence]) -> torch.Tensor:
-        return self.prefill_exec(self._bcast(self.prefill_plan(seqs)))
+    def prefill(self, chunks) -> torch.Tensor:
+        if chunks and isinstance(chunks[0], Sequence):
+            chunks = [PrefillChunk(s, 0, s.num_tokens) for s in chunks]
+        return self.prefill_exec(self._bcast(self.prefill_plan(chunks)))
 
     @torch.inference_mode()
     def decode(self, seqs: List[Sequence]) -> torch.Tensor:

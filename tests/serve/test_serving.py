@@ -31,8 +31,12 @@ def test_greedy_decode_matches_full_forward(engine):
 
 
 def test_kv_blocks_released(engine):
+    engine.prefix_cache.clear()
     free0 = engine.kv.num_free_blocks
     engine.generate([[1] * 30, [2] * 3], SamplingParams(max_tokens=5, temperature=0.0))
+    # finished sequences keep only the blocks the prefix cache indexes
+    assert engine.kv.num_free_blocks == free0 - len(engine.prefix_cache)
+    engine.prefix_cache.clear()
     assert engine.kv.num_free_blocks == free0
 
 
@@ -63,15 +67,38 @@ def test_kv_manager_semantics(impl):
     assert bt.shape == (0, 3)
 
 
-def test_scheduler_token_budget():
+def _run(s, out):
+    """What the engine does after executing a step: mark the work computed and append a
+    (dummy) sampled token to every sequence whose known tokens are now all cached."""
+    for q in out.decode:
+        s.computed(q, 1)
+        q.output_ids.append(0)
+    for c in out.prefill:
+        s.computed(c.seq, c.count)
+        if c.final:
+            c.seq.output_ids.append(0)
+
+
+def _chunks(out):
+    return [(len(c.seq.prompt_ids), c.start, c.count) for c in out.prefill]
+
+
+def test_scheduler_token_budget_chunks_prefills():
+    """Budget 40: the 30-token prompt fits, the 20-token one is split 10 + 10 across steps
+    (chunked prefill) and the 5-token one joins the second step beside the first decode."""
     kv = PyKVManager(100, 16)
     s = ContinuousBatchScheduler(kv, max_batch_size=8, max_batch_tokens=40, block_size=16)
     for n in (30, 20, 5):
         s.add(Sequence(prompt_ids=[1] * n, params=SamplingParams()))
     out = s.schedule()
-    assert [len(q.prompt_ids) for q in out.prefill] == [30]  # 30 + 20 > 40
+    assert _chunks(out) == [(30, 0, 30), (20, 0, 10)] and not out.decode
+    assert [c.final for c in out.prefill] == [True, False]
+    _run(s, out)
     out = s.schedule()
-    assert len(out.decode) == 1 and [len(q.prompt_ids) for q in out.prefill] == [20, 5]
+    assert len(out.decode) == 1 and _chunks(out) == [(20, 10, 10), (5, 0, 5)]
+    _run(s, out)
+    out = s.schedule()
+    assert len(out.decode) == 3 and not out.prefill
 
 
 def test_scheduler_prefill_first_policy():
@@ -80,11 +107,59 @@ def test_scheduler_prefill_first_policy():
     for n in (30, 20, 5):
         s.add(Sequence(prompt_ids=[1] * n, params=SamplingParams()))
     out = s.schedule()
-    assert [len(q.prompt_ids) for q in out.prefill] == [30] and not out.decode
+    assert _chunks(out) == [(30, 0, 30), (20, 0, 10)] and not out.decode
+    _run(s, out)
     out = s.schedule()  # admissions pending: the running sequence pauses
-    assert not out.decode and [len(q.prompt_ids) for q in out.prefill] == [20, 5]
+    assert not out.decode and _chunks(out) == [(20, 10, 10), (5, 0, 5)]
+    _run(s, out)
     out = s.schedule()  # queue drained: everyone decodes
     assert len(out.decode) == 3 and not out.prefill
+
+
+def test_prefix_cache_reuses_blocks_and_evicts():
+    from llmctl.serve.prefix_cache import PrefixCache
+
+    kv = PyKVManager(8, 4)
+    pc = PrefixCache(kv, 4)
+    s = ContinuousBatchScheduler(kv, max_batch_size=4, max_batch_tokens=64, block_size=4, prefix_cache=pc)
+    a = Sequence(prompt_ids=list(range(1, 11)), params=SamplingParams())  # 10 tokens: 2 full blocks
+    s.add(a)
+    out = s.schedule()
+    _run(s, out)
+    assert len(pc) == 2  # blocks [1..4], [5..8] indexed
+    s.finish(a, "length")
+    assert kv.num_free_blocks == 6  # the two cached blocks stay resident
+    b = Sequence(prompt_ids=list(range(1, 9)) + [42, 43], params=SamplingParams())
+    s.add(b)
+    out = s.schedule()
+    assert _chunks(out) == [(10, 8, 2)] and b.cached_tokens == 8  # only the new tail is computed
+    _run(s, out)
+    s.finish(b, "length")
+    # a prompt needing every block evicts the unused cached ones
+    c = Sequence(prompt_ids=[7] * 25, params=SamplingParams())
+    s.add(c)
+    out = s.schedule()
+    assert _chunks(out) == [(25, 0, 25)] and pc.stats["evicted"] >= 1
+
+
+def test_preempted_sequence_resumes_from_cached_blocks():
+    """A sequence preempted after its prompt was computed re-attaches its full blocks when it
+    is readmitted: only the tail past the last full block is recomputed."""
+    from llmctl.serve.prefix_cache import PrefixCache
+
+    kv = PyKVManager(64, 4)
+    pc = PrefixCache(kv, 4)
+    s = ContinuousBatchScheduler(kv, max_batch_size=4, max_batch_tokens=64, block_size=4, prefix_cache=pc)
+    a = Sequence(prompt_ids=list(range(1, 15)), params=SamplingParams())  # 14 tokens
+    s.add(a)
+    _run(s, s.schedule())
+    for _ in range(2):  # prompt (14) + two decodes computed = 16; 17 tokens known
+        _run(s, s.schedule())
+    assert a.num_computed == 16
+    s._preempt(a)
+    assert a.status == "waiting" and a.preemptions == 1
+    out = s.schedule()
+    assert a.cached_tokens == 16 and _chunks(out) == [(14, 16, 1)]
 
 
 def test_engine_prefill_first_matches_dynamic():
@@ -150,3 +225,69 @@ def test_http_streaming(client):
     assert lines[-1] == "data: [DONE]"
     toks = [json.loads(l[6:]) for l in lines[:-1]]
     assert len([t for t in toks if t["choices"][0]["finish_reason"] is None]) == 5
+
+
+@pytest.mark.parametrize("impl", ["py", "native"])
+def test_kv_manager_shared_prefix(impl):
+    kv = PyKVManager(10, 4) if impl == "py" else make_kv_manager(10, 4, prefer_native=True)
+    assert kv.add_sequence(1, 8)
+    shared = kv.block_table(1)
+    kv.incref_block(shared[0])  # an outside holder (the prefix cache)
+    assert kv.add_sequence_shared(2, 10, shared)  # 2 shared + 1 fresh
+    assert kv.block_table(2)[:2] == shared and kv.num_free_blocks == 10 - 3
+    assert kv.refcount(shared[0]) == 3 and kv.refcount(shared[1]) == 2
+    kv.free_sequence(1)
+    kv.free_sequence(2)
+    assert kv.num_free_blocks == 9 and kv.decref_block(shared[0]) and kv.num_free_blocks == 10
+    assert not kv.add_sequence_shared(3, 44, [])  # 11 blocks > 10: refused, nothing taken
+    assert kv.num_free_blocks == 10
+
+
+def _greedy(e, prompts, n=6):
+    return [s.output_ids for s in e.generate(prompts, SamplingParams(max_tokens=n, temperature=0.0))]
+
+
+def test_chunked_prefill_matches_single_shot():
+    """A 16-token step budget splits every prompt into several prefill chunks (each attending
+    its cached earlier chunks through the paged cache); greedy outputs equal the one-shot run."""
+    prompts = [[(7 * i + 3) % 250 + 1 for i in range(45)], [5] * 17, [1, 2, 3]]
+    kw = dict(device="cpu", max_batch_size=4, num_kv_blocks=64, block_size=8, max_model_len=256,
+              prefix_caching=False)
+    chunked = InferenceEngine("tiny", max_batch_tokens=16, **kw)
+    ref = InferenceEngine("tiny", max_batch_tokens=4096, **kw)
+    assert _greedy(chunked, prompts) == _greedy(ref, prompts)
+    assert chunked.stats["prefill_tokens"] == ref.stats["prefill_tokens"] == 45 + 17 + 3
+
+
+def test_prefix_cache_hit_skips_prefix_compute():
+    """A second request sharing a 32-token prefix computes only its own tail, and its tokens
+    equal an engine without prefix caching."""
+    base = [(11 * i) % 200 + 1 for i in range(32)]
+    p1, p2 = base + [9, 9, 9], base + [4, 5]
+    kw = dict(device="cpu", max_batch_size=2, num_kv_blocks=64, block_size=8, max_model_len=256)
+    e = InferenceEngine("tiny", **kw)
+    out1 = _greedy(e, [p1])
+    before = e.stats["prefill_tokens"]
+    out2 = _greedy(e, [p2])
+    assert e.stats["prefill_tokens"] - before == len(p2) - 32  # 4 cached blocks re-attached
+    ref = InferenceEngine("tiny", prefix_caching=False, **kw)
+    assert out1 + out2 == _greedy(ref, [p1]) + _greedy(ref, [p2])
+
+
+def test_preemption_resume_reuses_cached_blocks():
+    """A sequence preempted mid-generation re-attaches its full cached blocks when resumed:
+    only the tail past its last full block is recomputed, and greedy tokens are unchanged."""
+    prompt = [(5 * i) % 97 + 1 for i in range(21)]
+    kw = dict(device="cpu", max_batch_size=2, num_kv_blocks=64, block_size=4, max_model_len=128)
+    e = InferenceEngine("tiny", **kw)
+    seq = e.add_request(prompt, SamplingParams(max_tokens=10, temperature=0.0))
+    for _ in range(4):  # prefill + 3 decodes: 24 positions computed
+        e.step()
+    assert seq.num_computed == 24
+    e.scheduler._preempt(seq)
+    before = e.stats["prefill_tokens"]
+    while seq.status != "finished":
+        e.step()
+    assert seq.cached_tokens == 24 and e.stats["prefill_tokens"] - before == 1  # 25 known, 24 re-attached
+    ref = InferenceEngine("tiny", prefix_caching=False, **kw)
+    assert seq.output_ids == _greedy(ref, [prompt], 10)[0]
