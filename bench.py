@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--virtual-stages", type=int, default=1, help="interleaved pipeline chunks per rank")
+    ap.add_argument("--microbatches", type=int, default=0, help="pipeline micro-batches (0: 2*pp)")
     ap.add_argument("--zero", type=int, default=-1, help="ZeRO stage (-1: 0 on 1 GPU, 1 on >1)")
     ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--cp", type=int, default=1, help="context-parallel degree")
@@ -71,6 +73,7 @@ def main():
         gradient_accumulation_steps=args.grad_accum, learning_rate=3e-4, weight_decay=0.1, scheduler="cosine",
         warmup_steps=10, max_steps=args.warmup + args.steps, gradient_clipping=1.0, mixed_precision="bf16",
         tensor_parallel=args.tp, pipeline_parallel=args.pp, zero_stage=zero,
+        virtual_stages=args.virtual_stages, num_microbatches=args.microbatches,
         sequence_parallel=args.sequence_parallel, activation_checkpoint=args.activation_checkpoint,
         context_parallel=args.cp, context_parallel_mode=args.cp_mode, expert_parallel=args.ep,
         bucket_mb=args.bucket_mb, device=args.device, distributed_backend=args.backend, seed=1234,
@@ -116,6 +119,7 @@ def main():
     fpt = mc.flops_per_token(args.seq_len)
     mfu = tps * fpt / (2.5e15 * world) if dev.type == "cuda" else None
     par = f"dp{dp}" + (f"-tp{args.tp}" if args.tp > 1 else "") + (f"-pp{args.pp}" if args.pp > 1 else "") + \
+        (f"v{args.virtual_stages}" if args.pp > 1 and args.virtual_stages > 1 else "") + \
         (f"-zero{zero}" if zero else "") + ("-sp" if args.sequence_parallel else "") + \
         (f"-cp{args.cp}{'ring' if args.cp_mode == 'ring' else ''}" if args.cp > 1 else "") + \
         (f"-ep{args.ep}" if args.ep > 1 else "")

@@ -34,8 +34,8 @@ def compute_plan(model: Path, hardware: Path, target_flops: Optional[float] = 1e
                  pipeline_parallel: Optional[int] = None, zero_stage: Optional[int] = None,
                  sequence_parallel: Optional[bool] = None, activation_checkpoint: Optional[str] = None,
                  micro_batch_size: Optional[int] = None, global_batch_size: Optional[int] = None,
-                 seq_len: int = 2048, compat_reference: bool = False, max_memory_explicit: bool = False
-                 ) -> Dict[str, Any]:
+                 seq_len: int = 2048, compat_reference: bool = False, max_memory_explicit: bool = False,
+                 virtual_stages: Optional[int] = None) -> Dict[str, Any]:
     from llmctl.partition.planner import ParallelismPlanner, ReferenceCompatPlanner
     from llmctl.partition.shard_map import build_shard_map
 
@@ -56,19 +56,20 @@ def compute_plan(model: Path, hardware: Path, target_flops: Optional[float] = 1e
         mem_limit = max_memory_gb if max_memory_explicit else None
         if strategy == "auto":
             fixed = {"tp": tensor_parallel, "pp": pipeline_parallel, "zs": zero_stage, "sp": sequence_parallel,
-                     "ac": activation_checkpoint, "mb": micro_batch_size}
+                     "ac": activation_checkpoint, "mb": micro_batch_size, "vs": virtual_stages}
             plan = planner.search_optimal_plan(max_memory=mem_limit, global_batch=global_batch_size,
                                                fixed={k: v for k, v in fixed.items() if v is not None} or None)
         else:
             plan = planner.manual_plan(tensor_parallel or 1, pipeline_parallel or 1, 1 if zero_stage is None else zero_stage,
                                        sp=bool(sequence_parallel), ac=activation_checkpoint or "selective",
-                                       mb=micro_batch_size or 1, global_batch=global_batch_size)
+                                       mb=micro_batch_size or 1, global_batch=global_batch_size,
+                                       vs=virtual_stages or 1)
         params = planner.estimate_parameters()
         model_mem = planner.estimate_model_memory()
     sm = None
     if plan.get("data_parallel", 0) >= 1:
         sm = build_shard_map(model_config, plan["tensor_parallel"], plan["pipeline_parallel"], plan["data_parallel"],
-                             plan["zero_stage"])
+                             plan["zero_stage"], plan.get("virtual_stages", 1))
     return {"plan": plan, "params": params, "model_memory_gb": model_mem, "model": model_config,
             "hardware": hw_profile, "shard_map": sm}
 
@@ -81,6 +82,7 @@ def _display(plan: Dict[str, Any], params: int, model_mem: float, target_flops, 
     t.add_column("Description", style="dim")
     rows = [("Tensor Parallel", "tensor_parallel", "Degree of tensor parallelism"),
             ("Pipeline Parallel", "pipeline_parallel", "Degree of pipeline parallelism"),
+            ("Virtual Stages", "virtual_stages", "Model chunks per pipeline rank (interleaved 1F1B)"),
             ("Data Parallel", "data_parallel", "Degree of data parallelism"),
             ("ZeRO Stage", "zero_stage", "ZeRO optimizer sharding stage"),
             ("Sequence Parallel", "sequence_parallel", "Megatron-SP inside the TP group"),
@@ -122,6 +124,8 @@ def compute(
     strategy: str = typer.Option("auto", help="Strategy (auto, manual)"),
     tensor_parallel: Optional[int] = typer.Option(None, help="Manual tensor parallel degree"),
     pipeline_parallel: Optional[int] = typer.Option(None, help="Manual pipeline parallel degree"),
+    virtual_stages: Optional[int] = typer.Option(None, "--virtual-stages",
+                                                 help="Interleaved pipeline: model chunks per pipeline rank"),
     zero_stage: Optional[int] = typer.Option(None, help="Manual ZeRO stage"),
     sequence_parallel: Optional[bool] = typer.Option(None, "--sequence-parallel/--no-sequence-parallel",
                                                      help="Megatron sequence parallelism"),
@@ -140,7 +144,7 @@ def compute(
     res = compute_plan(model, hardware, target_flops, mm if mm is not None else 40.0, max_comm_bw_gbps, strategy,
                        tensor_parallel, pipeline_parallel, zero_stage, sequence_parallel, activation_checkpoint,
                        micro_batch_size, global_batch_size, seq_len, compat_reference,
-                       max_memory_explicit=explicit)
+                       max_memory_explicit=explicit, virtual_stages=virtual_stages)
     plan = res["plan"]
     hw_count = res["hardware"].get("gpu", {}).get("count", 0)
     console.print(f"[green]✓[/green] Model: {res['model'].get('name', 'Unknown')}")

@@ -96,6 +96,7 @@ class ParallelSection(_Open):
     strategy: str = "auto"
     tensor_parallel: int = 1
     pipeline_parallel: int = 1
+    virtual_stages: int = 1  # interleaved pipeline: model chunks per pipeline rank
     sequence_parallel: bool = False
     context_parallel: int = 1
     context_parallel_mode: str = "ulysses"  # ulysses | ring
@@ -162,6 +163,8 @@ class PlanParallelism(_Open):
     expert_parallel: int = 1
     activation_checkpoint: str = "none"
     grad_accum: int = 1
+    virtual_stages: int = 1
+    num_microbatches: Optional[int] = None
 
 
 class PlanSchema(_Open):
@@ -195,6 +198,7 @@ def resolve_training_config(train_file: Optional[Dict[str, Any]] = None, plan: O
         out["warmup_steps"] = int(sch.get("warmup_steps", 0))
         p = t.parallel
         out.update(tensor_parallel=p.tensor_parallel, pipeline_parallel=p.pipeline_parallel,
+                   virtual_stages=p.virtual_stages,
                    sequence_parallel=p.sequence_parallel, zero_stage=p.zero_stage,
                    context_parallel=p.context_parallel, context_parallel_mode=p.context_parallel_mode,
                    expert_parallel=p.expert_parallel, batch_size=p.micro_batch_size)
@@ -237,7 +241,9 @@ def resolve_training_config(train_file: Optional[Dict[str, Any]] = None, plan: O
                    zero_stage=pp.zero_stage, batch_size=pp.micro_batch_size,
                    sequence_parallel=pp.sequence_parallel, activation_checkpoint=pp.activation_checkpoint,
                    context_parallel=pp.context_parallel, expert_parallel=pp.expert_parallel,
-                   gradient_accumulation_steps=max(pp.grad_accum, 1))
+                   gradient_accumulation_steps=max(pp.grad_accum, 1), virtual_stages=pp.virtual_stages)
+        if pp.pipeline_parallel > 1 and pp.num_microbatches:
+            out["num_microbatches"] = pp.num_microbatches
     if cli:
         out.update({k: v for k, v in cli.items() if v is not None})
     return out

@@ -47,7 +47,7 @@ def load_model(path: str, device=None, dtype=torch.bfloat16, pc: Optional[Parall
     model = build_model(cfg, device=device, dtype=dtype, pc=pc, seed=seed)
     tp = pc.tp_size if pc else 1
     tpr = pc.tp_rank if pc else 0
-    start = pc.layer_start if pc else 0
+    start = pc.layer_index if pc else 0
     with torch.no_grad():
         for n, p in model.named_parameters():
             g = _global_name(n, start)

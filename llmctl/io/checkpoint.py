@@ -92,19 +92,22 @@ def shard_tp(name: str, full: torch.Tensor, tp: int, rank: int, cfg) -> torch.Te
     return torch.cat(out, 0)
 
 
-def _global_name(name: str, layer_start: int) -> str:
-    # "layers.<local>.x" -> "layers.<global>.x"
+def _global_name(name: str, layer_start) -> str:
+    """"layers.<local>.x" -> "layers.<global>.x"; ``layer_start`` is the offset of one
+    contiguous layer range or the list of global layer ids (``ParallelContext.layer_index``)."""
     if name.startswith("layers."):
         parts = name.split(".")
-        parts[1] = str(int(parts[1]) + layer_start)
+        i = int(parts[1])
+        parts[1] = str(layer_start[i] if isinstance(layer_start, (list, tuple)) else i + layer_start)
         return ".".join(parts)
     return name
 
 
-def _local_name(name: str, layer_start: int) -> str:
+def _local_name(name: str, layer_start) -> str:
     if name.startswith("layers."):
         parts = name.split(".")
-        parts[1] = str(int(parts[1]) - layer_start)
+        g = int(parts[1])
+        parts[1] = str(list(layer_start).index(g) if isinstance(layer_start, (list, tuple)) else g - layer_start)
         return ".".join(parts)
     return name
 
@@ -143,7 +146,7 @@ class CheckpointManager:
             else:
                 named = list(e.model.named_parameters())
             for n, p in named:
-                model_sd[_global_name(n, e.pc.layer_start)] = p.detach().to("cpu", copy=True).contiguous()
+                model_sd[_global_name(n, e.pc.layer_index)] = p.detach().to("cpu", copy=True).contiguous()
         opt_sd = {k: (v.detach().to("cpu", copy=True) if torch.is_tensor(v) else v)
                   for k, v in e.optimizer.state_dict().items()}
         opt_index = optimizer_index(e)
@@ -253,7 +256,7 @@ class CheckpointManager:
                  else list(e.model.named_parameters()))
         with torch.no_grad():
             for n, prm in named:
-                g = _global_name(n, e.pc.layer_start)
+                g = _global_name(n, e.pc.layer_index)
                 if hasattr(e, "_expert_global"):
                     g = e._expert_global(g)
                 if g == "lm_head" and g not in full and e.model_config.tie_word_embeddings:
@@ -301,7 +304,7 @@ def optimizer_index(e) -> Optional[Dict[str, Any]]:
     if getattr(e, "zero3", None) is not None:
         return None
     opt, flat = e.optimizer, e.flat
-    start = e.pc.layer_start
+    start = e.pc.layer_index
     params = [(flat.offsets[id(q)], q.numel(), _global_name(flat.names[id(q)], start), list(q.shape))
               for q in flat.params]
     segs = []
@@ -341,7 +344,7 @@ def reshard_optimizer(e, path: Path, state: Dict[str, Any]) -> None:
             for seg in idx["segments"]:
                 where.setdefault(seg[0], {}).setdefault(tr, []).append((idx, sd, seg))
     keys = ("master", "exp_avg", "exp_avg_sq")
-    start = e.pc.layer_start
+    start = e.pc.layer_index
     new_tp, new_tr = e.pg.layout.tp, e.pg.tp_rank
     for q in flat.params:
         g = _global_name(flat.names[id(q)], start)

@@ -230,6 +230,11 @@ MODEL_TEMPLATES: Dict[str, Dict[str, Dict[str, Any]]] = {
             "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
             "rope": {"base": 10000, "scaling": "linear"},
         },
+        "deep": {  # 8 thin layers: enough pipeline stages for interleaved (virtual-stage) tests
+            "name": "tiny-deep", "arch": "decoder-only", "layers": 8, "hidden": 128, "ffn": 352,
+            "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
+            "rope": {"base": 10000, "scaling": "linear"},
+        },
         "tied": {  # GPT-2 style (layernorm, GELU, learned positions, tied LM head)
             "name": "tiny-tied", "arch": "decoder-only", "layers": 2, "hidden": 256, "ffn": 1024,
             "heads": 4, "vocab_size": 512, "norm": "layernorm", "activation": "gelu",
@@ -244,7 +249,7 @@ ALIASES = {
     "llama-13b": ("llama", "13b"), "llama-30b": ("llama", "30b"), "llama3-70b": ("llama", "70b"),
     "llama-70b": ("llama", "70b"), "tiny": ("tiny", "test"), "tiny-test": ("tiny", "test"),
     "mixtral-8x7b": ("mixtral", "8x7b"), "tiny-moe": ("tiny", "moe"),
-    "tiny-tied": ("tiny", "tied"),
+    "tiny-tied": ("tiny", "tied"), "tiny-deep": ("tiny", "deep"),
 }
 
 

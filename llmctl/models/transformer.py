@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -42,6 +42,17 @@ class ParallelContext:
     layer_end: Optional[int] = None
     has_embedding: bool = True
     has_head: bool = True
+    # interleaved pipeline (virtual stages): this rank's model chunks as global [start, end)
+    # layer ranges, in chunk order (None: the single range [layer_start, layer_end))
+    layer_ranges: Optional[List[Tuple[int, int]]] = None
+
+    @property
+    def layer_index(self):
+        """Local -> global layer numbering for parameter names: the offset ``layer_start`` for
+        one contiguous range, or the list of global ids of the local layers (virtual stages)."""
+        if self.layer_ranges is None:
+            return self.layer_start
+        return [i for a, b in self.layer_ranges for i in range(a, b)]
     # recompute policy: "none" | "selective" | "full"
     activation_checkpoint: str = "none"
     # context parallel (llmctl.parallel.context_parallel): "ulysses" all-to-all around
@@ -250,9 +261,13 @@ class DecoderLM(nn.Module):
             if cfg.position == "learned":
                 self.pos_embed = nn.Parameter(torch.empty(cfg.max_position_embeddings, h, **kw))
                 _init_linear(self.pos_embed, 0.01)
-        self.layers = nn.ModuleList(
-            [DecoderLayer(cfg, pc, i, **kw) for i in range(pc.layer_start, end)]
-        )
+        ranges = pc.layer_ranges or [(pc.layer_start, end)]
+        self.layers = nn.ModuleList([DecoderLayer(cfg, pc, i, **kw) for a, b in ranges for i in range(a, b)])
+        # local [start, end) slice of every model chunk (one chunk unless virtual stages)
+        self.chunk_slices, o = [], 0
+        for a, b in ranges:
+            self.chunk_slices.append((o, o + b - a))
+            o += b - a
         self.final_norm_w = self.final_norm_b = self.lm_head = None
         if pc.has_head:
             self.final_norm_w = nn.Parameter(torch.ones(h, **kw))
@@ -307,14 +322,16 @@ class DecoderLM(nn.Module):
             x = x + pos
         return x
 
-    def run_layers(self, x, B, S, residual=None, positions=None, doc_start=None):
+    def run_layers(self, x, B, S, residual=None, positions=None, doc_start=None, chunk: Optional[int] = None):
+        """Run the local decoder layers (only model chunk ``chunk`` under virtual stages)."""
         if self.pc.cp_size > 1 and positions is None:
             positions = cp.local_positions(B, S, self.pc.cp_rank, x.device)
         if doc_start is not None and positions is None:  # packed documents: RoPE restarts per document
             positions = (torch.arange(S, device=x.device, dtype=torch.int32).view(1, S) - doc_start).reshape(-1)
         rope = self.rope_tables(S * self.pc.cp_size, x.device)
         ac = self.pc.activation_checkpoint
-        for layer in self.layers:
+        layers = self.layers if chunk is None else self.layers[self.chunk_slices[chunk][0]:self.chunk_slices[chunk][1]]
+        for layer in layers:
             if ac == "full" and self.training and torch.is_grad_enabled():
                 if residual is None:
                     x, residual = torch.utils.checkpoint.checkpoint(

@@ -43,6 +43,7 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("paged_prefill_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor work, float scale) -> Tensor");
   m.def("paged_attention_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, float scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w, Tensor? bias) -> Tensor");
+  m.def("skinny_linear_cfg(Tensor x, Tensor w, Tensor? bias, int config) -> Tensor");
   m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor uniform) -> Tensor");
   // benchmarks / tuning (gemm_bf16.hip, hbm_stream.hip)
   m.def("gemm_bf16(Tensor a, Tensor b) -> Tensor");

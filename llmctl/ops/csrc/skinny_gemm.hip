@@ -25,7 +25,6 @@ using attn::bf16x8_t;
 using f32x4_t = __attribute__((ext_vector_type(4))) float;
 
 constexpr int KBLK = 128;  // K per block: 4 MFMA steps of 32
-constexpr int NW = 8;      // waves per workgroup (K split)
 
 __device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -35,7 +34,7 @@ __device__ __forceinline__ bf16x8_t ld16(const unsigned short* p) {
   return *reinterpret_cast<const bf16x8_t*>(p);
 }
 
-template <int NT, int MT, int GB>
+template <int NT, int MT, int GB, int NW>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned short* __restrict__ x,
                                                               const unsigned short* __restrict__ w,
                                                               const unsigned short* __restrict__ bias,
@@ -134,7 +133,18 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
 
 }  // namespace
 
-at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+template <int NT, int MT, int GB, int NW>
+void launch_skinny(const at::Tensor& x, const at::Tensor& w, const unsigned short* bp, at::Tensor& y, int M, int N,
+                   int K) {
+  LLMCTL_CHECK(N % (16 * NT) == 0, "skinny_linear: N must be a multiple of ", 16 * NT, " for this config");
+  hipLaunchKernelGGL((skinny_gemm_kernel<NT, MT, GB, NW>), dim3(N / (16 * NT)), dim3(NW * 64), 0, stream(), bf_ptr(x),
+                     bf_ptr(w), bp, bf_mut(y), M, N, K);
+}
+
+// config: 0 = automatic (measured best per shape, tools/skinny_sweep.py); otherwise
+// 1 + index into {NT, GB, NW} of the table below (MT follows M: 1 for M <= 16, else 2)
+at::Tensor skinny_linear_cfg(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                             int64_t config) {
   LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(), "skinny_linear: 2-D contiguous");
   LLMCTL_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "skinny_linear: bf16");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
@@ -147,17 +157,36 @@ at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w, const c10::op
   }
   const c10::DeviceGuard guard(x.device());
   auto y = at::empty({M, N}, x.options());
-  // (a two-row-tile variant for wide projections measured slower: 32.8 vs 23.9 us on the
-  // GPT-7B QKV at M=1 — more rows per wave cost more than the shared token fragment saves)
-  dim3 grid(N / 16), block(NW * 64);
-  auto st = stream();
-  if (M <= 16)
-    hipLaunchKernelGGL((skinny_gemm_kernel<1, 1, 4>), grid, block, 0, st, bf_ptr(x), bf_ptr(w), bp, bf_mut(y), M, N, K);
-  else
-    hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 2>), grid, block, 0, st, bf_ptr(x), bf_ptr(w), bp, bf_mut(y), M, N, K);
+  int c = (int)config;
+  if (c == 0) c = 1;  // the original configuration (NT 1, GB 4 / 2, 8 waves)
+  const bool m1 = M <= 16;
+  switch (c) {
+    case 1: m1 ? launch_skinny<1, 1, 4, 8>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 2, 8>(x, w, bp, y, M, N, K); break;
+    case 2: m1 ? launch_skinny<1, 1, 4, 4>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 2, 4>(x, w, bp, y, M, N, K); break;
+    case 3: m1 ? launch_skinny<1, 1, 8, 4>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 4, 4>(x, w, bp, y, M, N, K); break;
+    case 4: m1 ? launch_skinny<2, 1, 4, 4>(x, w, bp, y, M, N, K) : launch_skinny<2, 2, 2, 4>(x, w, bp, y, M, N, K); break;
+    case 5: m1 ? launch_skinny<1, 1, 4, 2>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 2, 2>(x, w, bp, y, M, N, K); break;
+    case 6: m1 ? launch_skinny<2, 1, 2, 8>(x, w, bp, y, M, N, K) : launch_skinny<2, 2, 1, 8>(x, w, bp, y, M, N, K); break;
+    case 7: m1 ? launch_skinny<1, 1, 8, 2>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 4, 2>(x, w, bp, y, M, N, K); break;
+    case 8: m1 ? launch_skinny<1, 1, 4, 1>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 2, 1>(x, w, bp, y, M, N, K); break;
+    case 9: m1 ? launch_skinny<4, 1, 2, 4>(x, w, bp, y, M, N, K) : launch_skinny<4, 2, 1, 4>(x, w, bp, y, M, N, K); break;
+    case 10: m1 ? launch_skinny<4, 1, 2, 8>(x, w, bp, y, M, N, K) : launch_skinny<4, 2, 1, 8>(x, w, bp, y, M, N, K); break;
+    case 11: m1 ? launch_skinny<4, 1, 1, 8>(x, w, bp, y, M, N, K) : launch_skinny<4, 2, 1, 8>(x, w, bp, y, M, N, K); break;
+    case 12: m1 ? launch_skinny<8, 1, 1, 8>(x, w, bp, y, M, N, K) : launch_skinny<8, 2, 1, 8>(x, w, bp, y, M, N, K); break;
+    case 13: m1 ? launch_skinny<2, 1, 4, 8>(x, w, bp, y, M, N, K) : launch_skinny<2, 2, 2, 8>(x, w, bp, y, M, N, K); break;
+    case 14: m1 ? launch_skinny<4, 1, 2, 2>(x, w, bp, y, M, N, K) : launch_skinny<4, 2, 1, 2>(x, w, bp, y, M, N, K); break;
+    default: LLMCTL_CHECK(false, "skinny_linear: unknown config ", config);
+  }
   return y;
 }
 
-TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("skinny_linear", &skinny_linear); }
+at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+  return skinny_linear_cfg(x, w, bias, 0);
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("skinny_linear", &skinny_linear);
+  m.impl("skinny_linear_cfg", &skinny_linear_cfg);
+}
 
 }  // namespace llmctl

@@ -24,6 +24,70 @@ import torch
 import torch.distributed as dist
 
 
+def interleaved_order(P: int, V: int, M: int, s: int) -> List[Tuple[str, int, int]]:
+    """Megatron's interleaved 1F1B order on rank ``s``: (kind, model chunk, micro-batch).
+    Forward k runs chunk (k // P) % V on micro-batch (k // PV) * P + k % P (groups of P
+    micro-batches sweep the chunks), backward k the mirrored chunk V-1-(k // P) % V; warm-up
+    (P - s - 1) * 2 + (V - 1) * P forwards (all of them when M == P), then 1F1B, then cool-down."""
+    total = M * V
+
+    def mb(k):
+        return (k // (P * V)) * P + k % P
+
+    warm = total if M == P else min((P - s - 1) * 2 + (V - 1) * P, total)
+    order = [("F", (k // P) % V, mb(k)) for k in range(warm)]
+    f, b = warm, 0
+    while f < total:
+        order.append(("F", (f // P) % V, mb(f)))
+        order.append(("B", V - 1 - (b // P) % V, mb(b)))
+        f, b = f + 1, b + 1
+    while b < total:
+        order.append(("B", V - 1 - (b // P) % V, mb(b)))
+        b += 1
+    return order
+
+
+def build_interleaved_rounds(P: int, V: int, M: int):
+    """Lock-step execution table of the interleaved schedule, computed identically on every
+    rank: ``[(actions, messages)]`` per round, ``actions[s]`` = the (kind, chunk, mb) rank s
+    runs (or None: its next action's input has not arrived), ``messages`` =
+    (kind, src, dst, dst virtual stage, mb) sent after the round, in canonical order.  A message
+    sent in round r is consumed in a later round.  Raises if the order deadlocks."""
+    orders = [interleaved_order(P, V, M, s) for s in range(P)]
+    ptr = [0] * P
+    have = [set() for _ in range(P)]  # ("act" | "grad", virtual stage, mb) received
+    last = P * V - 1
+    rounds = []
+    while any(ptr[s] < len(orders[s]) for s in range(P)):
+        acts = [None] * P
+        for s in range(P):
+            if ptr[s] >= len(orders[s]):
+                continue
+            kind, c, m = orders[s][ptr[s]]
+            vs = c * P + s
+            need = (None if vs == 0 else ("act", vs, m)) if kind == "F" else (None if vs == last else ("grad", vs, m))
+            if need is None or need in have[s]:
+                acts[s] = (kind, c, m)
+                ptr[s] += 1
+        if all(a is None for a in acts):
+            raise RuntimeError(f"interleaved pipeline schedule deadlocks (P={P}, V={V}, M={M})")
+        msgs = []
+        for s, a in enumerate(acts):
+            if a is None:
+                continue
+            kind, c, m = a
+            vs = c * P + s
+            if kind == "F" and vs < last:
+                msgs.append(("act", s, (vs + 1) % P, vs + 1, m))
+            elif kind == "B" and vs > 0:
+                msgs.append(("grad", s, (vs - 1) % P, vs - 1, m))
+        msgs.sort()
+        for kind, src, dst, vs, m in msgs:
+            have[dst].add((kind, vs, m))
+        rounds.append((acts, msgs))
+    return rounds
+
+
 @torch.no_grad()
 def broadcast_tied_embedding(model, pg) -> None:
     """Copy stage 0's ``embed`` into the last stage's ``lm_head`` (tied word embeddings).
@@ -44,6 +108,11 @@ class PipelineSchedule:
         self.s = pg.pp_rank
         self.ranks = pg.pp_ranks
         self.num_microbatches = max(int(num_microbatches), 1)
+        self.V = max(int(getattr(engine.config, "virtual_stages", 1) or 1), 1)
+        if self.V > 1 and self.num_microbatches % self.P:
+            raise ValueError(f"interleaved pipeline: micro-batches ({self.num_microbatches}) must be a multiple of "
+                             f"pipeline_parallel ({self.P})")
+        self._rounds = build_interleaved_rounds(self.P, self.V, self.num_microbatches) if self.V > 1 else None
         self.prev = self.ranks[self.s - 1] if self.s > 0 else None
         self.next = self.ranks[self.s + 1] if self.s < self.P - 1 else None
         # tied word embeddings: stage 0 owns ``embed``, stage P-1 an ``lm_head`` copy.  The copy
@@ -54,6 +123,7 @@ class PipelineSchedule:
         if self.tied and self.is_last:
             engine.optimizer.norm_exclude.append(self._tied_grad)
         self.last_loss: Optional[torch.Tensor] = None
+        self._pending_sends: List = []
 
     # ------------------------------------------------------------------ tied embeddings
     def _tied_param(self):
@@ -103,20 +173,43 @@ class PipelineSchedule:
 
     def _p2p(self, send: Optional[Tuple[torch.Tensor, int]] = None,
              recv: Optional[Tuple[torch.Tensor, int]] = None) -> None:
+        """One matched send/recv group.  A group with a receive is waited for (its data is used
+        next).  A SEND-ONLY group (warm-up forwards, cool-down backwards) completes in the
+        background: its work handles and tensor are kept until ``_drain_sends`` (end of the
+        schedule), so the next micro-batch's compute starts while the activation / gradient is
+        still on the wire (no compute-stream wait on the send)."""
         ops = []
         if send is not None:
-            ops.append(dist.P2POp(dist.isend, send[0].contiguous(), send[1]))
+            t = send[0].contiguous()
+            ops.append(dist.P2POp(dist.isend, t, send[1]))
         if recv is not None:
             ops.append(dist.P2POp(dist.irecv, recv[0], recv[1]))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
+        if not ops:
+            return
+        works = dist.batch_isend_irecv(ops)
+        if recv is None:  # send-only group (warm-up / cool-down): completes in the background
+            self._pending_sends.extend((w, t) for w in works)
+        else:
+            # with a receive in the group, wait for the group (NCCL returns ONE work for a
+            # coalesced send+recv group, so the two cannot be waited for separately)
+            for w in works:
                 w.wait()
+
+    def _drain_sends(self) -> None:
+        for w, _ in self._pending_sends:
+            w.wait()
+        self._pending_sends.clear()
 
     def _empty(self, B, S):
         return torch.empty(self._act_shape(B, S), dtype=self.e.config.dtype, device=self.e.device)
 
     # ------------------------------------------------------------------ stage compute
-    def _forward(self, x_in: Optional[torch.Tensor], ids: torch.Tensor, labels: torch.Tensor, denom: float):
+    def _forward(self, x_in: Optional[torch.Tensor], ids: torch.Tensor, labels: torch.Tensor, denom: float,
+                 chunk: Optional[int] = None, first: Optional[bool] = None, last: Optional[bool] = None):
+        """One stage's (or, under virtual stages, one model chunk's) forward: embedding on the
+        first, loss on the last."""
+        first = self.is_first if first is None else first
+        last = self.is_last if last is None else last
         m = self.e.model
         B, S = ids.shape
         positions = doc_start = None
@@ -127,9 +220,9 @@ class PipelineSchedule:
             doc_start = document_starts(ids, c.doc_separator)
             labels = labels.masked_fill(ids == c.doc_separator, -100)
             positions = (torch.arange(S, device=ids.device, dtype=torch.int32).view(1, S) - doc_start).reshape(-1)
-        x = m.embed_tokens(ids, positions) if self.is_first else x_in
-        x, res = m.run_layers(x, B, S, positions=positions, doc_start=doc_start)
-        if self.is_last:
+        x = m.embed_tokens(ids, positions) if first else x_in
+        x, res = m.run_layers(x, B, S, positions=positions, doc_start=doc_start, chunk=chunk)
+        if last:
             logits = m.head(x, res)
             return m.loss(logits, labels, denom)
         return x + res if res is not None else x
@@ -143,6 +236,8 @@ class PipelineSchedule:
 
     # ------------------------------------------------------------------ 1F1B
     def run(self, batches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        if self.V > 1:
+            return self._run_interleaved(batches)
         M = len(batches)
         P, s = self.P, self.s
         B, S = batches[0][0].shape
@@ -221,10 +316,74 @@ class PipelineSchedule:
             if not self.is_first:
                 self._p2p(send=(g, self.prev))
         self._set_sync(True)
+        self._drain_sends()
         if self.is_last:
             loss = torch.stack(losses).sum()
         else:
             loss = torch.zeros((), device=self.e.device)
+        self.last_loss = loss
+        return loss
+
+    # ------------------------------------------------------------------ interleaved 1F1B
+    def _run_interleaved(self, batches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        """Virtual-stage schedule: rank s owns model chunks c = 0..V-1 = virtual stages
+        c*P + s; activations go to virtual stage +1 (rank s+1, or rank 0's next chunk after
+        the last rank), gradients back.  Each rank follows Megatron's interleaved order
+        (:func:`interleaved_order`); the lock-step round table from
+        :func:`build_interleaved_rounds` (identical on every rank) says which messages cross
+        the wire after each round, so both ends of every send/recv pair issue it in the same
+        round and in the same canonical order (NCCL matches point-to-point by order only)."""
+        M = len(batches)
+        if M != self.num_microbatches:
+            raise ValueError(f"interleaved pipeline was built for {self.num_microbatches} micro-batches, got {M}")
+        P, V, s = self.P, self.V, self.s
+        B, S = batches[0][0].shape
+        denom = float(batches[0][1].numel() * M * self.e.pg.layout.cp)
+        last_vs = P * V - 1
+        inputs: dict = {}
+        grads: dict = {}
+        stash: dict = {}
+        losses: List[torch.Tensor] = []
+        for acts, msgs in self._rounds:
+            a = acts[s]
+            out_msg: dict = {}
+            if a is not None:
+                kind, c, mb = a
+                vs = c * P + s
+                if kind == "F":
+                    x_in = None
+                    if vs > 0:
+                        x_in = inputs.pop((vs, mb))
+                        x_in.requires_grad_(True)
+                    ids, labels = batches[mb]
+                    out = self._forward(x_in, ids, labels, denom, chunk=c, first=vs == 0, last=vs == last_vs)
+                    stash[(vs, mb)] = (x_in, out)
+                    if vs == last_vs:
+                        losses.append(out.detach())
+                    else:
+                        out_msg[("act", vs + 1, mb)] = out.detach()
+                else:
+                    x_in, out = stash.pop((vs, mb))
+                    self._set_sync(mb == M - 1)  # the chunk's last micro-batch: its grads are final
+                    if vs == last_vs:
+                        out.backward()
+                    else:
+                        torch.autograd.backward(out, grads.pop((vs, mb)))
+                    if vs > 0:
+                        out_msg[("grad", vs - 1, mb)] = x_in.grad
+            ops = []
+            for kind, src, dst, vs_dst, mb in msgs:
+                if src == s:
+                    ops.append(dist.P2POp(dist.isend, out_msg[(kind, vs_dst, mb)].contiguous(), self.ranks[dst]))
+                elif dst == s:
+                    buf = self._empty(B, S)
+                    (inputs if kind == "act" else grads)[(vs_dst, mb)] = buf
+                    ops.append(dist.P2POp(dist.irecv, buf, self.ranks[src]))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+        self._set_sync(True)
+        loss = torch.stack(losses).sum() if losses else torch.zeros((), device=self.e.device)
         self.last_loss = loss
         return loss
 
@@ -244,6 +403,27 @@ class PipelineSchedule:
     @torch.no_grad()
     def eval_loss(self, ids: torch.Tensor, labels: torch.Tensor, denom: Optional[float] = None) -> torch.Tensor:
         B, S = ids.shape
+        if self.V > 1:  # walk the virtual stages in order: 0..P-1 on chunk 0, then chunk 1, ...
+            P, last_vs = self.P, self.P * self.V - 1
+            d = float(denom if denom is not None else labels.numel())
+            x, out = None, torch.zeros((), device=self.e.device)
+            for vs in range(last_vs + 1):
+                owner, c = vs % P, vs // P
+                if owner == self.s:
+                    if vs > 0:
+                        x = self._empty(B, S)
+                        self._p2p(recv=(x, self.ranks[(vs - 1) % P]))
+                    y = self._forward(x, ids, labels, d, chunk=c, first=vs == 0, last=vs == last_vs)
+                    if vs == last_vs:
+                        out = y
+                    else:
+                        self._p2p(send=(y, self.ranks[(vs + 1) % P]))
+                        self._drain_sends()
+            t = out.float().reshape(1).clone()
+            dist.all_reduce(t, group=self.e.pg.pp_group)
+            if self.e.pg.cp_group is not None:
+                dist.all_reduce(t, group=self.e.pg.cp_group)
+            return t[0]
         x_in = None
         if not self.is_first:
             x_in = self._empty(B, S)
@@ -251,6 +431,7 @@ class PipelineSchedule:
         out = self._forward(x_in, ids, labels, float(denom if denom is not None else labels.numel()))
         if not self.is_last:
             self._p2p(send=(out, self.next))
+            self._drain_sends()
             out = torch.zeros((), device=self.e.device)
         t = out.float().reshape(1).clone()
         dist.all_reduce(t, group=self.e.pg.pp_group)

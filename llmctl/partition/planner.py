@@ -272,7 +272,10 @@ class ParallelismPlanner:
             return 0.0
         return (n - 1) / n * nbytes / (bw_gbps * 1e9)
 
-    def step_time(self, tp, pp, dp, zs, mb, sp, ac, accum) -> Dict[str, float]:
+    def step_time(self, tp, pp, dp, zs, mb, sp, ac, accum, vs: int = 1) -> Dict[str, float]:
+        """``vs``: virtual stages per pipeline rank (interleaved 1F1B): the pipeline bubble
+        shrinks from (pp-1)/M to (pp-1)/(vs*M) of the compute, the stage-boundary p2p volume
+        grows vs-fold."""
         c = self.cfg
         tokens_per_rank = mb * self.seq_len * accum * pp  # pp: all micro-batches flow through every stage
         flops_rank = c.flops_per_token(self.seq_len) * tokens_per_rank / (tp * pp)
@@ -286,8 +289,8 @@ class ParallelismPlanner:
         eff = self.hw.gemm_efficiency * min((T / (T + 2048.0)) / (16384.0 / 18432.0), 1.05)
         compute = flops_rank / (self.hw.peak_flops * eff)
         M = accum * pp if pp > 1 else accum
-        bubble = (pp - 1) / (M + pp - 1) if pp > 1 else 0.0
-        compute_total = compute / (1 - bubble) if bubble < 1 else float("inf")
+        vs = max(int(vs), 1) if pp > 1 else 1
+        compute_total = compute * (1 + (pp - 1) / (vs * M)) if pp > 1 else compute
         # TP collectives: 4 per layer (2 fwd + 2 bwd) of the activation size, exposed
         act_bytes = mb * self.seq_len * c.hidden * 2.0
         tp_bw = self._link_bw(tp, 1)
@@ -298,7 +301,7 @@ class ParallelismPlanner:
         # PP p2p
         pp_time = 0.0
         if pp > 1:
-            pp_time = 2 * (M + pp - 1) * act_bytes / tp / (self._link_bw(2, tp * dp) * 1e9)
+            pp_time = 2 * (vs * M + pp - 1) * act_bytes / tp / (self._link_bw(2, tp * dp) * 1e9)
         # DP gradient sync (overlapped with backward except the last bucket)
         grad_bytes = self._stage_params(tp, pp) * 2.0
         dp_bw = self._link_bw(dp, tp)
@@ -337,23 +340,27 @@ class ParallelismPlanner:
                 for sp in ((False, True) if tp > 1 else (False,)):
                     for ac in ("none", "selective", "full"):
                         for mb in (1, 2, 4, 8, 16):
-                            out.append(dict(tp=tp, pp=pp, dp=dp, zs=zs, sp=sp, ac=ac, mb=mb))
+                            for vs in ((1, 2, 4) if pp > 1 and zs < 3 else (1,)):
+                                if vs > 1 and c.layers < pp * vs:
+                                    continue
+                                out.append(dict(tp=tp, pp=pp, dp=dp, zs=zs, sp=sp, ac=ac, mb=mb, vs=vs))
         return out
 
-    def evaluate(self, tp, pp, dp, zs, sp, ac, mb, global_batch: Optional[int] = None) -> Dict[str, Any]:
+    def evaluate(self, tp, pp, dp, zs, sp, ac, mb, global_batch: Optional[int] = None, vs: int = 1) -> Dict[str, Any]:
         if global_batch:
             accum = max(1, global_batch // (mb * dp * (pp if pp > 1 else 1)))
         else:
             accum = 1
         M = accum * pp if pp > 1 else accum
         mem = self.compute_memory_requirement(tp, pp, dp, zs, mb, sp, ac, M)
-        t = self.step_time(tp, pp, dp, zs, mb, sp, ac, accum)
+        t = self.step_time(tp, pp, dp, zs, mb, sp, ac, accum, vs)
         gbs = mb * dp * M
         tps = gbs * self.seq_len / t["total_s"]
         return dict(tensor_parallel=tp, pipeline_parallel=pp, data_parallel=dp, zero_stage=zs,
                     sequence_parallel=sp, activation_checkpoint=ac, micro_batch_size=mb,
                     expert_parallel=self.expert_parallel(dp),
                     global_batch_size=gbs, grad_accum=accum, num_microbatches=M,
+                    virtual_stages=vs if pp > 1 else 1,
                     estimated_memory_gb=round(mem, 3), estimated_comm_gb=round(t["comm_gb"], 3),
                     estimated_flops=self.estimate_flops(gbs), estimated_step_time_s=round(t["total_s"], 4),
                     estimated_tokens_per_sec=round(tps, 1),
@@ -385,7 +392,7 @@ class ParallelismPlanner:
         return best
 
     def manual_plan(self, tp: int, pp: int, zs: int, sp: bool = False, ac: str = "selective", mb: int = 1,
-                    global_batch: Optional[int] = None) -> Dict[str, Any]:
+                    global_batch: Optional[int] = None, vs: int = 1) -> Dict[str, Any]:
         n = self.hw.gpus
         dp = max(n // (tp * pp), 1)
-        return self.evaluate(tp, pp, dp, zs if dp > 1 else 0, sp and tp > 1, ac, mb, global_batch)
+        return self.evaluate(tp, pp, dp, zs if dp > 1 else 0, sp and tp > 1, ac, mb, global_batch, vs)

@@ -29,21 +29,26 @@ def split_layers(num_layers: int, pp: int) -> List[Tuple[int, int]]:
     return out
 
 
-def build_shard_map(model: Dict[str, Any], tp: int, pp: int, dp: int, zero_stage: int) -> Dict[str, Any]:
+def build_shard_map(model: Dict[str, Any], tp: int, pp: int, dp: int, zero_stage: int,
+                    virtual_stages: int = 1) -> Dict[str, Any]:
+    """Per-rank shard description.  With ``virtual_stages`` V > 1 (interleaved pipeline) the
+    layers are cut into pp*V chunks and pipeline rank p owns chunks p, p + pp, ... — its
+    ``layers`` entry then lists every [start, end) range it holds."""
     L = int(model.get("layers", 32))
     heads = int(model.get("heads", 32))
     kv = int(model.get("kv_heads", heads) or heads)
     ffn = int(model.get("ffn", 4 * int(model.get("hidden", 4096))))
     vocab = int(model.get("vocab_size", 32000))
     layout = ParallelLayout(tp * pp * dp, tp=tp, pp=pp, dp=dp)
-    stages = split_layers(L, pp)
+    V = max(int(virtual_stages), 1) if pp > 1 else 1
+    stages = split_layers(L, pp * V)
     ranks = []
     for r in range(layout.world_size):
         t, d, p = layout.coords(r)
-        lo, hi = stages[p]
+        mine = [list(stages[v * pp + p]) for v in range(V)]
         ranks.append({
             "rank": r, "tp_rank": t, "dp_rank": d, "pp_rank": p,
-            "layers": [lo, hi],
+            "layers": mine[0] if V == 1 else mine,
             "q_heads": [t * heads // tp, (t + 1) * heads // tp],
             "kv_heads": [t * kv // tp, (t + 1) * kv // tp],
             "ffn": [t * ffn // tp, (t + 1) * ffn // tp],
@@ -53,5 +58,6 @@ def build_shard_map(model: Dict[str, Any], tp: int, pp: int, dp: int, zero_stage
         })
     sm = layout.shard_map()
     sm["stages"] = [list(s) for s in stages]
+    sm["virtual_stages"] = V
     sm["ranks"] = ranks
     return sm

@@ -74,6 +74,7 @@ class TrainingConfig:
     zero_stage: int = 0
     activation_checkpoint: str = "none"  # none | selective | full
     num_microbatches: int = 0  # pipeline micro-batches per step (0 => 2*pp)
+    virtual_stages: int = 1  # interleaved pipeline: model chunks per pipeline rank (1 = plain 1F1B)
     bucket_mb: float = 256.0
     betas: Tuple[float, float] = (0.9, 0.95)
     eps: float = 1e-8
@@ -175,14 +176,25 @@ class TrainingEngine:
         # when the count does not divide; the planner's shard_map uses the same rule)
         from llmctl.partition.shard_map import split_layers
 
-        lo, hi = split_layers(L, pp)[pp_rank]
+        V = max(int(c.virtual_stages or 1), 1) if pp > 1 else 1
+        ranges = None
+        if V > 1:  # rank r owns virtual stages r, r + pp, ... (chunks of the pp*V-way split)
+            if L < pp * V:
+                raise ValueError(f"{L} layers cannot fill pipeline_parallel*virtual_stages = {pp * V} stages")
+            if c.zero_stage >= 3:
+                raise NotImplementedError("virtual pipeline stages with ZeRO-3 are not supported")
+            split = split_layers(L, pp * V)
+            ranges = [split[v * pp + pp_rank] for v in range(V)]
+            lo, hi = ranges[0][0], ranges[-1][1]
+        else:
+            lo, hi = split_layers(L, pp)[pp_rank]
         if mc.is_moe and pp > 1:
             # the pipeline stages compute only the LM loss: the router aux loss would be dropped
             raise NotImplementedError("MoE models with pipeline parallelism are not supported")
         pc = ParallelContext(
             tp_group=pg.tp_group, tp_size=pg.layout.tp, tp_rank=pg.tp_rank,
             sequence_parallel=c.sequence_parallel and pg.layout.tp > 1,
-            layer_start=lo, layer_end=hi, has_embedding=pp_rank == 0, has_head=pp_rank == pp - 1,
+            layer_start=lo, layer_end=hi, has_embedding=pp_rank == 0, has_head=pp_rank == pp - 1, layer_ranges=ranges,
             activation_checkpoint=c.activation_checkpoint,
             cp_group=pg.cp_group, cp_size=pg.layout.cp, cp_rank=pg.cp_rank, cp_mode=c.context_parallel_mode,
             ep_group=pg.ep_group, ep_size=pg.layout.ep, ep_rank=pg.ep_rank)
@@ -507,7 +519,7 @@ class TrainingEngine:
         named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
         with torch.no_grad():
             for n, p in named:
-                g = self._expert_global(_global_name(n, self.pc.layer_start))
+                g = self._expert_global(_global_name(n, self.pc.layer_index))
                 if g == "lm_head" and g not in full and self.model_config.tie_word_embeddings:
                     g = "embed"  # the last pipeline stage's copy of a tied matrix
                 t = shard_tp(g, full[g], self.pg.layout.tp, self.pg.tp_rank, self.model_config)
@@ -542,7 +554,7 @@ class TrainingEngine:
 
         self.optimizer.wait_params()
         named = self.zero3.full_named_parameters() if self.zero3 is not None else list(self.model.named_parameters())
-        local = {self._expert_global(_global_name(n, self.pc.layer_start)): p.detach().float().cpu() for n, p in named}
+        local = {self._expert_global(_global_name(n, self.pc.layer_index)): p.detach().float().cpu() for n, p in named}
         if self.zero3 is not None:
             self.zero3.release_all()
         if not dist.is_initialized():

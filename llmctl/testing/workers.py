@@ -54,6 +54,7 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
                   sequence_parallel=layout.get("sp", False),
                   activation_checkpoint=layout.get("ac", "none"),
                   num_microbatches=layout.get("microbatches", 0),
+                  virtual_stages=layout.get("vstages", 1),
                   context_parallel=layout.get("cp", 1),
                   context_parallel_mode=layout.get("cp_mode", "ulysses"),
                   expert_parallel=layout.get("ep", 1),

@@ -100,6 +100,24 @@ def test_pp2_tied_embeddings_matches_single():
     _close(out[0]["state"], ref["state"])
 
 
+@pytest.mark.parametrize("pp,vstages,micro", [(2, 2, 4), (2, 4, 2), (4, 2, 4)])
+def test_interleaved_pp_matches_single(pp, vstages, micro):
+    """Virtual pipeline stages (interleaved 1F1B): rank r owns chunks r, r+pp, ... of an
+    8-layer model; the trajectory equals one process accumulating the same micro-batches."""
+    ref = train_reference(STEPS, dp=1, model="tiny-deep", micro_per_rank=micro)
+    out = run_ranks(train_layout, pp, STEPS, {"pp": pp, "vstages": vstages, "microbatches": micro}, "tiny-deep")
+    _losses_close(out[0]["losses"], ref["losses"])
+    _losses_close([out[0]["eval"]], [ref["eval"]])
+    _close(out[0]["state"], ref["state"])
+
+
+def test_interleaved_pp2_dp2_zero1_matches_single():
+    ref = train_reference(STEPS, dp=2, model="tiny-deep", micro_per_rank=4)
+    out = run_ranks(train_layout, 4, STEPS, {"pp": 2, "vstages": 2, "zero": 1, "microbatches": 4}, "tiny-deep")
+    _losses_close(out[0]["losses"], ref["losses"])
+    _close(out[0]["state"], ref["state"])
+
+
 def test_pp2_tied_fresh_init_stays_tied():
     """From the engine's own init (no load_full_state_dict re-seeding the fp32 masters), the
     last stage's lm_head copy equals stage 0's embed after optimizer steps."""

@@ -125,3 +125,23 @@ def test_model_json_configs_load():
         cfg = get_model_config(str(f))
         d = json.loads(f.read_text())
         assert cfg.num_parameters() == d["estimated_params"], f.name
+
+
+def test_planner_virtual_stages_shrink_the_bubble():
+    """Interleaved pipeline: the planner's step time falls with virtual stages (bubble
+    (pp-1)/(vs*M)), the auto search may pick vs > 1, and the shard map lists each pipeline
+    rank's chunks (pp*vs-way layer split, rank p owns chunks p, p+pp, ...)."""
+    from llmctl.models import get_model_config
+    from llmctl.partition.planner import ParallelismPlanner
+    from llmctl.partition.shard_map import build_shard_map
+
+    cfg = get_model_config("llama-70b").to_dict()
+    hw = {"gpu": {"count": 8, "memory_gb": 288}}
+    pl = ParallelismPlanner(cfg, hw, seq_len=2048)
+    t1 = pl.evaluate(1, 4, 2, 1, False, "selective", 1, 64, vs=1)["estimated_step_time_s"]
+    t2 = pl.evaluate(1, 4, 2, 1, False, "selective", 1, 64, vs=2)["estimated_step_time_s"]
+    assert t2 < t1
+    sm = build_shard_map(cfg, 1, 4, 2, 1, virtual_stages=2)
+    assert sm["virtual_stages"] == 2 and len(sm["stages"]) == 8
+    r0 = [r for r in sm["ranks"] if r["pp_rank"] == 0][0]
+    assert r0["layers"] == [sm["stages"][0], sm["stages"][4]]
