@@ -158,7 +158,10 @@ at::Tensor skinny_linear_cfg(const at::Tensor& x, const at::Tensor& w, const c10
   const c10::DeviceGuard guard(x.device());
   auto y = at::empty({M, N}, x.options());
   int c = (int)config;
-  if (c == 0) c = 1;  // the original configuration (NT 1, GB 4 / 2, 8 waves)
+  // automatic choice from tools/skinny_sweep.py (profiles/skinny_sweep_r2.jsonl, uncached GPT-7B
+  // weights): 4 waves x 8 K-blocks each in flight (c3) everywhere except 5..16 tokens on the
+  // narrow projections, where 2 waves x 8 blocks (c7) wins
+  if (c == 0) c = (M > 4 && M <= 16 && N <= 4096) ? 7 : 3;
   const bool m1 = M <= 16;
   switch (c) {
     case 1: m1 ? launch_skinny<1, 1, 4, 8>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 2, 8>(x, w, bp, y, M, N, K); break;

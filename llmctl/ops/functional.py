@@ -361,16 +361,18 @@ def paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, s
 
 def decode_linear(x, w, b=None):
     """``x @ w^T (+ b)`` for decode-shaped inputs: the weight-streaming MFMA kernel
-    (``csrc/skinny_gemm.hip``) for the NARROW projections (out features <= 4096: o-proj,
-    down-proj, TP shards) where hipBLASLt's small-M kernels launch too few workgroups
-    (GPT-7B o-proj at M=16: 9.6 vs 18.6 us, ``profiles/decode_bench_r1.jsonl``); wide ones
-    (QKV, up, LM head) and anything over 16 tokens x 11008 stay on hipBLASLt via ``F.linear``.
+    (``csrc/skinny_gemm.hip``) where it beats hipBLASLt on uncached weights
+    (``profiles/skinny_sweep_r2.jsonl``): every projection at <= 4 tokens (GPT-7B QKV 21.9 vs
+    28.0 us, up 39.9 vs 53.2 us, LM head 54.4 vs 60.9 us at 1 token) and the NARROW ones
+    (out features <= 4096: o-proj, down-proj, TP shards) up to 32 tokens (o-proj at 16 tokens:
+    13.5 vs 22.0 us); wide projections at 5-32 tokens stay on hipBLASLt's small-M kernels.
     ``LLMCTL_SKINNY_GEMM=0`` / ``=all`` force the library / kernel path (A/B)."""
     mode = os.environ.get("LLMCTL_SKINNY_GEMM", "1")
-    if (mode != "0" and use_native(x) and x.dim() == 2 and x.shape[0] <= 32 and x.dtype == torch.bfloat16
+    M = x.shape[0] if x.dim() == 2 else 0
+    if (mode != "0" and use_native(x) and x.dim() == 2 and M <= 32 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and w.shape[0] % 16 == 0 and x.shape[1] % 128 == 0
             and x.is_contiguous() and w.is_contiguous() and (b is None or b.is_contiguous())
-            and (mode == "all" or (w.shape[0] <= 4096 and x.shape[0] * x.shape[1] <= 16 * 11008))):
+            and (mode == "all" or M <= 4 or (w.shape[0] <= 4096 and (M <= 16 or x.shape[1] <= 4096)))):
         return native().skinny_linear(x, w, b)
     return torch.nn.functional.linear(x, w, b)
 

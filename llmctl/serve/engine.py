@@ -250,11 +250,20 @@ class InferenceEngine:
 
     def _static(self, nb: int) -> Dict[str, torch.Tensor]:
         d = self.device
-        return {"ids": torch.zeros(nb, dtype=torch.long, device=d),
+        bufs = {"ids": torch.zeros(nb, dtype=torch.long, device=d),
                 "positions": torch.zeros(nb, dtype=torch.int32, device=d),
                 "slots": torch.full((nb,), -1, dtype=torch.long, device=d),
                 "block_tables": torch.zeros(nb, self.max_blocks_per_seq, dtype=torch.int32, device=d),
                 "ctx_lens": torch.ones(nb, dtype=torch.int32, device=d)}
+        # pinned host staging of the same inputs: one truly asynchronous H2D copy each per step
+        # (a non_blocking copy from pageable memory is synchronous)
+        pin = self.device.type == "cuda"
+        for k in ("ids", "positions", "slots", "block_tables", "ctx_lens"):
+            # initialised from the device defaults: rows past the live batch are copied too and
+            # must stay valid (block id 0, context 1) for the padded graph rows
+            h = bufs[k].to("cpu")
+            bufs["host_" + k] = h.pin_memory() if pin else h
+        return bufs
 
     def _capture(self, nb: int):
         bufs = self._static(nb)
@@ -299,13 +308,18 @@ class InferenceEngine:
             if nb not in self._graphs:
                 self._capture(nb)
             g, b = self._graphs[nb]
-            b["ids"][:n].copy_(torch.tensor(ids), non_blocking=True)
-            b["positions"][:n].copy_(torch.tensor(positions, dtype=torch.int32), non_blocking=True)
-            b["slots"].fill_(-1)
-            b["slots"][:n].copy_(torch.tensor(slots), non_blocking=True)
-            b["block_tables"][:n].copy_(torch.from_numpy(bt), non_blocking=True)
-            b["ctx_lens"].fill_(1)
-            b["ctx_lens"][:n].copy_(torch.tensor(ctx, dtype=torch.int32), non_blocking=True)
+            # the previous step's copies out of these pinned buffers completed before its
+            # sampled ids were read back (host sync per step), so they can be refilled here
+            h = {k: b["host_" + k].numpy() for k in ("ids", "positions", "slots", "block_tables", "ctx_lens")}
+            h["ids"][:n] = ids
+            h["positions"][:n] = positions
+            h["slots"][:] = -1
+            h["slots"][:n] = slots
+            h["block_tables"][:n] = bt
+            h["ctx_lens"][:] = 1
+            h["ctx_lens"][:n] = ctx
+            for k in ("ids", "positions", "slots", "block_tables", "ctx_lens"):
+                b[k].copy_(b["host_" + k], non_blocking=True)
             g.replay()
             self.stats["graph_replays"] += 1
             return b["logits"][:n]

@@ -93,6 +93,13 @@ class TPInferenceEngine(InferenceEngine):
 
     def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
         n, vl = logits.shape
+        if self.car is not None and logits.dtype == torch.bfloat16 and self.tp_size * n * vl * 2 <= self.car.max_bytes:
+            # all-gather as a sum of zero-padded slots through the one-shot IPC kernel: unlike the
+            # RCCL / gloo all-gather it is hipGraph-capturable in every backend configuration
+            buf = torch.zeros(self.tp_size, n, vl, dtype=logits.dtype, device=logits.device)
+            buf[self.tp_rank].copy_(logits)
+            self.car.all_reduce(buf)
+            return buf.permute(1, 0, 2).reshape(n, self.tp_size * vl)
         out = torch.empty(self.tp_size * n, vl, dtype=logits.dtype, device=logits.device)
         dist.all_gather_into_tensor(out, logits.contiguous(), group=self.tp_group)
         return out.view(self.tp_size, n, vl).permute(1, 0, 2).reshape(n, self.tp_size * vl)

@@ -143,6 +143,50 @@ def serve_generate(rank: int, world: int, max_tokens: int = 8) -> dict:
     return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": eng.kv_cache.k.shape[-2]}
 
 
+def serve_generate_gpu(rank: int, world: int, max_tokens: int = 8) -> dict:
+    """GPU serving with TP=world ranks sharing cuda:0 (gloo control/data plane; RCCL cannot put
+    two ranks on one device): the decode step, including the custom IPC all-reduces and the
+    vocab gather, is captured in a hipGraph and replayed.  world == 1: the plain engine."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from llmctl.serve.scheduler import SamplingParams
+
+    torch.cuda.set_device(0)
+    kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=64, block_size=16, max_model_len=256,
+              max_batch_tokens=512, seed=0, use_graphs=True)
+    prompts = PROMPTS + [[(5 * i) % 500 + 1 for i in range(40)]]
+    if world == 1:
+        from llmctl.serve.engine import InferenceEngine
+
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            os.environ.pop(k, None)
+        eng = InferenceEngine("tiny", **kw)
+    else:
+        from llmctl.serve.tp import TPInferenceEngine
+
+        dist.init_process_group("gloo")
+        eng = TPInferenceEngine("tiny", **kw)
+        assert eng.car is not None, "custom all-reduce not active"
+        if eng.tp_rank != 0:
+            eng.worker_loop()
+            eng.release_graphs()
+            dist.barrier()
+            eng.car.close()
+            return {}
+    seqs = eng.generate(prompts, SamplingParams(max_tokens=max_tokens, temperature=0.0))
+    out = {"tokens": [s.output_ids for s in seqs], "graph_replays": eng.stats["graph_replays"]}
+    if world > 1:
+        eng.stop_workers()
+        eng.release_graphs()
+        eng.car.check()
+        dist.barrier()
+        eng.car.close()
+    return out
+
+
 def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters: int = 20) -> dict:
     """Two+ processes sharing one GPU: the IPC one-shot all-reduce must equal the sum of the
     inputs (exact fp32 sum, bf16 output) over many calls (epoch parity) and under hipGraph

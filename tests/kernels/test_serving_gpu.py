@@ -161,3 +161,21 @@ def test_prefix_cache_and_preemption_gpu(native_lib):
     ref = InferenceEngine("tiny", prefix_caching=False, **kw)
     assert seq.output_ids == ref.generate([base[:40]], p)[0].output_ids
     assert s2.output_ids == ref.generate([base + [9, 9]], p)[0].output_ids
+
+
+def test_tp2_serving_two_processes_custom_ar_graphs(native_lib):
+    """TP=2 serving on the GPU code path: two processes share cuda:0 (gloo process group),
+    every decode step — per-layer custom IPC all-reduces and the vocab-shard gather — runs
+    inside a captured hipGraph.  Greedy tokens vs the TP=1 engine: bf16 partial sums are
+    rounded per rank before the reduction, so demand the first token of every prompt and
+    >= 90 % of all tokens to agree."""
+    from llmctl.testing.harness import run_ranks
+    from llmctl.testing.workers import serve_generate_gpu
+
+    ref = serve_generate_gpu(0, 1)
+    out = run_ranks(serve_generate_gpu, 2, timeout=300)
+    assert out[0]["graph_replays"] > 0
+    a, b = out[0]["tokens"], ref["tokens"]
+    assert [x[0] for x in a] == [y[0] for y in b]
+    agree = sum(int(x == y) for p, q in zip(a, b) for x, y in zip(p, q))
+    assert agree / sum(len(p) for p in b) >= 0.9, (a, b)
