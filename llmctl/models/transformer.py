@@ -61,6 +61,7 @@ class ParallelContext:
     cp_size: int = 1
     cp_rank: int = 0
     cp_mode: str = "ulysses"
+    cp_zigzag: bool = False  # ring mode: rank r holds pieces r and 2cp-1-r of the sequence
     # expert parallel (MoE models; llmctl.models.moe): all-to-all group of ep_size DP ranks
     ep_group: Optional[object] = None
     ep_size: int = 1
@@ -188,7 +189,7 @@ class DecoderLayer(nn.Module):
         k = k.view(B, S, self.nkv, self.D)
         v = v.view(B, S, self.nkv, self.D)
         if self.pc.cp_size > 1 and self.pc.cp_mode == "ring":  # K/V chunks around the CP ring
-            o = cp.ring_attention(q, k, v, self.pc.cp_group)
+            o = cp.ring_attention(q, k, v, self.pc.cp_group, zigzag=self.pc.cp_zigzag)
         elif self.pc.cp_size > 1:  # sequence chunk, all heads <-> all tokens, head chunk
             g = self.pc.cp_group
             o = cp.head_to_seq(ops.flash_attention(cp.seq_to_head(q, g), cp.seq_to_head(k, g),
@@ -313,8 +314,9 @@ class DecoderLM(nn.Module):
         if self.pos_embed is not None:
             if positions is not None:  # explicit (e.g. per-document) positions
                 pos = self.pos_embed[positions.long()]
-            elif pc.cp_size > 1:  # this rank's chunk of the sequence: global positions
-                pos = self.pos_embed[pc.cp_rank * S:(pc.cp_rank + 1) * S].repeat(B, 1)
+            elif pc.cp_size > 1:  # this rank's part of the sequence: global positions
+                pos = self.pos_embed[cp.local_positions(B, S, pc.cp_rank, ids.device, pc.cp_size,
+                                                        pc.cp_zigzag).long()]
             else:
                 pos = self.pos_embed[:S].repeat(B, 1)
             if pc.tp_size > 1 and pc.sequence_parallel:
@@ -325,7 +327,7 @@ class DecoderLM(nn.Module):
     def run_layers(self, x, B, S, residual=None, positions=None, doc_start=None, chunk: Optional[int] = None):
         """Run the local decoder layers (only model chunk ``chunk`` under virtual stages)."""
         if self.pc.cp_size > 1 and positions is None:
-            positions = cp.local_positions(B, S, self.pc.cp_rank, x.device)
+            positions = cp.local_positions(B, S, self.pc.cp_rank, x.device, self.pc.cp_size, self.pc.cp_zigzag)
         if doc_start is not None and positions is None:  # packed documents: RoPE restarts per document
             positions = (torch.arange(S, device=x.device, dtype=torch.int32).view(1, S) - doc_start).reshape(-1)
         rope = self.rope_tables(S * self.pc.cp_size, x.device)

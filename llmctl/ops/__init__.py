@@ -20,6 +20,7 @@ from .functional import (
     layernorm,
     paged_attention_decode,
     paged_prefill_attention,
+    attn_merge_,
     prefill_work_list,
     rmsnorm,
     rope_qkv,
@@ -32,6 +33,6 @@ from .functional import (
 __all__ = [
     "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy", "decode_linear",
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
-    "paged_prefill_attention", "prefill_work_list",
+    "paged_prefill_attention", "prefill_work_list", "attn_merge_",
     "rmsnorm", "rope_qkv", "rope_qkv_cache", "sample", "swiglu", "transpose_",
 ]

@@ -40,6 +40,7 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("fa_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor delta, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int abl) -> ()");
   // serving (paged_attn.hip, sampling.hip)
   m.def("kv_cache_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot_mapping) -> ()");
+  m.def("attn_merge_(Tensor(a!) o_acc, Tensor(b!) lse_acc, Tensor o_j, Tensor lse_j) -> ()");
   m.def("paged_prefill_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor work, float scale) -> Tensor");
   m.def("paged_attention_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, float scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w, Tensor? bias) -> Tensor");

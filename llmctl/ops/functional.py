@@ -334,6 +334,14 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scal
     return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale)
 
 
+def attn_merge_(o_acc, lse_acc, o_j, lse_j) -> None:
+    """Merge a partial attention output into an fp32 accumulator by log-sum-exp (in place)."""
+    if use_native(o_acc):
+        native().attn_merge_(o_acc, lse_acc, o_j, lse_j)
+    else:
+        ref.attn_merge_(o_acc, lse_acc, o_j, lse_j)
+
+
 def prefill_work_list(cu_q, q_block: int = 128) -> List[int]:
     """(sequence << 16) | q-block items for ``paged_prefill_attention``, heaviest (longest
     causal span: the last q-blocks of long chunks) first."""
@@ -387,5 +395,5 @@ __all__ = [
     "transpose_",
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample", "decode_linear", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list",
+    "sample", "decode_linear", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
 ]

@@ -212,6 +212,17 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scal
     return out
 
 
+def attn_merge_(o_acc, lse_acc, o_j, lse_j) -> None:
+    """In-place log-sum-exp merge: o_acc [B,S,H,D] fp32 / lse_acc [B,H,S] fp32 absorb the
+    partial (o_j, lse_j); a fresh accumulator is (0, -inf)."""
+    ln = torch.logaddexp(lse_acc, lse_j)
+    dead = torch.isinf(ln) & (ln < 0)
+    wa = torch.where(dead, torch.zeros_like(ln), torch.exp(lse_acc - ln)).transpose(1, 2).unsqueeze(-1)
+    wj = torch.where(dead, torch.zeros_like(ln), torch.exp(lse_j - ln)).transpose(1, 2).unsqueeze(-1)
+    o_acc.mul_(wa).add_(o_j.float() * wj)
+    lse_acc.copy_(ln)
+
+
 def paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale: float):
     """Packed new tokens q [T, Hq, D] of N sequences (rows cu_q[n]:cu_q[n+1]) attending, causally,
     every cached key of their sequence: after the chunk's cache write sequence n holds

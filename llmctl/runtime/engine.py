@@ -197,6 +197,7 @@ class TrainingEngine:
             layer_start=lo, layer_end=hi, has_embedding=pp_rank == 0, has_head=pp_rank == pp - 1, layer_ranges=ranges,
             activation_checkpoint=c.activation_checkpoint,
             cp_group=pg.cp_group, cp_size=pg.layout.cp, cp_rank=pg.cp_rank, cp_mode=c.context_parallel_mode,
+            cp_zigzag=self._cp_zigzag(),
             ep_group=pg.ep_group, ep_size=pg.layout.ep, ep_rank=pg.ep_rank)
         # identical init on every DP replica (seeded; TP ranks get different shards, so
         # their seeds differ by tp_rank/pp_rank only)
@@ -399,11 +400,16 @@ class TrainingEngine:
         self.consumed_samples += sum(b[0].shape[0] for b in batches) * self.pg.layout.dp
         return {"loss": loss, "grad_norm": gnorm, "lr": torch.tensor(lr)}
 
+    def _cp_zigzag(self) -> bool:
+        from llmctl.parallel.context_parallel import zigzag_enabled
+
+        return self.pg.layout.cp > 1 and self.config.context_parallel_mode == "ring" and zigzag_enabled()
+
     def _cp_split(self, batches):
         from llmctl.parallel.context_parallel import split_sequence
 
-        cpn, r = self.pg.layout.cp, self.pg.cp_rank
-        return [(split_sequence(x, cpn, r), split_sequence(y, cpn, r)) for x, y in batches]
+        cpn, r, z = self.pg.layout.cp, self.pg.cp_rank, self._cp_zigzag()
+        return [(split_sequence(x, cpn, r, z), split_sequence(y, cpn, r, z)) for x, y in batches]
 
     @torch.no_grad()
     def evaluate(self, batches) -> float:

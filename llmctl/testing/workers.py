@@ -324,8 +324,8 @@ def zero3_pp_tied_error(rank: int, world: int) -> dict:
     return {"error": ""}
 
 
-def ring_attention_check(rank: int, world: int, B: int = 2, S: int = 48, Hq: int = 4, Hkv: int = 2,
-                         D: int = 16) -> dict:
+def ring_attention_check(rank: int, world: int, zigzag: bool = False, B: int = 2, S: int = 48, Hq: int = 4,
+                         Hkv: int = 2, D: int = 16) -> dict:
     """Ring attention over a ``world``-rank CP group vs full causal attention (fp32, gloo):
     returns this rank's output / gradient chunks and the oracle's."""
     import torch.distributed as dist
@@ -342,9 +342,9 @@ def ring_attention_check(rank: int, world: int, B: int = 2, S: int = 48, Hq: int
     scale = D ** -0.5
     o_full, lse = ref.attention_fwd(q, k, v, scale, True)
     dq_full, dk_full, dv_full = ref.attention_bwd(do, q, k, v, o_full, lse, scale, True)
-    ql, kl, vl = (split_sequence(t, world, rank).requires_grad_(True) for t in (q, k, v))
-    o = ring_attention(ql, kl, vl, None if world == 1 else dist.group.WORLD, scale)
-    o.backward(split_sequence(do, world, rank))
-    ch = lambda t: split_sequence(t, world, rank)  # noqa: E731
+    ch = lambda t: split_sequence(t, world, rank, zigzag)  # noqa: E731
+    ql, kl, vl = (ch(t).requires_grad_(True) for t in (q, k, v))
+    o = ring_attention(ql, kl, vl, None if world == 1 else dist.group.WORLD, scale, zigzag=zigzag)
+    o.backward(ch(do))
     return {"o": o.detach(), "dq": ql.grad, "dk": kl.grad, "dv": vl.grad,
             "o_ref": ch(o_full), "dq_ref": ch(dq_full), "dk_ref": ch(dk_full), "dv_ref": ch(dv_full)}

@@ -177,7 +177,15 @@ def test_cp2_ulysses_matches_single(ref_dp1):
 
 
 def test_cp2_ring_matches_single(ref_dp1):
-    """Ring attention: K/V chunks (and their dK/dV) travel around the CP ring."""
+    """Ring attention (zigzag pieces, the default): K/V chunks travel around the CP ring."""
+    out = run_ranks(train_layout, 2, STEPS, {"cp": 2, "cp_mode": "ring"})
+    _losses_close(out[0]["losses"], ref_dp1["losses"])
+    _losses_close([out[0]["eval"]], [ref_dp1["eval"]])
+    _close(out[0]["state"], ref_dp1["state"])
+
+
+def test_cp2_ring_contiguous_matches_single(ref_dp1, monkeypatch):
+    monkeypatch.setenv("LLMCTL_CP_ZIGZAG", "0")
     out = run_ranks(train_layout, 2, STEPS, {"cp": 2, "cp_mode": "ring"})
     _losses_close(out[0]["losses"], ref_dp1["losses"])
     _close(out[0]["state"], ref_dp1["state"])
@@ -190,11 +198,13 @@ def test_cp2_dp2_zero1_matches_single(ref_dp2):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_ring_attention_matches_full_attention(world):
-    """Ring attention (fwd + bwd, GQA) over 2 / 3 CP ranks equals full causal attention."""
+@pytest.mark.parametrize("zigzag", [False, True])
+def test_ring_attention_matches_full_attention(world, zigzag):
+    """Ring attention (fwd + bwd, GQA) over 2 / 3 CP ranks equals full causal attention, with
+    contiguous chunks and with the load-balanced zigzag pieces."""
     from llmctl.testing.workers import ring_attention_check
 
-    out = run_ranks(ring_attention_check, world)
+    out = run_ranks(ring_attention_check, world, zigzag)
     for r in range(world):
         for name in ("o", "dq", "dk", "dv"):
             assert torch.allclose(out[r][name], out[r][name + "_ref"], atol=2e-5, rtol=1e-4), (r, name)

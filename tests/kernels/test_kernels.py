@@ -484,3 +484,24 @@ def test_rope_qkv_cache_fused_write(native_lib, with_pos):
     native_lib.kv_cache_write(k2, v2, kc2, vc2, slots)
     assert torch.equal(q, q2) and torch.equal(k, k2) and torch.equal(v, v2)
     assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_attn_merge_matches_ref(native_lib, D):
+    """LSE merge of ring-attention partials (HIP) vs the torch oracle, including rows where the
+    accumulator is still empty (-inf) and rows where the partial saw no key (-inf)."""
+    B, S, H = 2, 96, 4
+    g = torch.Generator(device=DEV).manual_seed(3)
+    o_acc = torch.randn(B, S, H, D, generator=g, device=DEV)
+    lse_acc = torch.randn(B, H, S, generator=g, device=DEV)
+    lse_acc[0, :, :10] = float("-inf")
+    o_acc[0, :10] = 0.0
+    o_j = torch.randn(B, S, H, D, generator=g, device=DEV).to(torch.bfloat16)
+    lse_j = torch.randn(B, H, S, generator=g, device=DEV)
+    lse_j[1, :, 5:9] = float("-inf")
+    a, la = o_acc.clone(), lse_acc.clone()
+    native_lib.attn_merge_(a, la, o_j, lse_j)
+    b, lb = o_acc.clone(), lse_acc.clone()
+    ref.attn_merge_(b, lb, o_j, lse_j)
+    assert torch.allclose(la, lb, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
