@@ -283,13 +283,27 @@ def _bench_compute(duration: float) -> Dict[str, Any]:
     return {"device": "cpu", "dtype": "fp32", "tflops": round(2 * n ** 3 * it / (time.perf_counter() - t0) / 1e12, 3)}
 
 
-def _bench_network() -> Dict[str, Any]:
+def _bench_network(ranks: int = 0, backend: str = "auto", sizes=(2 ** 20, 2 ** 24, 2 ** 28),
+                   patterns=("allreduce", "allgather", "reduce_scatter"), iters: int = 10) -> Dict[str, Any]:
+    """xGMI / RCCL collective bandwidth measured in-process: one spawned rank per visible GPU
+    (RCCL), each pattern at 1 MiB / 16 MiB / 256 MiB; reports bus bandwidth per size (the
+    reference only printed a constant, ``llmctl/cli/commands/hw.py:344-345``).  With fewer
+    than two GPUs it is skipped, unless ``backend="gloo"`` rehearses the same path on CPU."""
     import torch
 
+    from llmctl.benchmarks.comms import run_comms_benchmark
+
     n = torch.cuda.device_count() if torch.cuda.is_available() else 0
-    if n < 2:
-        return {"status": "skipped", "reason": f"{n} GPU(s) visible; use `llmctl bench comms` under torchrun"}
-    return {"status": "use `llmctl bench comms --ranks N` (one process per GPU)"}
+    if backend != "gloo" and n < 2:
+        return {"status": "skipped", "reason": f"{n} GPU(s) visible: xGMI needs >= 2 (or `llmctl bench comms` "
+                                               f"under torchrun across nodes)"}
+    world = ranks or (n if backend != "gloo" else 2)
+    res = {"status": "ok", "ranks": world, "backend": "nccl(RCCL)" if backend != "gloo" else "gloo", "results": []}
+    for pat in patterns:
+        for sz in sizes:
+            r = run_comms_benchmark(pat, sz, world, iters, backend if backend != "auto" else "auto")
+            res["results"].append({k: r.get(k) for k in ("pattern", "bytes", "time_ms", "algbw_gbps", "busbw_gbps")})
+    return res
 
 
 @app.command()

@@ -22,7 +22,8 @@ DTYPES = {"float32": "float32", "float16": "float16", "bfloat16": "bfloat16", "f
 
 @app.command()
 def kernels(
-    kernel_type: str = typer.Option("matmul", help="Kernel type to tune (matmul, attention, all)"),
+    kernel_type: str = typer.Option("matmul", help="Kernel type to tune (matmul, attention, all; GPU HIP knobs: "
+                                    "gemm64, decode-splits, fa-split, skinny, hip = all four)"),
     matrix_size: str = typer.Option("1024x1024x1024", help="Matrix size for matmul (MxKxN)"),
     seq_len: int = typer.Option(512, help="Sequence length for attention"),
     batch_size: int = typer.Option(8, help="Batch size for attention"),
@@ -54,9 +55,44 @@ def kernels(
         r = tuner.tune_attention(seq_len, head_dim, batch_size, num_heads, device)
         console.print(f"[green]Attention tuning completed: best {r.best_config} "
                       f"{r.best_performance * 1e3:.3f} ms ({r.improvement:.1f}%)[/green]")
+    _tune_hip_knobs(tuner, kernel_type, matrix_size, seq_len, batch_size, num_heads, head_dim, device)
     if save_results:
         tuner.save_results(str(save_results))
     console.print("[green]✓ Kernel tuning completed successfully![/green]")
+
+
+def _tune_hip_knobs(tuner, kind: str, matrix_size: str, seq_len: int, batch_size: int, num_heads: int, head_dim: int,
+                    device: str) -> dict:
+    """HIP kernel knobs (GPU only) whose winners TrainingEngine / InferenceEngine dispatch when
+    given the saved tuning cache (``llmctl.plugins.tuning_cache``)."""
+    import torch
+
+    out = {}
+    if kind not in ("gemm64", "decode-splits", "fa-split", "skinny", "hip"):
+        return out
+    if not torch.cuda.is_available() or device == "cpu":
+        console.print("[yellow]HIP kernel knobs need a GPU: skipped[/yellow]")
+        return out
+    m, k, n = map(int, matrix_size.lower().split("x"))
+    if kind in ("gemm64", "hip"):
+        for layout in ("dgrad", "wgrad"):
+            r = tuner.tune_gemm64(m, n, k, layout, device)
+            out[f"gemm64_{layout}"] = r.best_config
+            console.print(f"[green]gemm64 {layout} {m}x{n}x{k}: best {r.best_config} "
+                          f"{r.best_performance * 1e3:.3f} ms[/green]")
+    if kind in ("decode-splits", "hip"):
+        r = tuner.tune_decode_splits(batch_size, seq_len, num_heads, num_heads, head_dim, device)
+        out["decode_splits"] = r.best_config
+        console.print(f"[green]decode splits {batch_size}x{seq_len}: best {r.best_config}[/green]")
+    if kind in ("fa-split", "hip"):
+        r = tuner.tune_fa_split(batch_size, seq_len, num_heads, head_dim, device)
+        out["fa_split"] = r.best_config
+        console.print(f"[green]flash-attn split {batch_size}x{seq_len}: best {r.best_config}[/green]")
+    if kind in ("skinny", "hip"):
+        r = tuner.tune_skinny(batch_size, n, k, device)
+        out["skinny"] = r.best_config
+        console.print(f"[green]decode GEMM {batch_size}x{n}x{k}: best {r.best_config}[/green]")
+    return out
 
 
 @app.command()
@@ -111,7 +147,9 @@ def full(
     console.print("[blue]3/3 Tuning communication...[/blue]")
     r = tuner.tune_communication((1024, 1024))
     summary["communication"] = {"improvement": r.improvement, "best_config": r.best_config, "time": r.total_time}
-    (output_dir / "full_tuning_results.json").write_text(json.dumps(summary, indent=2))
+    # GPU: the HIP kernel knobs on GPT-7B shapes (consumed via the saved tuning cache)
+    summary.update(_tune_hip_knobs(tuner, "hip", "24576x4096x12288", 2048, 16, 32, 128, device))
+    (output_dir / "full_tuning_results.json").write_text(json.dumps(summary, indent=2, default=str))
     tuner.save_results(str(output_dir / "tuning_cache.json"))
     console.print("\n[green]✓ Comprehensive auto-tuning completed![/green]")
     for comp, res in summary.items():

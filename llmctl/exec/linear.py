@@ -36,8 +36,15 @@ import torch.nn.functional as F
 
 
 # gemm64_ex config: tile-order group 4, schedule variant 1 (DMA issued in the read section)
-# — the fastest of the A/B in profiles/gemm64_variants_r2.jsonl on every GPT-7B shape
+# — the fastest of the A/B in profiles/gemm64_variants_r2.jsonl on every GPT-7B shape.  A
+# tuning cache (llmctl.plugins.tuning_cache) can override it per layout or per exact shape.
 GEMM64_CONFIG = int(os.environ.get("LLMCTL_GEMM64_CONFIG", "104"))
+GEMM64_CONFIGS = {"dgrad": GEMM64_CONFIG, "wgrad": GEMM64_CONFIG}
+GEMM64_SHAPE_CONFIGS: dict = {}  # (layout, M, N, K) -> config
+
+
+def gemm64_config(layout: str, M: int, N: int, K: int) -> int:
+    return GEMM64_SHAPE_CONFIGS.get((layout, M, N, K), GEMM64_CONFIGS.get(layout, GEMM64_CONFIG))
 
 
 def _gemm64_enabled() -> bool:
@@ -80,7 +87,8 @@ def dgrad64(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     from llmctl.ops._lib import native
 
     dx = torch.empty(dy2.shape[0], w.shape[1], dtype=dy2.dtype, device=dy2.device)
-    native().gemm64_ex(dy2, w, dx, False, True, False, GEMM64_CONFIG)
+    cfg = gemm64_config("dgrad", dy2.shape[0], w.shape[1], w.shape[0])
+    native().gemm64_ex(dy2, w, dx, False, True, False, cfg)
     return dx
 
 
@@ -112,7 +120,7 @@ def wgrad_into(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate:
     if (_gemm64_ok(M, N, K, g, dy2, x2) and K * dy2.stride(0) * 2 < 2**31 and K * x2.stride(0) * 2 < 2**31):
         from llmctl.ops._lib import native
 
-        native().gemm64_ex(dy2, x2, g, True, True, accumulate, GEMM64_CONFIG)
+        native().gemm64_ex(dy2, x2, g, True, True, accumulate, gemm64_config("wgrad", M, N, K))
     elif _gemm_ex_ok(g, dy2, x2):
         from llmctl.ops._lib import native
 

@@ -24,6 +24,8 @@
 //     q-block is split over two workgroups that write fp32 partial outputs + LSEs, merged by a
 //     combine kernel — halves the critical path of the causal tail.
 // Outputs O [B,S,Hq,HD] bf16 and LSE [B,Hq,S] fp32 (natural log) for the backward pass.
+#include <cstdlib>
+
 #include "attn_common.h"
 
 namespace llmctl {
@@ -338,8 +340,13 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   auto s = stream();
   // a grid that the CUs hold in one residency round (2 workgroups per CU) finishes when its
   // heaviest causal block does: split every block's K/V range over two workgroups
-  const bool split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 4 &&
-                     (long)B * Hq * nqb <= 2L * num_cus();
+  bool split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 4 &&
+               (long)B * Hq * nqb <= 2L * num_cus();
+  // LLMCTL_FA_SPLIT=0 / =1 override the heuristic (autotuner knob, llmctl.plugins.autotuning)
+  if (const char* e = std::getenv("LLMCTL_FA_SPLIT")) {
+    if (e[0] == '0') split = false;
+    else if (e[0] == '1') split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 2;
+  }
   if (split) {
     auto o_part = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
     auto lse_part = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));

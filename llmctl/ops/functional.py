@@ -367,6 +367,9 @@ def paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, s
     return ref.paged_prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale)
 
 
+SKINNY_CONFIGS: dict = {}  # (M, N, K) -> tuned config (0 = hipBLASLt), from a tuning cache
+
+
 def decode_linear(x, w, b=None):
     """``x @ w^T (+ b)`` for decode-shaped inputs: the weight-streaming MFMA kernel
     (``csrc/skinny_gemm.hip``) where it beats hipBLASLt on uncached weights
@@ -377,6 +380,12 @@ def decode_linear(x, w, b=None):
     ``LLMCTL_SKINNY_GEMM=0`` / ``=all`` force the library / kernel path (A/B)."""
     mode = os.environ.get("LLMCTL_SKINNY_GEMM", "1")
     M = x.shape[0] if x.dim() == 2 else 0
+    tuned = SKINNY_CONFIGS.get((M, w.shape[0], w.shape[1])) if SKINNY_CONFIGS and x.dim() == 2 else None
+    if tuned is not None and mode == "1" and use_native(x):
+        if tuned == 0:
+            return torch.nn.functional.linear(x, w, b)
+        if x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype == torch.bfloat16:
+            return native().skinny_linear_cfg(x, w, b, tuned)
     if (mode != "0" and use_native(x) and x.dim() == 2 and M <= 32 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and w.shape[0] % 16 == 0 and x.shape[1] % 128 == 0
             and x.is_contiguous() and w.is_contiguous() and (b is None or b.is_contiguous())

@@ -10,7 +10,13 @@ reference's knobs were mostly no-ops and its comm tuning was a random-number sim
 * Attention: implementation (llmctl flash-attn HIP kernel / torch SDPA / eager), causal;
 * Communication: bucket size and op (all-reduce vs reduce-scatter+all-gather) measured on
   the live process group (RCCL on GPU, gloo on CPU); without a process group it measures
-  the local chunked copy path and says so in the result (``mode: "local"``).
+  the local chunked copy path and says so in the result (``mode: "local"``);
+* HIP kernel knobs (round 2): the gemm64 tile-order group / schedule variant per GEMM
+  layout (``Gemm64Tuner``), the paged-decode context split count (``DecodeSplitTuner``), the
+  flash-attention forward K/V split (``FlashSplitTuner``) and the decode-GEMM configuration
+  (``SkinnyTuner``).  ``save_results`` writes ``tuning_cache.json``; TrainingEngine /
+  InferenceEngine read it back through :mod:`llmctl.plugins.tuning_cache` and dispatch the
+  tuned configurations.
 
 ``max_iterations``, ``warmup`` and ``measurement`` iterations and ``tolerance`` are all
 honoured (the reference read only ``timeout``/``tolerance``).
@@ -219,6 +225,162 @@ class CommunicationTuner(Tunable):
         return _time(fn, self.dev, max(1, config.warmup_iterations // 2), config.measurement_iterations)
 
 
+class _EnvKnob:
+    """Set an environment knob for the duration of one measurement."""
+
+    def __init__(self, name: str, value: Optional[str]):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        import os
+
+        self.prev = os.environ.get(self.name)
+        if self.value is None:
+            os.environ.pop(self.name, None)
+        else:
+            os.environ[self.name] = self.value
+
+    def __exit__(self, *a):
+        import os
+
+        if self.prev is None:
+            os.environ.pop(self.name, None)
+        else:
+            os.environ[self.name] = self.prev
+
+
+class Gemm64Tuner(Tunable):
+    """gemm64_ex configuration (tile-order group + 100 * schedule variant) for one GEMM of a
+    linear layer: ``layout`` fwd (x W^T), dgrad (dy W) or wgrad (dy^T x) with M tokens."""
+
+    LAYOUTS = {"fwd": (False, False), "dgrad": (False, True), "wgrad": (True, True)}
+
+    def __init__(self, M: int, N: int, K: int, layout: str = "dgrad", device: str = "auto"):
+        self.M, self.N, self.K, self.layout = M, N, K, layout
+        self.dev = _dev(device)
+
+    def get_parameter_space(self):
+        return {"config": [4, 8, 104, 108, 204, 304]}
+
+    def validate_parameters(self, p):
+        return self.dev.type == "cuda" and self.M % 256 == 0 and self.N % 256 == 0 and self.K % 128 == 0
+
+    def set_parameters(self, params):
+        self.params = params
+        at, bt = self.LAYOUTS[self.layout]
+        g = torch.Generator(device="cpu").manual_seed(0)
+        A = (torch.rand(self.M, self.K, generator=g) * 2 - 1).to(self.dev, torch.bfloat16)
+        B = (torch.rand(self.N, self.K, generator=g) * 2 - 1).to(self.dev, torch.bfloat16)
+        self.a = A.t().contiguous() if at else A
+        self.b = B.t().contiguous() if bt else B
+        self.out = torch.empty(self.M, self.N, device=self.dev, dtype=torch.bfloat16)
+        self.flags = (at, bt)
+
+    def benchmark(self, config):
+        from llmctl.ops import _lib
+
+        ops = _lib.native()
+        c = int(self.params["config"])
+        fn = lambda: ops.gemm64_ex(self.a, self.b, self.out, self.flags[0], self.flags[1], False, c)  # noqa: E731
+        return _time(fn, self.dev, config.warmup_iterations, config.measurement_iterations)
+
+
+class DecodeSplitTuner(Tunable):
+    """Paged-attention decode: context splits per (sequence, kv-head) (``LLMCTL_DECODE_SPLITS``)."""
+
+    def __init__(self, batch: int, ctx: int, heads: int = 32, kv_heads: int = 32, head_dim: int = 128,
+                 block_size: int = 16, device: str = "auto"):
+        self.N, self.ctx, self.H, self.Hkv, self.D, self.bs = batch, ctx, heads, kv_heads, head_dim, block_size
+        self.dev = _dev(device)
+
+    def get_parameter_space(self):
+        return {"splits": [1, 2, 4, 8, 16]}
+
+    def validate_parameters(self, p):
+        return self.dev.type == "cuda"
+
+    def set_parameters(self, params):
+        self.params = params
+        nbs = (self.ctx + self.bs - 1) // self.bs
+        nb = self.N * nbs
+        self.kc = torch.randn(nb, self.bs, self.Hkv, self.D, device=self.dev, dtype=torch.bfloat16)
+        self.vc = torch.randn_like(self.kc)
+        self.bt = torch.randperm(nb, device=self.dev).to(torch.int32).view(self.N, nbs).contiguous()
+        self.lens = torch.full((self.N,), self.ctx, device=self.dev, dtype=torch.int32)
+        self.q = torch.randn(self.N, self.H, self.D, device=self.dev, dtype=torch.bfloat16)
+
+    def benchmark(self, config):
+        from llmctl.ops import _lib
+
+        ops = _lib.native()
+        with _EnvKnob("LLMCTL_DECODE_SPLITS", str(self.params["splits"])):
+            fn = lambda: ops.paged_attention_decode(self.q, self.kc, self.vc, self.bt, self.lens, self.D ** -0.5)  # noqa
+            return _time(fn, self.dev, config.warmup_iterations, config.measurement_iterations)
+
+
+class FlashSplitTuner(Tunable):
+    """Flash-attention forward: split every causal q-block's K/V range over two workgroups
+    (+ combine) or not (``LLMCTL_FA_SPLIT``); pays off on small grids (short prefills)."""
+
+    def __init__(self, batch: int, seq_len: int, heads: int = 32, head_dim: int = 128, device: str = "auto"):
+        self.B, self.S, self.H, self.D = batch, seq_len, heads, head_dim
+        self.dev = _dev(device)
+
+    def get_parameter_space(self):
+        return {"split": [0, 1]}
+
+    def validate_parameters(self, p):
+        return self.dev.type == "cuda" and self.D in (64, 128)
+
+    def set_parameters(self, params):
+        self.params = params
+        g = torch.Generator(device="cpu").manual_seed(0)
+        self.q, self.k, self.v = (torch.randn(self.B, self.S, self.H, self.D, generator=g).to(self.dev, torch.bfloat16)
+                                  for _ in range(3))
+
+    def benchmark(self, config):
+        from llmctl.ops import _lib
+
+        ops = _lib.native()
+        with _EnvKnob("LLMCTL_FA_SPLIT", str(self.params["split"])):
+            fn = lambda: ops.flash_attn_fwd(self.q, self.k, self.v, self.D ** -0.5, True, None)  # noqa: E731
+            return _time(fn, self.dev, config.warmup_iterations, config.measurement_iterations)
+
+
+class SkinnyTuner(Tunable):
+    """Decode GEMM (M <= 32 tokens): hipBLASLt (config 0 here) or one of the weight-streaming
+    MFMA kernel's configurations (``skinny_linear_cfg``), on uncached weights."""
+
+    def __init__(self, M: int, N: int, K: int, device: str = "auto"):
+        self.M, self.N, self.K = M, N, K
+        self.dev = _dev(device)
+
+    def get_parameter_space(self):
+        return {"config": [0, 1, 2, 3, 4, 5, 7]}
+
+    def validate_parameters(self, p):
+        return self.dev.type == "cuda" and self.M <= 32 and self.N % 32 == 0 and self.K % 128 == 0
+
+    def set_parameters(self, params):
+        self.params = params
+        pool = max(2, int(1e9 // (self.N * self.K * 2)))
+        self.ws = [torch.randn(self.N, self.K, device=self.dev, dtype=torch.bfloat16) for _ in range(pool)]
+        self.x = torch.randn(self.M, self.K, device=self.dev, dtype=torch.bfloat16)
+
+    def benchmark(self, config):
+        from llmctl.ops import _lib
+
+        ops = _lib.native()
+        c = int(self.params["config"])
+        it = [0]
+
+        def fn():
+            w = self.ws[it[0] % len(self.ws)]
+            it[0] += 1
+            return torch.nn.functional.linear(self.x, w) if c == 0 else ops.skinny_linear_cfg(self.x, w, None, c)
+        return _time(fn, self.dev, config.warmup_iterations, config.measurement_iterations)
+
+
 class AutoTuner:
     def __init__(self, config: Optional[TuningConfig] = None):
         self.config = config or TuningConfig()
@@ -271,6 +433,23 @@ class AutoTuner:
         res = self.grid_search(t, f"comm_{tuple(tensor_shape)}_{dtype}")
         res.best_config = dict(res.best_config, mode=t.mode)
         return res
+
+    # ---- HIP kernel knobs (consumed by llmctl.plugins.tuning_cache)
+    def tune_gemm64(self, M: int, N: int, K: int, layout: str = "dgrad", device: str = "auto") -> TuningResult:
+        return self.grid_search(Gemm64Tuner(M, N, K, layout, device), f"gemm64_{layout}_{M}x{N}x{K}")
+
+    def tune_decode_splits(self, batch: int, ctx: int, heads: int = 32, kv_heads: int = 32, head_dim: int = 128,
+                           device: str = "auto") -> TuningResult:
+        return self.grid_search(DecodeSplitTuner(batch, ctx, heads, kv_heads, head_dim, device=device),
+                                f"decode_splits_{batch}x{ctx}x{kv_heads}")
+
+    def tune_fa_split(self, batch: int, seq_len: int, heads: int = 32, head_dim: int = 128,
+                      device: str = "auto") -> TuningResult:
+        return self.grid_search(FlashSplitTuner(batch, seq_len, heads, head_dim, device),
+                                f"fa_split_{batch}x{seq_len}x{heads}x{head_dim}")
+
+    def tune_skinny(self, M: int, N: int, K: int, device: str = "auto") -> TuningResult:
+        return self.grid_search(SkinnyTuner(M, N, K, device), f"skinny_{M}x{N}x{K}")
 
     def save_results(self, filepath: str) -> None:
         data = {k: {"best_config": r.best_config, "best_performance": r.best_performance,

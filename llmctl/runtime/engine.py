@@ -75,6 +75,7 @@ class TrainingConfig:
     activation_checkpoint: str = "none"  # none | selective | full
     num_microbatches: int = 0  # pipeline micro-batches per step (0 => 2*pp)
     virtual_stages: int = 1  # interleaved pipeline: model chunks per pipeline rank (1 = plain 1F1B)
+    tuning_cache: Optional[str] = None  # autotuner results to apply (else $LLMCTL_TUNING_CACHE)
     bucket_mb: float = 256.0
     betas: Tuple[float, float] = (0.9, 0.95)
     eps: float = 1e-8
@@ -113,6 +114,12 @@ class TrainingEngine:
         self._setup_distributed()
         set_seed(c.seed, c.deterministic)
         self.model_config = model_config or get_model_config(c.model_name_or_path)
+        from llmctl.plugins import tuning_cache
+
+        tc = tuning_cache.resolve(c.tuning_cache)
+        self.tuned = tuning_cache.apply_training(tc, c) if tc is not None else {}
+        if self.tuned:
+            log.info("tuning cache %s applied: %s", tc, self.tuned)
         self.global_step = 0
         self.epoch = 0
         self.consumed_samples = 0

@@ -48,7 +48,8 @@ class InferenceEngine:
     def __init__(self, model_path: str = "tiny", device: str = "auto", dtype=torch.bfloat16, max_batch_size: int = 8,
                  max_batch_tokens: int = 8192, max_model_len: Optional[int] = None, kv_cache_fraction: float = 0.85,
                  block_size: int = 16, num_kv_blocks: Optional[int] = None, scheduler: str = "dynamic",
-                 use_graphs: bool = True, seed: int = 0, pc=None, prefix_caching: bool = True):
+                 use_graphs: bool = True, seed: int = 0, pc=None, prefix_caching: bool = True,
+                 tuning_cache: Optional[str] = None):
         if device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -60,6 +61,10 @@ class InferenceEngine:
             from llmctl.exec.gemm_tuning import enable_tuned_gemms
 
             enable_tuned_gemms()
+        from llmctl.plugins import tuning_cache as _tc
+
+        tc = _tc.resolve(tuning_cache)
+        self.tuned = _tc.apply_serving(tc) if tc is not None else {}
         self.dtype = dtype
         self.model_path = model_path
         self.model: DecoderLM

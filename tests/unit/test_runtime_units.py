@@ -315,3 +315,62 @@ def test_param_gather_waits_follow_forward_order(tied):
         assert seen <= (k + 1) * per_layer + 1, (k, seen, len(order), waits)
     seen = max([seen, *waits[-1]])
     assert seen == len(order) - 1  # everything is waited by the end of the forward
+
+
+def test_tuning_cache_changes_dispatch(tmp_path, monkeypatch):
+    """A tuning cache's winners are applied: TrainingEngine takes the DP bucket size and the
+    gemm64 configuration per layout / exact shape, InferenceEngine the decode split count and
+    the decode-GEMM table (reference: AutoTuner.load_results filled a dict nothing read)."""
+    import json
+    import os
+
+    import importlib
+
+    linear = importlib.import_module("llmctl.exec.linear")  # the package re-exports a function named linear
+    from llmctl.models import get_model_config
+    from llmctl.ops import functional
+    from llmctl.runtime.engine import TrainingConfig, TrainingEngine
+    from llmctl.serve.engine import InferenceEngine
+
+    cache = {
+        "comm_(1024, 1024)_torch.float32": {"best_config": {"bucket_mb": 1, "algorithm": "allreduce"}},
+        "gemm64_dgrad_24576x4096x11008": {"best_config": {"config": 108}},
+        "gemm64_wgrad_4096x4096x24576": {"best_config": {"config": 204}},
+        "decode_splits_16x2048x32": {"best_config": {"splits": 4}},
+        "skinny_16x12288x4096": {"best_config": {"config": 0}},
+    }
+    p = tmp_path / "tuning_cache.json"
+    p.write_text(json.dumps(cache))
+    monkeypatch.delenv("LLMCTL_DECODE_SPLITS", raising=False)
+    saved = (dict(linear.GEMM64_CONFIGS), dict(linear.GEMM64_SHAPE_CONFIGS), dict(functional.SKINNY_CONFIGS))
+    try:
+        cfg = TrainingConfig(model_name_or_path="tiny", batch_size=2, seq_len=16, device="cpu", log_level="warning",
+                             tuning_cache=str(p))
+        eng = TrainingEngine(cfg, get_model_config("tiny"))
+        assert eng.config.bucket_mb == 1 and eng.tuned["bucket_mb"] == 1
+        assert linear.gemm64_config("dgrad", 24576, 4096, 11008) == 108
+        assert linear.gemm64_config("wgrad", 4096, 4096, 24576) == 204
+        assert linear.GEMM64_CONFIGS["dgrad"] == 108  # the layout default follows the winner
+        eng.shutdown()
+        ie = InferenceEngine("tiny", device="cpu", num_kv_blocks=16, block_size=8, max_model_len=64,
+                             tuning_cache=str(p))
+        assert os.environ["LLMCTL_DECODE_SPLITS"] == "4" and ie.tuned["decode_splits"] == 4
+        assert functional.SKINNY_CONFIGS[(16, 12288, 4096)] == 0
+    finally:
+        linear.GEMM64_CONFIGS.clear()
+        linear.GEMM64_CONFIGS.update(saved[0])
+        linear.GEMM64_SHAPE_CONFIGS.clear()
+        linear.GEMM64_SHAPE_CONFIGS.update(saved[1])
+        functional.SKINNY_CONFIGS.clear()
+        functional.SKINNY_CONFIGS.update(saved[2])
+        os.environ.pop("LLMCTL_DECODE_SPLITS", None)
+
+
+def test_hw_network_benchmark_gloo_rehearsal():
+    """``hw benchmark --component network`` measures collectives in-process (here: the gloo
+    rehearsal of the RCCL path, 2 ranks, small sizes)."""
+    from llmctl.cli.commands.hw import _bench_network
+
+    r = _bench_network(ranks=2, backend="gloo", sizes=(4096,), patterns=("allreduce", "allgather"), iters=2)
+    assert r["status"] == "ok" and len(r["results"]) == 2
+    assert all(x["busbw_gbps"] is not None and x["time_ms"] > 0 for x in r["results"])
