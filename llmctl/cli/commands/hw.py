@@ -284,7 +284,7 @@ def _bench_compute(duration: float) -> Dict[str, Any]:
 
 
 def _bench_network(ranks: int = 0, backend: str = "auto", sizes=(2 ** 20, 2 ** 24, 2 ** 28),
-                   patterns=("allreduce", "allgather", "reduce_scatter"), iters: int = 10) -> Dict[str, Any]:
+                   patterns=("allreduce", "all_gather", "reduce_scatter"), iters: int = 10) -> Dict[str, Any]:
     """xGMI / RCCL collective bandwidth measured in-process: one spawned rank per visible GPU
     (RCCL), each pattern at 1 MiB / 16 MiB / 256 MiB; reports bus bandwidth per size (the
     reference only printed a constant, ``llmctl/cli/commands/hw.py:344-345``).  With fewer

@@ -371,6 +371,6 @@ def test_hw_network_benchmark_gloo_rehearsal():
     rehearsal of the RCCL path, 2 ranks, small sizes)."""
     from llmctl.cli.commands.hw import _bench_network
 
-    r = _bench_network(ranks=2, backend="gloo", sizes=(4096,), patterns=("allreduce", "allgather"), iters=2)
+    r = _bench_network(ranks=2, backend="gloo", sizes=(4096,), patterns=("allreduce", "all_gather"), iters=2)
     assert r["status"] == "ok" and len(r["results"]) == 2
     assert all(x["busbw_gbps"] is not None and x["time_ms"] > 0 for x in r["results"])
