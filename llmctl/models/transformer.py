@@ -25,6 +25,7 @@ import torch.nn.functional as F
 
 from llmctl import ops
 from llmctl.exec.linear import data_grad, linear, weight_grad
+from llmctl.parallel import async_tp
 from llmctl.parallel import context_parallel as cp
 from llmctl.parallel import tensor_parallel as tp
 from .config import ModelConfig
@@ -176,8 +177,14 @@ class DecoderLayer(nn.Module):
             return x
         return tp.reduce_scatter_to_sp(x, pc.tp_group) if pc.sequence_parallel else tp.reduce_from_tp(x, pc.tp_group)
 
+    def _async_sp(self) -> bool:
+        return self.pc.tp_size > 1 and self.pc.sequence_parallel and async_tp.enabled()
+
     def attention(self, xn, B, S, rope, positions=None, doc_start=None):
-        qkv = linear(self._col_in(xn), self.wqkv, self.bqkv)
+        if self._async_sp():  # SP all-gather overlapped with the QKV GEMM
+            qkv = async_tp.column_parallel_sp(xn, self.wqkv, self.bqkv, self.pc.tp_group)
+        else:
+            qkv = linear(self._col_in(xn), self.wqkv, self.bqkv)
         if rope is not None:
             q, k, v = ops.rope_qkv(qkv, rope[0], rope[1], self.nq, self.nkv, S, positions)
         else:
@@ -196,8 +203,10 @@ class DecoderLayer(nn.Module):
                                                    cp.seq_to_head(v, g), causal=True), g)
         else:
             o = ops.flash_attention(q, k, v, causal=True, doc_start=doc_start)
-        out = linear(o.reshape(B * S, self.nq * self.D), self.wo)
-        out = self._row_out(out)
+        if self._async_sp():  # o-proj GEMM with the SP reduce-scatter overlapped
+            out = async_tp.row_parallel_sp(o.reshape(B * S, self.nq * self.D), self.wo, self.pc.tp_group)
+        else:
+            out = self._row_out(linear(o.reshape(B * S, self.nq * self.D), self.wo))
         if self.bo is not None:
             out = out + self.bo
         return out
@@ -205,17 +214,24 @@ class DecoderLayer(nn.Module):
     def mlp(self, xn):
         if self.moe is not None:
             return self.moe(xn)
-        x = self._col_in(xn)
-        if self.cfg.gated_mlp:
-            gu = linear(x, self.w_up, self.b_up)
-            if self.pc.activation_checkpoint == "selective":
-                out = _SwiGLUDown.apply(gu, self.w_down)
-            else:
-                out = linear(ops.swiglu(gu), self.w_down)
+        if self._async_sp() and self.pc.activation_checkpoint != "selective":
+            # SP all-gather / reduce-scatter overlapped with the up / down GEMMs
+            g = self.pc.tp_group
+            h = async_tp.column_parallel_sp(xn, self.w_up, self.b_up, g)
+            h = ops.swiglu(h) if self.cfg.gated_mlp else ops.gelu(h)
+            out = async_tp.row_parallel_sp(h, self.w_down, g)
         else:
-            hdn = ops.gelu(linear(x, self.w_up, self.b_up))
-            out = linear(hdn, self.w_down)
-        out = self._row_out(out)
+            x = self._col_in(xn)
+            if self.cfg.gated_mlp:
+                gu = linear(x, self.w_up, self.b_up)
+                if self.pc.activation_checkpoint == "selective":
+                    out = _SwiGLUDown.apply(gu, self.w_down)
+                else:
+                    out = linear(ops.swiglu(gu), self.w_down)
+            else:
+                hdn = ops.gelu(linear(x, self.w_up, self.b_up))
+                out = linear(hdn, self.w_down)
+            out = self._row_out(out)
         if self.b_down is not None:
             out = out + self.b_down
         return out

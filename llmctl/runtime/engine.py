@@ -164,6 +164,11 @@ class TrainingEngine:
                 # the GEMM grids, so the last buckets are not left exposed after backward
                 os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
             dist.init_process_group(backend=backend, **kw)
+        if self.env.world_size > 1 and backend == "gloo" and self.device.type == "cuda":
+            # single-GPU multi-rank rehearsal: device tensors cross gloo through host copies
+            from llmctl.comms import host_staging
+
+            host_staging.install()
         if c.pack_sequences and c.context_parallel > 1:
             raise NotImplementedError("pack_sequences with context parallelism is not supported")
         if c.expert_parallel > 1 and (c.tensor_parallel > 1 or c.pipeline_parallel > 1 or c.context_parallel > 1

@@ -49,6 +49,10 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
     gathered full state + losses (rank 0 meaningful)."""
     from llmctl.runtime.engine import TrainingEngine
 
+    if layout.get("staging"):  # host-staging patches installed (CPU tensors pass through)
+        from llmctl.comms import host_staging
+
+        host_staging.install()
     cfg = _config(model_name_or_path=model, tensor_parallel=layout.get("tp", 1),
                   pipeline_parallel=layout.get("pp", 1), zero_stage=layout.get("zero", 0),
                   sequence_parallel=layout.get("sp", False),
@@ -348,3 +352,74 @@ def ring_attention_check(rank: int, world: int, zigzag: bool = False, B: int = 2
     o.backward(ch(do))
     return {"o": o.detach(), "dq": ql.grad, "dk": kl.grad, "dv": vl.grad,
             "o_ref": ch(o_full), "dq_ref": ch(dq_full), "dk_ref": ch(dk_full), "dv_ref": ch(dv_full)}
+
+
+def async_tp_check(rank: int, world: int, T: int = 24, K: int = 16, N: int = 12) -> dict:
+    """Async-TP linears over a ``world``-rank TP group vs the unsharded fp32 products (gloo):
+    column-parallel (AG-GEMM fwd, GEMM-RS dgrad) then row-parallel (GEMM-RS fwd, AG-GEMM dgrad)
+    — the MLP pattern, ``y = RS(gelu(AG(x) W1_r^T + b_r) W2_r^T)``."""
+    import torch.distributed as dist
+    import torch.nn.functional as F
+
+    from llmctl.parallel.async_tp import column_parallel_sp, row_parallel_sp
+
+    dist.init_process_group("gloo")
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(T, K, generator=g)
+    w1 = torch.randn(N * world, K, generator=g) / K ** 0.5
+    b1 = torch.randn(N * world, generator=g)
+    w2 = torch.randn(K, N * world, generator=g) / N ** 0.5
+    dy = torch.randn(T, K, generator=g)
+    xr, w1r, b1r, w2r = (t.clone().requires_grad_(True) for t in (x, w1, b1, w2))
+    yr = F.linear(F.gelu(F.linear(xr, w1r, b1r)), w2r)
+    yr.backward(dy)
+    tl = T // world
+    rows = slice(rank * tl, (rank + 1) * tl)
+    cols = slice(rank * N, (rank + 1) * N)
+    xl = x[rows].clone().requires_grad_(True)
+    w1l = w1[cols].clone().requires_grad_(True)
+    b1l = b1[cols].clone().requires_grad_(True)
+    w2l = w2[:, cols].clone().requires_grad_(True)
+    grp = dist.group.WORLD
+    y = row_parallel_sp(F.gelu(column_parallel_sp(xl, w1l, b1l, grp)), w2l, grp)
+    y.backward(dy[rows])
+    return {"y": y.detach(), "dx": xl.grad, "dw1": w1l.grad, "db1": b1l.grad, "dw2": w2l.grad,
+            "y_ref": yr.detach()[rows], "dx_ref": xr.grad[rows], "dw1_ref": w1r.grad[cols],
+            "db1_ref": b1r.grad[cols], "dw2_ref": w2r.grad[:, cols]}
+
+
+def train_layout_gpu(rank: int, world: int, steps: int, layout: dict, model: str = "tiny",
+                     micro_per_rank: int = 4) -> dict:
+    """``train_layout`` on the GPU kernel path (bf16, HIP kernels) with every rank on cuda:0:
+    world > 1 runs over gloo with host-staged collectives (``llmctl.comms.host_staging`` — RCCL
+    cannot put two ranks on one device), world == 1 is the single-process reference (the
+    micro-batches are accumulation steps)."""
+    import os
+
+    from llmctl.ops import _lib
+    from llmctl.runtime.engine import TrainingEngine
+
+    if world == 1:
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            os.environ.pop(k, None)
+    torch.cuda.set_device(0)
+    cfg = _config(model_name_or_path=model, device="cuda:0", mixed_precision="bf16", seq_len=128, batch_size=2,
+                  distributed_backend="gloo", tensor_parallel=layout.get("tp", 1),
+                  pipeline_parallel=layout.get("pp", 1), zero_stage=layout.get("zero", 0),
+                  sequence_parallel=layout.get("sp", False), num_microbatches=layout.get("microbatches", 0),
+                  virtual_stages=layout.get("vstages", 1), context_parallel=layout.get("cp", 1),
+                  context_parallel_mode=layout.get("cp_mode", "ulysses"))
+    eng = TrainingEngine(cfg)
+    eng.load_full_state_dict(reference_state(model))
+    vocab = eng.model_config.vocab_size
+    nmb = eng.pipeline.num_microbatches if eng.pipeline is not None else micro_per_rank
+    dev = torch.device("cuda", 0)
+    losses = []
+    for s in range(steps):
+        batches = [tuple(t.to(dev) for t in make_batch(vocab, cfg.seq_len, cfg.batch_size, s, eng.pg.dp_rank, i))
+                   for i in range(nmb)]
+        loss = eng.train_step(batches)["loss"]
+        losses.append(eng.pipeline.broadcast_loss(loss) if eng.pipeline is not None else float(loss))
+    ev = eng.evaluate([tuple(t.to(dev) for t in make_batch(vocab, cfg.seq_len, cfg.batch_size, 99, 0))])
+    torch.cuda.synchronize()
+    return {"losses": losses, "eval": ev, "native": bool(_lib.load()), "backend": eng.backend}

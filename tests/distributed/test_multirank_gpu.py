@@ -40,3 +40,24 @@ def test_two_rank_zero1_matches_zero0_on_gpu():
     assert z0["config"]["parallelism"] == "dp2" and z1["config"]["parallelism"] == "dp2-zero1"
     assert z0["n_gpus"] == 2 and z0["config"]["global_batch"] == 4
     assert abs(z0["final_loss"] - z1["final_loss"]) < 2e-2, (z0["final_loss"], z1["final_loss"])
+
+
+def _layout_losses(world, layout):
+    from llmctl.testing.harness import run_ranks
+    from llmctl.testing.workers import train_layout_gpu
+
+    return run_ranks(train_layout_gpu, world, 3, layout, timeout=150)
+
+
+@pytest.mark.parametrize("async_tp", ["1", "0"])
+def test_tp2_pp2_sp2_four_ranks_one_gpu(monkeypatch, async_tp):
+    """Config #3 of the planner (TP2 x PP2, sequence parallel) as 4 ranks on cuda:0: bf16 HIP
+    kernels, the 1F1B schedule's device-tensor p2p and the async-TP ring steps (or the plain
+    SP collectives) over host-staged gloo; the losses follow the single-process GPU run."""
+    monkeypatch.setenv("LLMCTL_ASYNC_TP", async_tp)
+    ref = _layout_losses(1, {})[0]
+    out = _layout_losses(4, {"tp": 2, "pp": 2, "sp": True, "microbatches": 4})
+    assert all(o["native"] for o in out) and out[0]["backend"] == "gloo"
+    for a, b in zip(out[0]["losses"], ref["losses"]):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (out[0]["losses"], ref["losses"])
+    assert abs(out[0]["eval"] - ref["eval"]) < 3e-2, (out[0]["eval"], ref["eval"])

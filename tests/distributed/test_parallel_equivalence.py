@@ -50,6 +50,25 @@ def test_tp2_matches_single(ref_dp1, sp):
     _close(out[0]["state"], ref_dp1["state"])
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_async_tp_linears_match_unsharded(world):
+    """AG-GEMM / GEMM-RS ring decompositions (fwd + both grads) equal the unsharded products."""
+    from llmctl.testing.workers import async_tp_check
+
+    out = run_ranks(async_tp_check, world)
+    for r in range(world):
+        for name in ("y", "dx", "dw1", "db1", "dw2"):
+            assert torch.allclose(out[r][name], out[r][name + "_ref"], atol=1e-5, rtol=1e-4), (r, name)
+
+
+def test_tp2_sp_plain_collectives_match_single(ref_dp1, monkeypatch):
+    """LLMCTL_ASYNC_TP=0: Megatron-SP with the synchronous all-gather / reduce-scatter."""
+    monkeypatch.setenv("LLMCTL_ASYNC_TP", "0")
+    out = run_ranks(train_layout, 2, STEPS, {"tp": 2, "sp": True})
+    _losses_close(out[0]["losses"], ref_dp1["losses"])
+    _close(out[0]["state"], ref_dp1["state"])
+
+
 def test_tp2_dp2_zero1_matches_single(ref_dp2):
     out = run_ranks(train_layout, 4, STEPS, {"tp": 2, "zero": 1, "sp": True})
     _losses_close(out[0]["losses"], ref_dp2["losses"])
@@ -79,8 +98,11 @@ def test_pp2_1f1b_matches_single(ref_dp1_m4):
     _close(out[0]["state"], ref_dp1_m4["state"])
 
 
-def test_pp2_tp2_sp_matches_single(ref_dp1_m4):
-    out = run_ranks(train_layout, 4, STEPS, {"pp": 2, "tp": 2, "sp": True, "microbatches": 4})
+@pytest.mark.parametrize("staging", [False, True])
+def test_pp2_tp2_sp_matches_single(ref_dp1_m4, staging):
+    """TP2 x PP2 with SP (async-TP ring steps); ``staging``: with the one-GPU rehearsal's
+    host-staging patches installed, which must pass CPU tensors through untouched."""
+    out = run_ranks(train_layout, 4, STEPS, {"pp": 2, "tp": 2, "sp": True, "microbatches": 4, "staging": staging})
     _losses_close(out[0]["losses"], ref_dp1_m4["losses"])
     _close(out[0]["state"], ref_dp1_m4["state"])
 
