@@ -6,15 +6,20 @@ import pytest
 import torch
 
 from llmctl.ops import ref
+from llmctl.testing.numerics import rel_frob as _rel, row_err as _row_err
 
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
 
 
-def _rel(a, b):
-    a, b = a.float(), b.float()
-    return (a - b).norm().item() / max(b.norm().item(), 1e-12)
+
+def _attn_check(o, lse, grads, o_ref, lse_ref, grads_ref, o_tol=2e-2, g_tol=4e-2):
+    """Forward rows, LSE entries and every gradient row against the fp32 oracle."""
+    assert _row_err(o, o_ref) < o_tol, ("o", _row_err(o, o_ref))
+    assert (lse - lse_ref).abs().max().item() < 2e-2, ("lse", (lse - lse_ref).abs().max().item())
+    for name, a, b in zip(("dq", "dk", "dv"), grads, grads_ref):
+        assert _row_err(a, b, floor=0.5) < g_tol, (name, _row_err(a, b, floor=0.5), _row_err(a, b))
 
 
 def _bf(*shape, scale=1.0, seed=0):
@@ -29,7 +34,7 @@ def test_rmsnorm(native_lib, T, H):
     x, w = _bf(T, H, seed=1), _bf(H, seed=2, scale=0.5)
     y, rstd = native_lib.rmsnorm_fwd(x, w, 1e-5)
     yr, rr = ref.rmsnorm_fwd(x, w, 1e-5)
-    assert _rel(y, yr) < 1e-2 and _rel(rstd, rr) < 1e-5
+    assert _row_err(y, yr) < 1.5e-2 and _rel(rstd, rr) < 1e-5
     dy = _bf(T, H, seed=3)
     dres = _bf(T, H, seed=4)
     dx, dw = native_lib.rmsnorm_bwd(dy, x, w, rstd, dres)
@@ -44,7 +49,7 @@ def test_add_rmsnorm(native_lib, T, H):
     ro_r = (x.float() + res.float()).to(torch.bfloat16)
     yr, rr = ref.rmsnorm_fwd(ro_r, w, 1e-5)
     assert torch.equal(ro, ro_r)
-    assert _rel(y, yr) < 1e-2
+    assert _row_err(y, yr) < 1.5e-2, _row_err(y, yr)
 
 
 @pytest.mark.parametrize("T,H", [(100, 768), (9, 4096)])
@@ -52,7 +57,7 @@ def test_layernorm(native_lib, T, H):
     x, w, b = _bf(T, H, seed=1, scale=2.0), _bf(H, seed=2), _bf(H, seed=3)
     y, mu, rstd = native_lib.layernorm_fwd(x, w, b, 1e-5)
     yr, mr, rr = ref.layernorm_fwd(x, w, b, 1e-5)
-    assert _rel(y, yr) < 1e-2 and _rel(mu, mr) < 1e-4 and _rel(rstd, rr) < 1e-4
+    assert _row_err(y, yr) < 1.5e-2 and _rel(mu, mr) < 1e-4 and _rel(rstd, rr) < 1e-4
     dy = _bf(T, H, seed=4)
     dx, dw, db = native_lib.layernorm_bwd(dy, x, w, mu, rstd, None)
     dxr, dwr, dbr = ref.layernorm_bwd(dy, x, w, mr, rr)
@@ -171,14 +176,11 @@ def test_flash_attn(native_lib, B, S, Hq, Hkv, D, causal):
     scale = D ** -0.5
     o, lse = native_lib.flash_attn_fwd(q, k, v, scale, causal)
     orf, lser = ref.attention_fwd(q, k, v, scale, causal)
-    assert _rel(o, orf) < 2e-2, _rel(o, orf)
-    assert torch.allclose(lse, lser, atol=2e-2, rtol=1e-3)
     do = _bf(B, S, Hq, D, seed=24)
-    dq, dk, dv = native_lib.flash_attn_bwd(do, q, k, v, o, lse, scale, causal)
-    dqr, dkr, dvr = ref.attention_bwd(do, q, k, v, o, lse, scale, causal)
-    assert _rel(dv, dvr) < 3e-2, _rel(dv, dvr)
-    assert _rel(dk, dkr) < 3e-2, _rel(dk, dkr)
-    assert _rel(dq, dqr) < 3e-2, _rel(dq, dqr)
+    grads = native_lib.flash_attn_bwd(do, q, k, v, o, lse, scale, causal)
+    # the oracle's backward runs on the oracle's own forward (o, lse), not the kernel's
+    grads_ref = ref.attention_bwd(do, q, k, v, orf, lser, scale, causal)
+    _attn_check(o, lse, grads, orf, lser, grads_ref)
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(2, 384, 4, 2, 128), (1, 1000, 2, 2, 64), (2, 256, 4, 4, 128)])
@@ -196,14 +198,10 @@ def test_flash_attn_packed_documents(native_lib, B, S, Hq, Hkv, D):
     scale = D ** -0.5
     o, lse = native_lib.flash_attn_fwd(q, k, v, scale, True, doc)
     orf, lser = ref.attention_fwd(q, k, v, scale, True, doc_start=doc)
-    assert _rel(o, orf) < 2e-2, _rel(o, orf)
-    assert torch.allclose(lse, lser, atol=2e-2, rtol=1e-3)
     do = _bf(B, S, Hq, D, seed=44)
-    dq, dk, dv = native_lib.flash_attn_bwd(do, q, k, v, o, lse, scale, True, doc)
-    dqr, dkr, dvr = ref.attention_bwd(do, q, k, v, o, lse, scale, True, doc_start=doc)
-    assert _rel(dv, dvr) < 3e-2, _rel(dv, dvr)
-    assert _rel(dk, dkr) < 3e-2, _rel(dk, dkr)
-    assert _rel(dq, dqr) < 3e-2, _rel(dq, dqr)
+    grads = native_lib.flash_attn_bwd(do, q, k, v, o, lse, scale, True, doc)
+    grads_ref = ref.attention_bwd(do, q, k, v, orf, lser, scale, True, doc_start=doc)
+    _attn_check(o, lse, grads, orf, lser, grads_ref)
 
 
 def test_packed_model_matches_separate_documents(native_lib):
@@ -231,7 +229,7 @@ def test_flash_attn_forced_rescale(native_lib):
     k[0, 300] = (q[0, 310] * 6).to(torch.bfloat16)
     o, lse = native_lib.flash_attn_fwd(q, k, v, D ** -0.5, True)
     orf, _ = ref.attention_fwd(q, k, v, D ** -0.5, True)
-    assert _rel(o, orf) < 2e-2
+    assert _row_err(o, orf) < 2e-2, _row_err(o, orf)
 
 
 def test_functional_autograd_matches_ref(native_lib):
@@ -273,7 +271,7 @@ def test_paged_attention_decode(native_lib, Hq, Hkv, D):
     q = _bf(N, Hq, D, seed=43)
     o = native_lib.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
     orf = ref.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
-    assert _rel(o, orf) < 2e-2, _rel(o, orf)
+    assert _row_err(o, orf) < 2e-2, _row_err(o, orf)
 
 
 @pytest.mark.parametrize("splits", ["1", "3", "8", "auto"])
@@ -293,7 +291,7 @@ def test_paged_attention_decode_context_splits(native_lib, monkeypatch, Hq, Hkv,
     q = _bf(N, Hq, D, seed=63)
     o = native_lib.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
     orf = ref.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
-    assert _rel(o, orf) < 2e-2, _rel(o, orf)
+    assert _row_err(o, orf) < 2e-2, _row_err(o, orf)
 
 
 def test_kv_cache_write(native_lib):
@@ -327,7 +325,7 @@ def test_sampling(native_lib):
 def test_gemm_and_copy(native_lib):
     a, b = _bf(256, 512, seed=61), _bf(512, 512, seed=62)
     c = native_lib.gemm_bf16(a, b)
-    assert _rel(c, a.float() @ b.float().t()) < 1e-2
+    assert _row_err(c, a.float() @ b.float().t()) < 1.5e-2
     src = _bf(1 << 16, seed=63)
     dst = torch.empty_like(src)
     native_lib.hbm_copy(src, dst)
@@ -348,7 +346,7 @@ def test_gemm_ex(native_lib, M, N, K, at, bt, acc):
     native_lib.gemm_ex(a, b, out, at, bt, acc)
     want = A.float() @ B.float().t() + (c0.float() if acc else 0.0)
     assert torch.isfinite(out.float()).all()
-    assert _rel(out, want) < 8e-3
+    assert _row_err(out, want) < 1.5e-2, _row_err(out, want)
 
 
 def test_gemm_ex_strided_views(native_lib):
@@ -361,7 +359,7 @@ def test_gemm_ex_strided_views(native_lib):
     # A K-major: A(m,k) = a[k][m] -> M = 512, K = 1024
     native_lib.gemm_ex(a, b, out, True, True, False)
     want = a.float().t() @ b.float()
-    assert _rel(out, want) < 8e-3
+    assert _row_err(out, want) < 1.5e-2, _row_err(out, want)
     assert (out_buf[:, :256] == 0).all()
 
 
@@ -463,7 +461,7 @@ def test_skinny_linear_decode_gemm(native_lib, M, N, K, bias):
     y = native_lib.skinny_linear(x, w, b)
     ref_y = x.float() @ w.float().t() + (b.float() if bias else 0.0)
     assert y.shape == (M, N) and y.dtype == torch.bfloat16
-    assert _rel(y, ref_y) < 1e-2, _rel(y, ref_y)
+    assert _row_err(y, ref_y) < 1.5e-2, _row_err(y, ref_y)
 
 
 @pytest.mark.parametrize("with_pos", [False, True])
