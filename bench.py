@@ -41,7 +41,10 @@ def parse():
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--virtual-stages", type=int, default=1, help="interleaved pipeline chunks per rank")
     ap.add_argument("--microbatches", type=int, default=0, help="pipeline micro-batches (0: 2*pp)")
-    ap.add_argument("--zero", type=int, default=-1, help="ZeRO stage (-1: 0 on 1 GPU, 1 on >1)")
+    ap.add_argument("--zero", type=int, default=-1, help="ZeRO stage (-1: the planner's choice)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "manual"],
+                    help="auto: TP/PP/ZeRO/SP/recompute/virtual stages from llmctl.partition's planner at the "
+                         "fixed micro-batch when no layout flag is given; manual: the flags as given")
     ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--cp", type=int, default=1, help="context-parallel degree")
     ap.add_argument("--cp-mode", default="ulysses", choices=["ulysses", "ring"])
@@ -66,8 +69,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    zero = args.zero if args.zero >= 0 else (1 if world > 1 else 0)
     mc = get_model_config(args.model)
+    plan = None
+    if args.layout == "auto" and args.tp == 1 and args.pp == 1 and args.zero < 0 and args.cp == 1 and args.ep == 1 \
+            and not args.sequence_parallel and args.activation_checkpoint == "none":
+        # run what `llmctl plan --strategy auto` picks for this node size (the micro-batch is
+        # part of the metric's config, so it is fixed)
+        import dataclasses
+
+        from llmctl.partition.planner import HardwareModel, ParallelismPlanner
+
+        planner = ParallelismPlanner(dataclasses.asdict(mc), {}, args.seq_len, hw=HardwareModel(gpus=world))
+        plan = planner.search_optimal_plan(fixed={"mb": args.micro_batch})
+        args.tp, args.pp = plan["tensor_parallel"], plan["pipeline_parallel"]
+        args.zero = plan["zero_stage"]
+        args.sequence_parallel = plan["sequence_parallel"]
+        args.activation_checkpoint = plan["activation_checkpoint"]
+        args.virtual_stages = plan["virtual_stages"]
+        if args.pp > 1:
+            args.microbatches = plan["num_microbatches"]
+    zero = args.zero if args.zero >= 0 else (1 if world > 1 else 0)
     cfg = TrainingConfig(
         model_name_or_path=args.model, batch_size=args.micro_batch, seq_len=args.seq_len,
         gradient_accumulation_steps=args.grad_accum, learning_rate=3e-4, weight_decay=0.1, scheduler="cosine",
@@ -141,7 +162,9 @@ def main():
         "data": "synthetic (random tokens, random-init weights)",
         "config": {"model": mc.name, "global_batch": global_batch, "seq_len": args.seq_len,
                    "parallelism": par, "micro_batch": args.micro_batch, "grad_accum": accum,
-                   "activation_checkpoint": args.activation_checkpoint},
+                   "activation_checkpoint": args.activation_checkpoint,
+                   "layout": "planner" if plan is not None else "flags",
+                   "planner_estimate_tokens_per_sec": plan["estimated_tokens_per_sec"] if plan else None},
         "mfu": round(mfu, 4) if mfu is not None else None,
         "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
         "final_loss": round(loss, 4),

@@ -141,9 +141,11 @@ class HardwareModel:
     peak_flops: float = MI355X["peak_flops"]
     intra_bw_gbps: float = MI355X["xgmi_links"] * MI355X["xgmi_link_gbps"]  # per-GPU aggregate
     inter_bw_gbps: float = 50.0
-    # end-to-end model-FLOP efficiency calibrated on MI355X: GPT-7B mb=8 single GPU measured
-    # 23.5k tok/s = 39 % MFU (GEMMs ~51 % of peak, attention/elementwise/optimizer the rest)
-    gemm_efficiency: float = 0.40
+    hbm_bw_gbps: float = 8000.0
+    # model-FLOP efficiency of forward+backward, calibrated on MI355X: GPT-7B mb=12 single GPU
+    # measured 28.1k tok/s (46 % MFU, profiles/bench_r2_gemm64_ab.jsonl) including the AdamW
+    # term below
+    gemm_efficiency: float = 0.465
     collective_efficiency: float = 0.6
 
     @classmethod
@@ -315,12 +317,20 @@ class ParallelismPlanner:
         if ep > 1:
             a2a = mb * self.seq_len * c.experts_per_token * c.hidden * 2.0 * (ep - 1) / ep
             ep_time = 4 * a2a / (self._link_bw(ep, tp) * 1e9) * math.ceil(c.layers / pp) * accum
-        total = compute_total + tp_time + pp_time + exposed_dp + ep_time
-        return dict(compute_s=compute_total, tp_s=tp_time, pp_s=pp_time, dp_s=dp_time, total_s=total,
+        # fused AdamW: ~28 B of HBM traffic per parameter (bf16 grad + fp32 master/m/v read and
+        # written + bf16 param), sharded over DP from ZeRO-1 on; the updated-parameter all-gather
+        # of ZeRO-1/2 waits in the next forward's per-bucket hooks (mostly hidden)
+        opt_time = 28.0 * self._stage_params(tp, pp) / (self.hw.hbm_bw_gbps * 1e9 * 0.75)
+        if zs >= 1:
+            opt_time /= dp
+            if zs < 3:
+                dp_time += 0.1 * self._ring(grad_bytes, dp, dp_bw)
+        total = compute_total + tp_time + pp_time + exposed_dp + ep_time + opt_time
+        return dict(compute_s=compute_total, tp_s=tp_time, pp_s=pp_time, dp_s=dp_time, opt_s=opt_time, total_s=total,
                     comm_gb=(grad_bytes * 2 * (dp > 1) + (4 * act_bytes * c.layers if tp > 1 else 0)) / GiB)
 
     # ---------------------------------------------------------------- search
-    def candidates(self) -> List[Dict[str, Any]]:
+    def candidates(self, micro_batches=(1, 2, 4, 8, 16)) -> List[Dict[str, Any]]:
         c = self.cfg
         n = self.hw.gpus
         out = []
@@ -339,7 +349,7 @@ class ParallelismPlanner:
                     continue
                 for sp in ((False, True) if tp > 1 else (False,)):
                     for ac in ("none", "selective", "full"):
-                        for mb in (1, 2, 4, 8, 16):
+                        for mb in micro_batches:
                             for vs in ((1, 2, 4) if pp > 1 and zs < 3 else (1,)):
                                 if vs > 1 and c.layers < pp * vs:
                                     continue
@@ -371,17 +381,24 @@ class ParallelismPlanner:
                             max_comm_bw: Optional[float] = None, global_batch: Optional[int] = None,
                             fixed: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
         max_mem = max_memory if max_memory else 0.9 * self.hw.hbm_gb
-        best, best_key = None, None
-        for cand in self.candidates():
+        mbs = (fixed["mb"],) if fixed and fixed.get("mb") else (1, 2, 4, 8, 16)
+        feasible = []
+        for cand in self.candidates(mbs):
             if fixed and any(fixed.get(k) is not None and cand[k] != fixed[k] for k in cand):
                 continue
             plan = self.evaluate(global_batch=global_batch, **cand)
-            if plan["estimated_memory_gb"] > max_mem:
-                continue
-            # prefer throughput; tie-break towards less memory
-            key = (-plan["estimated_tokens_per_sec"], plan["estimated_memory_gb"])
-            if best_key is None or key < best_key:
-                best, best_key = plan, key
+            if plan["estimated_memory_gb"] <= max_mem:
+                feasible.append(plan)
+        best = None
+        if feasible:
+            # throughput first; within 0.5 % of the best (the model's resolution) prefer the
+            # simpler layout: lower ZeRO stage, less model parallelism, less recompute, less memory
+            top = max(p["estimated_tokens_per_sec"] for p in feasible)
+            acr = {"none": 0, "selective": 1, "full": 2}
+            near = [p for p in feasible if p["estimated_tokens_per_sec"] >= 0.995 * top]
+            best = min(near, key=lambda p: (p["zero_stage"], p["tensor_parallel"] * p["pipeline_parallel"],
+                                            acr[p["activation_checkpoint"]], -p["estimated_tokens_per_sec"],
+                                            p["estimated_memory_gb"]))
         if best is None:
             # nothing fits: most-sharded configuration, flagged by the memory estimate
             n = self.hw.gpus

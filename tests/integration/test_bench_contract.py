@@ -45,6 +45,7 @@ def test_bench_multirank_json_line(n, extra, par):
     assert res["higher_is_better"] is True and res["scaling"] == "weak" and res["dtype"] == "bf16"
     cfg = res["config"]
     assert cfg["parallelism"] == par and cfg["seq_len"] == 64
+    assert cfg["layout"] == ("planner" if not extra else "flags")  # default: the planner's layout
     dp = n // (2 if "--tp" in extra else 1)
     assert cfg["global_batch"] == 2 * dp
     # value is the whole-job aggregate: global tokens over the (max-over-ranks) timed window
