@@ -41,6 +41,11 @@
 //   * Stream items past the last K-tile re-load the last K-tile (clamped source) into slots
 //     nobody reads again, so the wait counts never change in the tail.
 //   * XCD-aware bijective block remap + grouped tile order (GROUP tile-rows).
+//   * Tail split ("split-K on the last round"): with one 512-thread workgroup per CU, a grid of
+//     T tiles runs ceil(T / CUs) rounds and the last one is partly idle (GPT-7B wgrad of the
+//     up-projection: 1376 tiles = 5.375 rounds, 10 % of its time).  The tiles of the partial
+//     round are cut into S K-ranges; those items write fp32 partials to a workspace and a
+//     reduction kernel applies the epilogue, so the last round costs ~1/S of a tile.
 #include "attn_common.h"
 
 namespace llmctl {
@@ -69,6 +74,10 @@ struct G64Args {
   long lda, ldb, ldc;
   int M, N, K;
   int tiles_m, tiles_n;
+  int n_main;   // tiles computed whole (blocks [0, n_main)); the rest are split
+  int splits;   // K-ranges per split tile (1: no split items)
+  int kt_part;  // K-tiles per split item (even)
+  float* ws;    // [n_tail][splits][256][256] fp32 partials
 };
 
 __device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
@@ -163,12 +172,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 
-  // ---- tile selection: XCD-bijective remap, then grouped (GROUP tile-rows) order
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  int wg;
-  {
+  // ---- work item: main tiles [0, n_main) through an XCD-bijective remap, then split items
+  //      (tail tile u, K-range sp) in block order; tiles in grouped (GROUP tile-rows) order
+  const int bid = blockIdx.x;
+  int wg, sp = -1, u = 0;
+  if (bid < args.n_main) {
+    const int nwg = args.n_main;
     const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
     wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
+  } else {
+    const int i = bid - args.n_main;
+    u = i / args.splits;
+    sp = i - u * args.splits;
+    wg = args.n_main + u;
   }
   const int per_group = GROUP * args.tiles_n;
   const int grp = wg / per_group;
@@ -184,7 +200,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   // byte step of one K-tile in each operand
   const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
   const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
-  const int KT = args.K / TK;
+  const int KT = sp < 0 ? args.K / TK : args.kt_part;
+  const unsigned kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);  // first K-tile of this item
 
   unsigned vo[4][2];
 #pragma unroll
@@ -199,7 +216,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   // stream item: half-tile KIND of K-tile t (clamped: past-the-end items re-load the last tile)
   auto issue = [&](auto kind_c, int t) {
     constexpr int kind = decltype(kind_c)::value;
-    const int tc = t < KT ? t : KT - 1;
+    const unsigned tc = kt0 + (unsigned)(t < KT ? t : KT - 1);
     const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
     if constexpr (kind <= A_HI) {
       const unsigned so = __builtin_amdgcn_readfirstlane(tc * a_kstep);
@@ -317,6 +334,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 
   // ---- epilogue: lane holds C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3
   const int g = lane >> 4, i16 = lane & 15;
+  if (sp >= 0) {  // split item: fp32 partial tile, row-major 256 x 256
+    float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 64 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + 16 * j) = acc[i][j];
+    return;
+  }
   unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 64 + 4 * g;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -339,23 +364,102 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   }
 }
 
+// sum of the split partials of tail tile u (grouped-order position n_main + u) + epilogue;
+// thread = 8 consecutive columns of one row
+template <int EPI, int GROUP>
+__global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
+  const int u = blockIdx.x / (TM * TN / 8 / 256);
+  const int e = (blockIdx.x % (TM * TN / 8 / 256)) * 256 + threadIdx.x;  // 8-column chunk in the tile
+  const int row = e / (TN / 8), col = (e % (TN / 8)) * 8;
+  const int wg = args.n_main + u;
+  const int per_group = GROUP * args.tiles_n;
+  const int grp = wg / per_group;
+  const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
+  const int inner = wg - grp * per_group;
+  const int tm = grp * GROUP + inner % gsz, tn = inner / gsz;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float* W = args.ws + (long)u * args.splits * (TM * TN) + row * TN + col;
+  for (int sp = 0; sp < args.splits; ++sp) {
+    const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(W + (long)sp * (TM * TN));
+    const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(W + (long)sp * (TM * TN) + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] += x0[j];
+      v[4 + j] += x1[j];
+    }
+  }
+  unsigned short* p = args.c + (long)(tm * TM + row) * args.ldc + tn * TN + col;
+  if constexpr (EPI == EPI_ACC) {
+    float old[8];
+    load8(p, old);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += old[j];
+  }
+  store8(p, v);
+}
+
 template <bool AT, bool BT, int EPI, int GROUP>
 void launch_g(const G64Args& g, int variant) {
-  const dim3 grid(g.tiles_m * g.tiles_n), block(NTHR);
+  const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
+  const dim3 grid(n_items), block(NTHR);
   switch (variant) {
     case 1: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g); break;
     case 2: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 2>), grid, block, 0, stream(), g); break;
     case 3: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 3>), grid, block, 0, stream(), g); break;
     default: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 0>), grid, block, 0, stream(), g); break;
   }
+  const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
+  if (n_tail > 0)
+    hipLaunchKernelGGL((gemm64_split_reduce<EPI, GROUP>), dim3(n_tail * (TM * TN / 8 / 256)), dim3(256), 0, stream(),
+                       g);
 }
 
 // config = group (tile-rows per tile-order group: 4 / 8) + 100 * schedule variant
+//          + 1000 * split (0: automatic tail split, 1: none, S >= 2: S K-ranges when legal)
 template <bool AT, bool BT, int EPI>
 void launch(const G64Args& g, int config) {
-  const int group = config % 100, variant = config / 100;
+  const int group = config % 100, variant = (config / 100) % 10;
   if (group == 8) launch_g<AT, BT, EPI, 8>(g, variant);
   else launch_g<AT, BT, EPI, 4>(g, variant);
+}
+
+// Tail split plan: tiles of the last, partial round (when it is at most half full) are cut into
+// S K-ranges (KT % S == 0, an even number >= 4 of K-tiles each).  Estimated cost in tile-times:
+//   ceil(n_tail * S / CUs) / S   + workspace traffic (write + re-read of S fp32 partial tiles,
+//   ~0.5 us per partial tile at ~4 TB/s) in units of one tile's run time.
+void plan_split(G64Args& g, int mode) {
+  const int tiles = g.tiles_m * g.tiles_n, KT = g.K / TK, cus = num_cus();
+  g.n_main = tiles;
+  g.splits = 1;
+  g.kt_part = KT;
+  g.ws = nullptr;
+  if (mode == 1) return;
+  // tiles of the last round; a forced split of a whole number of rounds splits the last round
+  const int n_tail = tiles % cus ? tiles % cus : (mode >= 2 ? min(tiles, cus) : 0);
+  // auto: only a last round at most half full (measured: a 69 %-full round of the GPT-7B
+  // down-projection wgrad lost 2 % to the workspace traffic; 37 % / 12 % / 50 % ones gained
+  // 8.6 % / 3.6 % / 18 %, profiles/gemm64_split_r2.txt)
+  if (n_tail == 0 || (mode == 0 && n_tail * 2 > cus)) return;
+  // one tile's time on one CU at ~1.4 PF chip-wide
+  const double tile_us = 2.0 * TM * TN * (double)g.K / (1.4e15 / cus) * 1e6;
+  double best = 1.0;  // unsplit tail: one full tile-time
+  int best_s = 1;
+  const int cands[] = {2, 3, 4, 6, 8, 12, 16};
+  for (int S : cands) {
+    if (mode >= 2 && S != mode) continue;
+    if (KT % S || (KT / S) % 2 || KT / S < 4) continue;
+    const double rounds = (double)((n_tail * S + cus - 1) / cus) / S;
+    const double traffic = 2.0 * n_tail * S * (TM * TN * 4.0) / 4e12 * 1e6 / tile_us;
+    const double cost = rounds + traffic + 0.1;  // + reduction launch / pipeline ramp of the items
+    if (cost < best || mode >= 2) {
+      best = cost;
+      best_s = S;
+    }
+  }
+  if (best_s == 1) return;
+  g.n_main = tiles - n_tail;
+  g.splits = best_s;
+  g.kt_part = KT / best_s;
 }
 
 }  // namespace
@@ -389,8 +493,14 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   const c10::DeviceGuard dg(a.device());
   G64Args g{reinterpret_cast<const unsigned short*>(a.data_ptr()), reinterpret_cast<const unsigned short*>(b.data_ptr()),
             reinterpret_cast<unsigned short*>(out.data_ptr()), a.stride(0), b.stride(0), out.stride(0),
-            (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN)};
-  const int grp = (int)config;
+            (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr};
+  plan_split(g, (int)(config / 1000));
+  at::Tensor ws;
+  if (g.splits > 1) {
+    ws = at::empty({(long)(g.tiles_m * g.tiles_n - g.n_main) * g.splits * TM * TN}, a.options().dtype(at::kFloat));
+    g.ws = ws.data_ptr<float>();
+  }
+  const int grp = (int)(config % 1000);
   const int sel = (at_ ? 4 : 0) | (bt_ ? 2 : 0) | (accumulate ? 1 : 0);
   switch (sel) {
     case 0: launch<false, false, EPI_STORE>(g, grp); break;

@@ -26,22 +26,24 @@ TOL = 1.2e-2  # bf16 output rounding is <= 2^-8 of the row max; fp32 accumulatio
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (768, 512, 1024), (2304, 1280, 256)])
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
 @pytest.mark.parametrize("acc", [False, True])
-def test_gemm64_ex(native_lib, M, N, K, at, bt, acc):
+@pytest.mark.parametrize("split", [0, 1, 2])
+def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split):
     A = _bf(M, K, seed=71)
     B = _bf(N, K, seed=72)
     a = A.t().contiguous() if at else A
     b = B.t().contiguous() if bt else B
     c0 = _bf(M, N, seed=73)
     out = c0.clone() if acc else torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    native_lib.gemm64_ex(a, b, out, at, bt, acc, 104)
+    native_lib.gemm64_ex(a, b, out, at, bt, acc, 104 + 1000 * split)
     want = A.float() @ B.float().t() + (c0.float() if acc else 0.0)
     assert torch.isfinite(out.float()).all()
     assert row_err(out, want) < TOL
 
 
-@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304])
+@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304, 1104, 2104, 4008, 8104])
 def test_gemm64_configs(native_lib, config):
-    """Every tile-order group / schedule variant computes the same product (fwd and wgrad)."""
+    """Every tile-order group / schedule variant / tail split computes the same product (fwd
+    and wgrad); 1xxx = no split, Sxxx = S K-ranges (24 tiles < one round: all of them split)."""
     M, N, K = 1536, 1024, 2048  # 24 tiles: more tiles than one group, several K-tile pairs
     A, B = _bf(M, K, seed=3), _bf(N, K, seed=4)
     want = A.float() @ B.float().t()
@@ -50,6 +52,20 @@ def test_gemm64_configs(native_lib, config):
     assert row_err(out, want) < TOL
     native_lib.gemm64_ex(A.t().contiguous(), B.t().contiguous(), out, True, True, False, config)
     assert row_err(out, want) < TOL
+
+
+def test_gemm64_split_tail_multi_round(native_lib):
+    """More tiles than CUs with a partial last round: the main tiles run whole, the tail tiles
+    in K-ranges through the workspace; store and accumulate epilogues, wgrad layout."""
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    M, N, K = 256 * (n_cu // 8 + 1), 256 * 8, 1024  # n_cu + 8 tiles: 8 tail tiles
+    A, B = _bf(K, M, seed=91), _bf(K, N, seed=92)
+    c0 = _bf(M, N, seed=93)
+    want = A.float().t() @ B.float()
+    for cfg in (104, 8104):
+        out = c0.clone()
+        native_lib.gemm64_ex(A, B, out, True, True, True, cfg)
+        assert row_err(out, want + c0.float()) < TOL, cfg
 
 
 def test_gemm64_strided_views(native_lib):
