@@ -47,6 +47,17 @@ def compile_flags(arch: str, save_temps: bool = False):
     return flags
 
 
+# per-source extra flags.  flash_attn_bwd: MFMA results in the VGPR form — by default hipcc gave
+# the S / dP products AGPR destinations (occupancy-1 kernel, AGPRs free) and then moved every
+# element back with v_accvgpr_read for the softmax VALU (~120 moves per tile); the dK/dV
+# accumulators are pinned to AGPRs by their inline-asm MFMAs instead.
+FILE_FLAGS = {"flash_attn_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
+def file_flags(src: Path, flags):
+    return flags + FILE_FLAGS.get(src.name, [])
+
+
 def _digest(src: Path, flags) -> str:
     """Content key of one object: the source, every csrc header and the compile flags (not
     mtimes: a restored or copied tree can carry stale objects with newer timestamps)."""
@@ -74,16 +85,16 @@ def build(arch: str = "gfx950", jobs: int = 0, force: bool = False, save_temps: 
     for s in srcs:
         o = BUILD / (s.name + ".o")
         objs.append(o)
-        if force or _needs(s, o, flags):
+        if force or _needs(s, o, file_flags(s, flags)):
             todo.append((s, o))
 
     def _one(so):
         s, o = so
-        cmd = [hipcc()] + flags + ["-c", str(s), "-o", str(o)]
+        cmd = [hipcc()] + file_flags(s, flags) + ["-c", str(s), "-o", str(o)]
         r = subprocess.run(cmd, capture_output=True, text=True, cwd=str(BUILD))
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {s.name}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        o.with_suffix(o.suffix + ".key").write_text(_digest(s, flags))
+        o.with_suffix(o.suffix + ".key").write_text(_digest(s, file_flags(s, flags)))
         return s.name
 
     jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))

@@ -25,6 +25,16 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// x combined with lane l^32's x in one v_permlane32_swap (no LDS round trip, unlike __shfl_xor)
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_add(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // row index of register i of a 32x32 accumulator for lane half h
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
@@ -123,6 +133,34 @@ __device__ __forceinline__ void vm_wait() {
   else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
   else static_assert(N == 0 || N == 5 || N == 9, "add the immediate");
 }
+// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): base and record count are scalar, so a
+// per-tile move of the source window costs SALU only; loads at offsets >= num_records return 0.
+using i32x4_t = __attribute__((ext_vector_type(4))) int;
+__device__ __forceinline__ i32x4_t buf_rsrc(const void* base, unsigned num_records) {
+  const unsigned long a = (unsigned long)base;
+  i32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));
+  r[2] = __builtin_amdgcn_readfirstlane((int)num_records);
+  r[3] = 0x00020000;  // raw buffer, 32-bit data format
+  return r;
+}
+__device__ __forceinline__ void buf_dma16(i32x4_t rsrc, unsigned voff, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc),
+               "s"(lds_byte)
+               : "memory");
+}
+__device__ __forceinline__ void buf_dma4(i32x4_t rsrc, unsigned voff, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc),
+               "s"(lds_byte)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  static_assert(N >= 0 && N <= 63, "vmcnt immediate");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p);

@@ -22,8 +22,9 @@
 //   each raw s_barrier behind a counted vmcnt; lse / delta (/ document starts) ride in the same
 //   DMA ring as 256-B row-constant vectors.
 // fa_bwd_dq_kernel — query-stationary, the forward's structure: workgroup = 4 waves = 128 query
-//   rows of one (batch, q-head), Q and dO fragments in registers, K/V tiles of 64 keys staged
-//   through LDS (register staging split around the MFMAs, guide T14); "swapped" products keep the
+//   rows of one (batch, q-head), Q and dO fragments in registers, K/V tiles of 64 keys arrive by
+//   LDS-DMA into a 2-slot ring (one barrier per tile), XCD-aware block order, scalar-uniform
+//   masking (only diagonal / sequence-end tiles run the selects); "swapped" products keep the
 //   key on the registers so dS^T is directly the B operand of dQ^T += K^T dS^T.  dQ is written
 //   once, in bf16.
 // A pre-kernel computes delta.
@@ -39,7 +40,6 @@ constexpr int KV_QT = 64;   // query rows per streamed tile
 constexpr int KV_NBUF = 3;  // LDS ring depth
 constexpr int DQ_QB = 128;  // query rows per dQ workgroup
 constexpr int DQ_KB = 64;   // keys per dQ tile
-constexpr int DKV_VAR = 0;  // dK/dV loop-body schedule (see fa_bwd_dkv_kernel); A/B: fa_bwd_ablate 3/4
 
 struct BwdArgs {
   const unsigned short *q, *k, *v, *dout;
@@ -80,6 +80,45 @@ __global__ __launch_bounds__(256) void delta_kernel(const unsigned short* __rest
   if (row < R && sub == 0) delta[((long)b * Hq + hq) * S + sq] = s;
 }
 
+// dK^T / dV^T accumulation pinned to AGPRs: through the builtin, hipcc kept these 128 registers
+// in VGPRs and shuttled the S / dP accumulators through AGPRs instead (~500 v_accvgpr moves per
+// tile).  One asm statement issues a 16-row step's MFMAs for every d-block (dV^T += dO^T P^T and
+// dK^T += Q^T dS^T interleaved), so hipcc can place nothing between them.  It pads no wait states
+// into asm (guide §5.7 item 2), so the string carries them: s_nop 1 before (a just-written VALU
+// operand, e.g. P^T / dS^T from v_cvt_pk) and s_nop 11 after (8-pass XDL result -> any non-MFMA
+// reader or writer, e.g. a compiler v_accvgpr_mov of an accumulator).
+template <int NDB>
+__device__ __forceinline__ void dvdk_step(f32x16* dv, f32x16* dk, const bf16x8_t* da, const bf16x8_t* qa, bf16x8_t p,
+                                          bf16x8_t ds) {
+  if constexpr (NDB == 4) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_32x32x16_bf16 %0, %8, %16, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %4, %12, %17, %4\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %9, %16, %1\n\t"
+        "v_mfma_f32_32x32x16_bf16 %5, %13, %17, %5\n\t"
+        "v_mfma_f32_32x32x16_bf16 %2, %10, %16, %2\n\t"
+        "v_mfma_f32_32x32x16_bf16 %6, %14, %17, %6\n\t"
+        "v_mfma_f32_32x32x16_bf16 %3, %11, %16, %3\n\t"
+        "v_mfma_f32_32x32x16_bf16 %7, %15, %17, %7\n\t"
+        "s_nop 11"
+        : "+a"(dv[0]), "+a"(dv[1]), "+a"(dv[2]), "+a"(dv[3]), "+a"(dk[0]), "+a"(dk[1]), "+a"(dk[2]), "+a"(dk[3])
+        : "v"(da[0]), "v"(da[1]), "v"(da[2]), "v"(da[3]), "v"(qa[0]), "v"(qa[1]), "v"(qa[2]), "v"(qa[3]), "v"(p),
+          "v"(ds));
+  } else {
+    static_assert(NDB == 2, "head_dim 64 or 128");
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_32x32x16_bf16 %0, %4, %8, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %2, %6, %9, %2\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %5, %8, %1\n\t"
+        "v_mfma_f32_32x32x16_bf16 %3, %7, %9, %3\n\t"
+        "s_nop 11"
+        : "+a"(dv[0]), "+a"(dv[1]), "+a"(dk[0]), "+a"(dk[1])
+        : "v"(da[0]), "v"(da[1]), "v"(qa[0]), "v"(qa[1]), "v"(p), "v"(ds));
+  }
+}
+
 __device__ __forceinline__ void store_bf16x4(unsigned short* p, const float* x, float mul) {
   unsigned short w[4];
 #pragma unroll
@@ -91,31 +130,47 @@ __device__ __forceinline__ void store_bf16x4(unsigned short* p, const float* x, 
 // =============================================================================================
 // dK / dV
 // =============================================================================================
-template <int HD, bool CAUSAL, bool DOC, int VAR = DKV_VAR>
+template <int HD, bool CAUSAL, bool DOC>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
   constexpr int NKS = HD / 16;
   constexpr int NDB = HD / 32;
   constexpr int ROWB = HD * 2;
   constexpr int TILE_B = KV_QT * ROWB;     // one Q (or dO) tile
   constexpr int NP = TILE_B / 1024 / 4;    // 1-KiB DMA pieces per wave per operand
-  constexpr int VM = 2 * NP + 1;           // DMA instructions per wave per tile
   constexpr int RC_B = KV_QT * 4;          // one row-constant vector
-  constexpr int BUF_B = 2 * TILE_B + 4 * RC_B;  // Q | dO | lse | delta | doc | (dummy)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[KV_NBUF * BUF_B];
+  constexpr int BUF_B = 2 * TILE_B + 4 * RC_B;  // Q | dO | lse | delta | doc | (pad)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF_B];  // 2-slot ring
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
+  const int nkb = (a.S + KV_KB - 1) / KV_KB;
   const int BH = a.B * a.Hkv;
-  const int bh = blockIdx.x % BH;
-  const int kblk = blockIdx.x / BH;  // small kblk = most query tiles under causal: dispatched first
+  int bh, kblk;
+  if (BH % 8) {
+    bh = blockIdx.x % BH;
+    kblk = blockIdx.x / BH;  // small kblk = most query tiles under causal: dispatched first
+  } else {  // XCD-aware: XCD x walks kv-heads [x*BH/8, (x+1)*BH/8), a head's key blocks back to back
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    bh = x * (BH >> 3) + j / nkb;
+    kblk = j % nkb;
+  }
   const int b = bh / a.Hkv, hk = bh % a.Hkv;
   const int group = a.Hq / a.Hkv;
   const int k0 = kblk * KV_KB;
-  const int wkey0 = k0 + wave * 32;
+  const int wkey0 = k0 + wave * 32;  // wave-uniform
   const int my_key = wkey0 + r;
 
+  // zero the ring (rows past S may stay unwritten by the DMA; every value read must be finite)
+#pragma unroll
+  for (int i = 0; i < 2 * BUF_B / 4096; ++i)
+    *reinterpret_cast<uint4*>(smem + i * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
+  if (tid < (2 * BUF_B % 4096) / 16)
+    *reinterpret_cast<uint4*>(smem + (2 * BUF_B / 4096) * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  const unsigned lds0 = lds_addr(smem);
   // ---- this wave's K / V fragments (B operands): lane holds X[my_key][16ks + 8hh + j]
   bf16x8_t kf[NKS], vf[NKS];
   {
@@ -150,66 +205,79 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
       if (ds[mid] > k0 + KV_KB - 1) hi = mid;
       else lo = mid + 1;
     }
-    q_end = lo;
+    q_end = __builtin_amdgcn_readfirstlane(lo);
   }
   const int nq = q_end > q_start ? (q_end - q_start + KV_QT - 1) / KV_QT : 0;
   const int ntiles = group * nq;
-  const unsigned lds0 = lds_addr(smem);
-
-  // ---- DMA of tile t into ring slot t % 3: every wave issues exactly VM instructions
-  auto issue = [&](int t) {
-    const int g = t / nq;
-    const int q0 = q_start + (t - g * nq) * KV_QT;
+  // ---- DMA of tile (g, qi) into ring slot t & 1: every wave issues exactly 2*NP+1 instructions;
+  //      buffer descriptors re-based per tile (SALU), per-lane offsets fixed: the tr image is
+  //      built by permuting the source rows/chunks; rows past S read as zeros
+  unsigned vq[NP], vd[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int byte = (i * 4 + wave) * 1024 + lane * 16;
+    const int row = byte / ROWB;
+    const int lch = ((byte % ROWB) >> 4) ^ swz_tr<HD>(row);
+    vq[i] = (unsigned)((row * a.q_ss + lch * 8) * 2);
+    vd[i] = (unsigned)((row * a.do_ss + lch * 8) * 2);
+  }
+  const float* rc_src = wave == 1 ? a.delta : a.lse;  // wave 0: lse, 1: delta, 2: doc (DOC), 3: pad
+  auto issue = [&](int t, int g, int qi) __attribute__((always_inline)) {
+    const int q0 = q_start + qi * KV_QT;
     const int hq = hk * group + g;
-    const unsigned slot = lds0 + (unsigned)((t % KV_NBUF) * BUF_B);
-    const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh;
-    const unsigned short* Dp = a.dout + b * a.do_sb + hq * a.do_sh;
+    const int nr = min(KV_QT, a.S - q0);
+    i32x4_t rq = buf_rsrc(a.q + b * a.q_sb + hq * a.q_sh + (long)q0 * a.q_ss, (unsigned)(((nr - 1) * a.q_ss + HD) * 2));
+    i32x4_t rd = buf_rsrc(a.dout + b * a.do_sb + hq * a.do_sh + (long)q0 * a.do_ss,
+                          (unsigned)(((nr - 1) * a.do_ss + HD) * 2));
+    const long rc0 = ((long)b * a.Hq + hq) * a.S + q0;
+    i32x4_t rr = (DOC && wave == 2) ? buf_rsrc(a.doc + (long)b * a.S + q0, (unsigned)(nr * 4))
+                                    : buf_rsrc(rc_src + rc0, (unsigned)(nr * 4));
+    // descriptor SGPRs may come from v_readfirstlane: 5 wait states before a VMEM reads them
+    asm volatile("s_nop 4" : "+s"(rq), "+s"(rd), "+s"(rr));
+    const unsigned slot = lds0 + (unsigned)((t & 1) * BUF_B);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      const int piece = i * 4 + wave;
-      const int byte = piece * 1024 + lane * 16;
-      const int row = byte / ROWB;
-      const int pch = (byte % ROWB) >> 4;                // physical chunk in the tr image
-      const int lch = pch ^ swz_tr<HD>(row);             // logical chunk it holds
-      const long qq = min(q0 + row, a.S - 1);            // rows past S: P masked to 0
-      dma16(Qp + qq * a.q_ss + lch * 8, slot + piece * 1024);
-      dma16(Dp + qq * a.do_ss + lch * 8, slot + TILE_B + piece * 1024);
+      buf_dma16(rq, vq[i], slot + (i * 4 + wave) * 1024);
+      buf_dma16(rd, vd[i], slot + TILE_B + (i * 4 + wave) * 1024);
     }
-    const int qq = min(q0 + lane, a.S - 1);
-    const long rc = ((long)b * a.Hq + hq) * a.S + qq;
-    const void* src = wave == 1 ? (const void*)(a.delta + rc)
-                    : (DOC && wave == 2) ? (const void*)(a.doc + (long)b * a.S + qq)
-                                         : (const void*)(a.lse + rc);
-    dma4(src, slot + 2 * TILE_B + wave * RC_B);
+    buf_dma4(rr, lane * 4, slot + 2 * TILE_B + wave * RC_B);
   };
 
-  if (ntiles > 0) issue(0);
-  if (ntiles > 1) issue(1);
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) vm_wait<VM>();  // this wave's DMA of tile t landed (t+1 stays in flight)
-    else vm_wait<0>();
-    __builtin_amdgcn_s_barrier();       // ... and every other wave's; slot (t+2)%3 is free
-    if (t + 2 < ntiles) issue(t + 2);
-
-    const int g = t / nq;
-    const int q0 = q_start + (t - g * nq) * KV_QT;
-    const unsigned char* Qs = smem + (t % KV_NBUF) * BUF_B;
+  // tile counters (g, qi) of the tile being issued: scalar, incremental (no per-tile division)
+  int ig = 0, iq = 0;
+  if (ntiles > 0) {
+    issue(0, ig, iq);
+    if (++iq == nq) { iq = 0; ++ig; }
+  }
+  int qi = 0;  // q-tile index of tile t
+  auto step = [&](auto slot_c, int t) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot_c)::value;
+    vm_wait_n<0>();                     // this wave's DMA of tile t (and of the K/V block) landed
+    __builtin_amdgcn_s_barrier();       // ... and every other wave's; everyone is done with t-1
+    if (t + 1 < ntiles) {               // into tile t-1's slot; lands under this tile's MFMAs
+      issue(t + 1, ig, iq);
+      if (++iq == nq) { iq = 0; ++ig; }
+    }
+    const int q0 = q_start + qi * KV_QT;
+    if (++qi == nq) qi = 0;
+    // wave-uniform tile classes: all of this wave's keys after all of the tile's rows -> nothing
+    // to do; diagonal / sequence-end / document tiles -> masked softmax; the rest -> plain
+    if (CAUSAL && wkey0 > q0 + KV_QT - 1) return;
+    const bool need_mask = DOC || (CAUSAL && wkey0 + 31 > q0) || (q0 + KV_QT > a.S) || (wkey0 + 31 >= a.S);
+    const unsigned char* Qs = smem + SL * BUF_B;
     const unsigned char* Ds = Qs + TILE_B;
     const float* lse_s = reinterpret_cast<const float*>(Ds + TILE_B);
     const float* del_s = lse_s + KV_QT;
     const int* doc_s = reinterpret_cast<const int*>(del_s + KV_QT);
-    // no early-out for tiles a wave sees nothing of (only the first tile of a causal block, for
-    // half the waves): a branch here makes hipcc shuttle dK/dV between AGPRs and VGPRs every tile
 
     // ---- per 32-row half h: S = Q K^T, dP = dO V^T (q on regs, key on lane), then
     //      dV^T += dO^T P and dK^T += Q^T dS (sum over the half's rows = the registers).
-    //      Masks are branch-free selects.  VAR 0: half after half; VAR 1: both halves'
-    //      S/dP chains first (the second half's MFMAs cover the first half's exp/VALU work);
-    //      VAR 2: as 1 with each half's operand fragments read into registers ahead of its MFMAs.
-    auto sdp = [&](int h, f32x16& s, f32x16& dp) {
+    //      One wave per SIMD: nothing else hides LDS latency, so each phase's fragments are read
+    //      as a batch ahead of its MFMAs (the transposed ones before the softmax VALU).
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
-      if constexpr (VAR == 2) {
+    for (int h = 0; h < 2; ++h) {
+      f32x16 s, dp;
+      {
         bf16x8_t qa[NKS], da[NKS];
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
@@ -217,81 +285,90 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
           da[ks] = lds_read_b128(Ds, tr_off<HD>(32 * h + r, 2 * ks + hh));
         }
 #pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
+#pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
           s = mfma32(qa[ks], kf[ks], s);
           dp = mfma32(da[ks], vf[ks], dp);
         }
-      } else {
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // first 16-row step's transposed fragments, read under the softmax (causal kernels only: the
+      // full-attention build runs out of VGPRs with them)
+      bf16x8_t dfr[NDB], qfr[NDB];
+      if constexpr (CAUSAL) {
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8_t qa = lds_read_b128(Qs, tr_off<HD>(32 * h + r, 2 * ks + hh));
-          const bf16x8_t da = lds_read_b128(Ds, tr_off<HD>(32 * h + r, 2 * ks + hh));
-          s = mfma32(qa, kf[ks], s);
-          dp = mfma32(da, vf[ks], dp);
+        for (int d = 0; d < NDB; ++d) {
+          dfr[d] = tr_frag<HD>(Ds, 32 * h, d * 32, lane);
+          qfr[d] = tr_frag<HD>(Qs, 32 * h, d * 32, lane);
         }
       }
-    };
-    auto soft = [&](int h, const f32x16& s, const f32x16& dp, bf16x8_t* pb, bf16x8_t* sb) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (need_mask) {  // wave-uniform: one scalar branch around branch-free selects
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int row0 = 32 * h + 8 * gq + 4 * hh;  // rows of registers 4gq .. 4gq+3
+          int sv[4] = {0, 0, 0, 0};
+          if constexpr (DOC) {
+            const int4 s4 = *reinterpret_cast<const int4*>(doc_s + row0);
+            sv[0] = s4.x; sv[1] = s4.y; sv[2] = s4.z; sv[3] = s4.w;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int qq = q0 + row0 + j;
+            bool ok = qq < a.S && my_key < a.S;
+            if constexpr (CAUSAL) ok = ok && my_key <= qq;
+            if constexpr (DOC) ok = ok && my_key >= sv[j];
+            s[4 * gq + j] = ok ? s[4 * gq + j] : -INFINITY;
+          }
+        }
+      }
       float p[16], dsv[16];
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
-        const int row0 = 32 * h + 8 * gq + 4 * hh;  // rows of registers 4gq .. 4gq+3
+        const int row0 = 32 * h + 8 * gq + 4 * hh;
         const float4 l4 = *reinterpret_cast<const float4*>(lse_s + row0);
         const float4 d4 = *reinterpret_cast<const float4*>(del_s + row0);
-        int4 s4 = make_int4(0, 0, 0, 0);
-        if constexpr (DOC) s4 = *reinterpret_cast<const int4*>(doc_s + row0);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float nl[4] = {-l4.x * LOG2E, -l4.y * LOG2E, -l4.z * LOG2E, -l4.w * LOG2E};
         const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
-        const int sv[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * gq + j;
-          const int qq = q0 + row0 + j;
-          bool dead = (qq >= a.S) | (my_key >= a.S);
-          if constexpr (CAUSAL) dead |= my_key > qq;
-          if constexpr (DOC) dead |= my_key < sv[j];
-          const float pv = dead ? 0.f : fast_exp2(s[i] * a.scale_log2 - lv[j] * LOG2E);
+          const float pv = fast_exp2(__builtin_fmaf(s[i], a.scale_log2, nl[j]));
           p[i] = pv;
           dsv[i] = pv * (dp[i] - dv4[j]);
         }
       }
+      bf16x8_t pb[2], sb[2];
       pb[0] = to_bf16x8(p);
       pb[1] = to_bf16x8(p + 8);
       sb[0] = to_bf16x8(dsv);
       sb[1] = to_bf16x8(dsv + 8);
-    };
-    auto dvdk = [&](int h, const bf16x8_t* pb, const bf16x8_t* sb) {
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
+      if constexpr (!CAUSAL) {
 #pragma unroll
         for (int d = 0; d < NDB; ++d) {
-          const bf16x8_t da = tr_frag<HD>(Ds, 32 * h + 16 * st, d * 32, lane);
-          dv[d] = mfma32(da, pb[st], dv[d]);
-          const bf16x8_t qa = tr_frag<HD>(Qs, 32 * h + 16 * st, d * 32, lane);
-          dk[d] = mfma32(qa, sb[st], dk[d]);
+          dfr[d] = tr_frag<HD>(Ds, 32 * h, d * 32, lane);
+          qfr[d] = tr_frag<HD>(Qs, 32 * h, d * 32, lane);
         }
-    };
-    if constexpr (VAR == 0) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f32x16 s, dp;
-        bf16x8_t pb[2], sb[2];
-        sdp(h, s, dp);
-        soft(h, s, dp, pb, sb);
-        dvdk(h, pb, sb);
       }
-    } else {
-      f32x16 s0, dp0, s1, dp1;
-      bf16x8_t pb0[2], sb0[2], pb1[2], sb1[2];
-      sdp(0, s0, dp0);
-      sdp(1, s1, dp1);
-      soft(0, s0, dp0, pb0, sb0);
-      dvdk(0, pb0, sb0);
-      soft(1, s1, dp1, pb1, sb1);
-      dvdk(1, pb1, sb1);
+      bf16x8_t dfr1[NDB], qfr1[NDB];  // second step's fragments land under the first step's MFMAs
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) {
+        dfr1[d] = tr_frag<HD>(Ds, 32 * h + 16, d * 32, lane);
+        qfr1[d] = tr_frag<HD>(Qs, 32 * h + 16, d * 32, lane);
+      }
+      dvdk_step<NDB>(dv, dk, dfr, qfr, pb[0], sb[0]);
+      dvdk_step<NDB>(dv, dk, dfr1, qfr1, pb[1], sb[1]);
     }
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
   }
-  // ---- write dK (scaled), dV: lane = key, registers = d
+  // ---- write dK (scaled), dV: lane = key, registers = d.  The asm MFMAs' results are read by
+  //      compiler code below: 8-pass XDL D -> non-MFMA reader needs 12 wait states (unpadded by hipcc)
+#pragma unroll
+  for (int d = 0; d < NDB; ++d) asm volatile("s_nop 7\n\ts_nop 7" : "+a"(dk[d]), "+a"(dv[d]));
   if (my_key < a.S) {
     unsigned short* dkp = a.dk + ((long)b * a.S + my_key) * a.Hkv * HD + (long)hk * HD;
     unsigned short* dvp = a.dv + ((long)b * a.S + my_key) * a.Hkv * HD + (long)hk * HD;
@@ -320,27 +397,39 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   constexpr int NKS = HD / 16;
   constexpr int NDB = HD / 32;
   constexpr int ROWB = HD * 2;
-  constexpr int CPR = HD / 8;
-  constexpr int LD_ITERS = DQ_KB * CPR / 256;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * DQ_KB * ROWB];
-  unsigned char* Ks = smem;                // tr image: row reads (S^T) and column reads (dQ^T)
-  unsigned char* Vs = smem + DQ_KB * ROWB;  // row image
+  constexpr int TILE = DQ_KB * ROWB;       // one K (or V) tile image
+  constexpr int PPW = TILE / 1024 / 4;     // 1-KiB DMA pieces per wave per operand
+  constexpr int SLOT = 2 * TILE;           // K (tr image) | V (row image)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * SLOT];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = (a.S + DQ_QB - 1) / DQ_QB;
   const int BH = a.B * a.Hq;
-  const int bh = blockIdx.x % BH;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest first
+  int bh, qi;
+  if (BH % 8) {
+    bh = blockIdx.x % BH;
+    qi = blockIdx.x / BH;
+  } else {  // XCD-aware: XCD x walks heads [x*BH/8, (x+1)*BH/8), a head's q-blocks back to back
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    bh = x * (BH >> 3) + j / nqb;
+    qi = j % nqb;
+  }
+  const int qblk = nqb - 1 - qi;  // heaviest first
   const int b = bh / a.Hq, hq = bh % a.Hq;
   const int hk = hq / (a.Hq / a.Hkv);
-  const int q_row0 = qblk * DQ_QB + wave * 32;
+  const int q_row0 = qblk * DQ_QB + wave * 32;  // wave-uniform
   const int my_q = q_row0 + r;
   const int qc = min(my_q, a.S - 1);
 
   const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh;
   const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh;
+
+#pragma unroll
+  for (int i = 0; i < 2 * SLOT / 4096; ++i)
+    *reinterpret_cast<uint4*>(smem + i * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
 
   // ---- Q and dO fragments (B operands of S^T = K Q^T and dP^T = V dO^T)
   bf16x8_t qf[NKS], df[NKS];
@@ -356,6 +445,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   const long rc = ((long)b * a.Hq + hq) * a.S + qc;
   const float nlse2 = -a.lse[rc] * LOG2E;
   const float dlt = a.delta[rc];
+  // retire the loads here (a first use inside the loop would carry a per-iteration vmcnt(0) that
+  // also drains the next tile's DMA)
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]), "v"(df[ks]));
+  asm volatile("" ::"v"(nlse2), "v"(dlt));
 
   f32x16 dq[NDB];
 #pragma unroll
@@ -369,42 +463,40 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   if constexpr (DOC) {
     const int* ds = a.doc + (long)b * a.S;
     my_start = ds[qc];
-    w_min = ds[min(q_row0, a.S - 1)];
-    w_max = ds[min(q_row0 + 31, a.S - 1)];
-    t0 = ds[min(qblk * DQ_QB, a.S - 1)] / DQ_KB;
+    w_min = __builtin_amdgcn_readfirstlane(ds[min(q_row0, a.S - 1)]);
+    w_max = __builtin_amdgcn_readfirstlane(ds[min(q_row0 + 31, a.S - 1)]);
+    t0 = __builtin_amdgcn_readfirstlane(ds[min(qblk * DQ_QB, a.S - 1)]) / DQ_KB;
   }
+  const int key_hi = CAUSAL ? qc : a.S - 1;  // last key this lane's row sees
 
-  uint4 kst[LD_ITERS], vst[LD_ITERS];
-  auto issue = [&](int t) {
+  // ---- DMA ring (see the forward kernel): K as a tr image, V as a row image
+  unsigned vk[PPW], vv[PPW];
 #pragma unroll
-    for (int it = 0; it < LD_ITERS; ++it) {
-      const int c = tid + 256 * it;
-      const int row = c / CPR, ch = c % CPR;
-      const int key = min(t * DQ_KB + row, a.S - 1);  // keys past S: masked
-      kst[it] = gload16(Kp + (long)key * a.k_ss + ch * 8);
-      vst[it] = gload16(Vp + (long)key * a.v_ss + ch * 8);
+  for (int i = 0; i < PPW; ++i) {
+    const int byte = (i * 4 + wave) * 1024 + lane * 16;
+    const int row = byte / ROWB, pch = (byte % ROWB) >> 4;
+    vk[i] = (unsigned)((row * a.k_ss + ((pch ^ swz_tr<HD>(row)) << 3)) * 2);
+    vv[i] = (unsigned)((row * a.v_ss + ((pch ^ swz_row<HD>(row)) << 3)) * 2);
+  }
+  const unsigned lds0 = lds_addr(smem);
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    const int key0 = t * DQ_KB;
+    const int nk = min(DQ_KB, a.S - key0);
+    i32x4_t rk = buf_rsrc(Kp + (long)key0 * a.k_ss, (unsigned)(((nk - 1) * a.k_ss + HD) * 2));
+    i32x4_t rv = buf_rsrc(Vp + (long)key0 * a.v_ss, (unsigned)(((nk - 1) * a.v_ss + HD) * 2));
+    // descriptor SGPRs may come from v_readfirstlane: VALU-written SGPR -> VMEM read needs 5
+    // wait states, which hipcc does not pad into the asm below (guide §5.7 item 2)
+    asm volatile("s_nop 4" : "+s"(rk), "+s"(rv));
+    const unsigned slot = lds0 + (unsigned)(((t - t0) & 1) * SLOT) + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      buf_dma16(rk, vk[i], slot + i * 4096);
+      buf_dma16(rv, vv[i], slot + TILE + i * 4096);
     }
   };
-  auto commit = [&]() {
-#pragma unroll
-    for (int it = 0; it < LD_ITERS; ++it) {
-      const int c = tid + 256 * it;
-      const int row = c / CPR, ch = c % CPR;
-      *reinterpret_cast<uint4*>(Ks + tr_off<HD>(row, ch)) = kst[it];
-      *reinterpret_cast<uint4*>(Vs + row_off<HD>(row, ch)) = vst[it];
-    }
-  };
 
-  if (t0 < ntiles) issue(t0);
-  for (int t = t0; t < ntiles; ++t) {
-    __syncthreads();  // all waves finished reading the previous tile
-    commit();
-    __syncthreads();
-    if (t + 1 < ntiles) issue(t + 1);  // overlaps the MFMAs below
-    const int kv0 = t * DQ_KB;
-    if (CAUSAL && kv0 > q_row0 + 31) continue;  // tile entirely above this wave's diagonal
-    if (DOC && kv0 + DQ_KB <= w_min) continue;  // tile entirely before every row's document
-    const bool need_mask = (CAUSAL && kv0 + DQ_KB - 1 > q_row0) || (kv0 + DQ_KB > a.S) || (DOC && kv0 < w_max);
+  auto tile = [&](bool need_mask, const unsigned char* Ks, const unsigned char* Vs, int kv0)
+                  __attribute__((always_inline)) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       // ---- S^T = K Q^T, dP^T = V dO^T   (key on regs, q on lane)
@@ -413,32 +505,51 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
       for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8_t kfr = lds_read_b128(Ks, tr_off<HD>(kb * 32 + r, 2 * ks + hh));
-        s = mfma32(kfr, qf[ks], s);
-        const bf16x8_t vfr = lds_read_b128(Vs, row_off<HD>(kb * 32 + r, 2 * ks + hh));
-        dp = mfma32(vfr, df[ks], dp);
+        s = mfma32(lds_read_b128(Ks, tr_off<HD>(kb * 32 + r, 2 * ks + hh)), qf[ks], s);
+        dp = mfma32(lds_read_b128(Vs, row_off<HD>(kb * 32 + r, 2 * ks + hh)), df[ks], dp);
+      }
+      if (need_mask) {  // wave-uniform: a scalar branch around branch-free selects
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kv0 + kb * 32 + acc_row(i, hh);
+          bool ok = key <= key_hi;
+          if constexpr (DOC) ok = ok && key >= my_start;
+          s[i] = ok ? s[i] : -INFINITY;
+        }
       }
       float dsv[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pv = fast_exp2(s[i] * a.scale_log2 + nlse2);
-        if (need_mask) {
-          const int key = kv0 + kb * 32 + acc_row(i, hh);
-          if ((CAUSAL && key > my_q) || key >= a.S || (DOC && key < my_start)) pv = 0.f;
-        }
-        dsv[i] = pv * (dp[i] - dlt);
-      }
+      for (int i = 0; i < 16; ++i) dsv[i] = fast_exp2(__builtin_fmaf(s[i], a.scale_log2, nlse2)) * (dp[i] - dlt);
       // ---- dQ^T += K^T dS^T   (sum over keys = the registers of dS^T)
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         const bf16x8_t sbf = to_bf16x8(dsv + 8 * st);
 #pragma unroll
-        for (int d = 0; d < NDB; ++d) {
-          const bf16x8_t kt = tr_frag<HD>(Ks, kb * 32 + 16 * st, d * 32, lane);
-          dq[d] = mfma32(kt, sbf, dq[d]);
-        }
+        for (int d = 0; d < NDB; ++d) dq[d] = mfma32(tr_frag<HD>(Ks, kb * 32 + 16 * st, d * 32, lane), sbf, dq[d]);
       }
     }
+  };
+
+  __syncthreads();  // ring zeroed before any DMA lands in it
+  auto step = [&](auto slot_c, int t) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot_c)::value;
+    vm_wait_n<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + 1 < ntiles) issue(t + 1);
+    const int kv0 = t * DQ_KB;
+    bool live = true;
+    if constexpr (CAUSAL) live = kv0 <= q_row0 + 31;
+    if constexpr (DOC) live = live && kv0 + DQ_KB > w_min;
+    if (live) {
+      const bool need_mask =
+          (CAUSAL && kv0 + DQ_KB - 1 > q_row0) || (kv0 + DQ_KB > a.S) || (DOC && kv0 < w_max);
+      tile(need_mask, smem + SL * SLOT, smem + SL * SLOT + TILE, kv0);
+    }
+  };
+  if (t0 < ntiles) issue(t0);
+  for (int t = t0; t < ntiles; t += 2) {
+    step(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
   }
   // ---- dQ = scale * (dQ^T)^T: lane = q row, registers = d
   if (my_q < a.S) {
@@ -546,7 +657,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
 }
 
 // timing-only entry for tools/attn_ablate.py (causal, no documents): abl 0 = both kernels,
-// 1 = dK/dV kernel only, 2 = dQ kernel only, 3 / 4 = dK/dV schedule variants 1 / 2.  ``delta`` is taken as given.
+// 1 = dK/dV kernel only, 2 = dQ kernel only.  ``delta`` is taken as given.
 void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                    const at::Tensor& delta, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
                    int64_t abl) {
@@ -557,14 +668,6 @@ void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
                "fa_bwd_ablate: bf16 dq/dk/dv, fp32 delta");
   const c10::DeviceGuard g(q.device());
   BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, 1.0 / std::sqrt((double)D));
-  if (abl == 3 || abl == 4) {
-    LLMCTL_CHECK(D == 128, "fa_bwd_ablate: schedule variants at head_dim 128");
-    const int nkb = (a.S + KV_KB - 1) / KV_KB;
-    const dim3 grid((unsigned)(a.B * a.Hkv * nkb));
-    if (abl == 3) hipLaunchKernelGGL((fa_bwd_dkv_kernel<128, true, false, 1>), grid, dim3(256), 0, stream(), a);
-    else hipLaunchKernelGGL((fa_bwd_dkv_kernel<128, true, false, 2>), grid, dim3(256), 0, stream(), a);
-    return;
-  }
   dispatch_bwd(a, D, true, false, stream(), abl != 1, abl != 2);
 }
 

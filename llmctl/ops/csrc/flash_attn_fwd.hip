@@ -2,20 +2,28 @@
 //
 // Structure (CDNA guide App. B "Fused attention prefill"):
 //   * workgroup = 4 waves = 128 query rows of one (batch, q-head); each wave owns 32 rows;
+//     two workgroups per CU (2 waves per SIMD: one wave's softmax VALU issues under the
+//     other's MFMAs);
 //   * Q fragments live in registers for the whole kernel (HD/16 x bf16x8 per lane);
-//   * K/V tiles of 64 keys are staged global -> registers -> LDS (async-STAGE split, T14:
-//     the next tile's global loads are issued before this tile's MFMAs and written to LDS
-//     after the next barrier);
+//   * K/V tiles of 64 keys arrive by LDS-DMA (buffer_load_dwordx4 ... lds, source-swizzled)
+//     into a 2-slot ring: one s_barrier per tile, the next tile's DMA is issued right after it
+//     and lands under this tile's MFMAs.  The buffer resource is re-based per tile (SALU only)
+//     and its record count stops at the last key, so keys past S read as zeros;
 //   * "swapped" QK^T: S^T = K Q^T puts the key index in registers and the query on the
 //     lane, so the online-softmax row max/sum are in-lane + one xor-32 shuffle, and P^T
 //     is directly the B operand of O^T += V^T P^T (no P round-trip through LDS);
 //   * K is read with ds_read_b128 from an XOR-swizzled row image (T2), V with
 //     ds_read_b64_tr_b16 from a swizzled tr image (T10) — both bank-conflict free;
-//   * exp2-domain softmax with the 1/sqrt(d)*log2(e) scale folded into one multiply;
-//   * causal: tiles wholly above a wave's diagonal are skipped, the mask is applied only
-//     on diagonal tiles; the heaviest q-blocks are dispatched first;
-//   * blocks that share a K/V head are B*Hq apart in dispatch order, i.e. on one XCD (L2
-//     reuse of the K/V stream) when B*Hq % 8 == 0;
+//   * exp2-domain softmax: the row max is taken on the raw scores and the 1/sqrt(d)*log2(e)
+//     scale is folded into the exponent's FMA (p = 2^(s*c - m)), ~4 VALU per score;
+//   * masking is a scalar-uniform choice per (wave, tile): only causal-diagonal / sequence-end /
+//     document-boundary tiles run the masked softmax (branch-free selects), every other tile the
+//     plain one — round 1's per-element divergent branches cost ~30 % of the loop's issue slots
+//     (profiles/attn_fwd_isa_r2.txt);
+//   * causal: tiles wholly above a wave's diagonal are skipped; dispatch is XCD-aware: each XCD
+//     (workgroup i -> XCD i % 8) walks a contiguous range of heads with a head's q-blocks back
+//     to back, heaviest first, so the few heads resident per XCD keep their K/V in its L2
+//     (the head-major order kept ~48 heads = 48 MB of K/V live per 4 MB L2);
 //   * packed sequences (optional ``doc_start[B,S]``: position where each token's document
 //     begins, non-decreasing): key j is visible to query i iff doc_start[i] <= j <= i; the
 //     K/V loop starts at the block's first document start, so the work is sum(doc_len^2);
@@ -32,7 +40,7 @@ namespace llmctl {
 using namespace attn;
 namespace {
 
-constexpr int QB = 128;  // query rows per workgroup
+// workgroup shape (A/B knob FA_NW, see the host code): NW waves x 32 query rows, NBUF-slot ring
 constexpr int KB = 64;   // keys per tile
 constexpr float kRescaleTh = 8.f;  // log2-domain headroom of the deferred softmax rescale
 
@@ -53,34 +61,53 @@ struct FwdArgs {
   float* lse_part;   // SPLIT: [2, B, Hq, S] natural-log partial LSEs
 };
 
-template <int HD, bool CAUSAL, bool DOC = false, bool SPLIT = false>
-__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
-  constexpr int NKS = HD / 16;  // k-steps of QK^T
-  constexpr int NDB = HD / 32;  // 32-wide d blocks of O
-  constexpr int ROWB = HD * 2;  // bytes per LDS row
-  constexpr int CPR = HD / 8;   // 16-B chunks per row
-  constexpr int LD_ITERS = KB * CPR / 256;  // 16-B chunks per thread per tile (4 for HD=128)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * KB * ROWB];
-  unsigned char* Ks = smem;
-  unsigned char* Vs = smem + KB * ROWB;
+template <int HD, bool CAUSAL, bool DOC = false, bool SPLIT = false, int NW = 4, int NBUF = 2>
+__global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
+  constexpr int QB = NW * 32;  // query rows per workgroup
+  constexpr int NTHR = NW * 64;
+  constexpr int NKS = HD / 16;            // k-steps of QK^T
+  constexpr int NDB = HD / 32;            // 32-wide d blocks of O
+  constexpr int ROWB = HD * 2;            // bytes per LDS row
+  constexpr int TILE = KB * ROWB;         // one K (or V) tile image
+  constexpr int PPW = TILE / 1024 / NW;   // 1-KiB DMA pieces per wave per operand
+  constexpr int SLOT = 2 * TILE;          // K | V
+  static_assert(PPW * NW * 1024 == TILE, "pieces must split evenly over the waves");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * SLOT];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = (a.S + QB - 1) / QB;
   const int BH = a.B * a.Hq;
-  const int bh = blockIdx.x % BH;
-  const int rest = blockIdx.x / BH;
+  int bh, rest;
+  if (SPLIT || BH % 8) {
+    bh = blockIdx.x % BH;
+    rest = blockIdx.x / BH;
+  } else {
+    // XCD-aware order: workgroup i runs on XCD i % 8; XCD x walks the heads
+    // [x*BH/8, (x+1)*BH/8) one after another, all q-blocks of a head back to back (heaviest
+    // first), so the K/V stream of the ~4 heads resident on an XCD stays in its 4 MB L2
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    bh = x * (BH >> 3) + j / nqb;
+    rest = j % nqb;
+  }
   const int part = SPLIT ? rest & 1 : 0;
   const int qblk = nqb - 1 - (SPLIT ? rest >> 1 : rest);  // heaviest (largest causal span) first
   const int b = bh / a.Hq, hq = bh % a.Hq;
   const int hk = hq / (a.Hq / a.Hkv);
-  const int q_row0 = qblk * QB + wave * 32;
+  const int q_row0 = qblk * QB + wave * 32;  // wave-uniform
   const int my_q = q_row0 + r;
 
   const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh;
   const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh;
   const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh;
+
+  // zero the ring once: DMA of keys past S may leave LDS unwritten, and V rows must be finite
+  // (P is exactly 0 there, but 0 * NaN is not)
+#pragma unroll
+  for (int i = 0; i < NBUF * SLOT / (NTHR * 16); ++i)
+    *reinterpret_cast<uint4*>(smem + i * NTHR * 16 + tid * 16) = make_uint4(0, 0, 0, 0);
 
   // ---- Q fragments (B operand of S^T = K Q^T): Q[my_q][16ks + 8hh + j]
   bf16x8_t qf[NKS];
@@ -96,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
   for (int d = 0; d < NDB; ++d)
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
-  float m_i = -INFINITY, l_i = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;  // running max (log2 domain, scaled) and row sum
 
   const int kv_end = CAUSAL ? min(a.S, qblk * QB + QB) : a.S;
   int ntiles = (kv_end + KB - 1) / KB;
@@ -106,9 +133,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
   if constexpr (DOC) {
     const int* ds = a.doc + (long)b * a.S;
     my_start = ds[min(my_q, a.S - 1)];
-    w_min = ds[min(q_row0, a.S - 1)];
-    w_max = ds[min(q_row0 + 31, a.S - 1)];
-    t0 = ds[min(qblk * QB, a.S - 1)] / KB;
+    w_min = __builtin_amdgcn_readfirstlane(ds[min(q_row0, a.S - 1)]);
+    w_max = __builtin_amdgcn_readfirstlane(ds[min(q_row0 + 31, a.S - 1)]);
+    t0 = __builtin_amdgcn_readfirstlane(ds[min(qblk * QB, a.S - 1)]) / KB;
   }
   if constexpr (SPLIT) {  // part 0: tiles [t0, mid), part 1: [mid, ntiles) (holds the diagonal)
     const int mid = (t0 + ntiles) / 2;
@@ -116,78 +143,73 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     else t0 = mid;
   }
 
-  // ---- staging registers for one K and one V tile
-  uint4 kst[LD_ITERS], vst[LD_ITERS];
-  auto issue = [&](int t) {
+  // ---- DMA: piece p = i*4 + wave of a tile image holds LDS bytes [p*1024, +1024), lane-linear;
+  //      the source is permuted so the image is the swizzled one (K: row image, V: tr image)
+  unsigned vk[PPW], vv[PPW];
 #pragma unroll
-    for (int it = 0; it < LD_ITERS; ++it) {
-      const int c = tid + 256 * it;
-      const int row = c / CPR, ch = c % CPR;
-      const int key = t * KB + row;
-      if (key < a.S) {
-        kst[it] = gload16(Kp + (long)key * a.k_ss + ch * 8);
-        vst[it] = gload16(Vp + (long)key * a.v_ss + ch * 8);
-      } else {
-        kst[it] = make_uint4(0, 0, 0, 0);
-        vst[it] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  auto commit = [&]() {
+  for (int i = 0; i < PPW; ++i) {
+    const int byte = (i * NW + wave) * 1024 + lane * 16;
+    const int row = byte / ROWB, pch = (byte % ROWB) >> 4;
+    vk[i] = (unsigned)((row * a.k_ss + ((pch ^ swz_row<HD>(row)) << 3)) * 2);
+    vv[i] = (unsigned)((row * a.v_ss + ((pch ^ swz_tr<HD>(row)) << 3)) * 2);
+  }
+  const unsigned lds0 = lds_addr(smem);
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    const int key0 = t * KB;
+    const int nk = min(KB, a.S - key0);
+    i32x4_t rk = buf_rsrc(Kp + (long)key0 * a.k_ss, (unsigned)(((nk - 1) * a.k_ss + HD) * 2));
+    i32x4_t rv = buf_rsrc(Vp + (long)key0 * a.v_ss, (unsigned)(((nk - 1) * a.v_ss + HD) * 2));
+    // descriptor SGPRs may come from v_readfirstlane: VALU-written SGPR -> VMEM read needs 5
+    // wait states, which hipcc does not pad into the asm below (guide §5.7 item 2)
+    asm volatile("s_nop 4" : "+s"(rk), "+s"(rv));
+    const unsigned slot = lds0 + (unsigned)(((t - t0) % NBUF) * SLOT) + wave * 1024;
 #pragma unroll
-    for (int it = 0; it < LD_ITERS; ++it) {
-      const int c = tid + 256 * it;
-      const int row = c / CPR, ch = c % CPR;
-      *reinterpret_cast<uint4*>(Ks + row_off<HD>(row, ch)) = kst[it];
-      *reinterpret_cast<uint4*>(Vs + tr_off<HD>(row, ch)) = vst[it];
+    for (int i = 0; i < PPW; ++i) {
+      buf_dma16(rk, vk[i], slot + i * NW * 1024);
+      buf_dma16(rv, vv[i], slot + TILE + i * NW * 1024);
     }
   };
 
-  issue(t0);
-  for (int t = t0; t < ntiles; ++t) {
-    __syncthreads();  // all waves finished reading the previous tile
-    commit();
-    __syncthreads();
-    if (t + 1 < ntiles) issue(t + 1);  // overlaps the MFMAs below
-    const int kv0 = t * KB;
-    if (CAUSAL && kv0 > q_row0 + 31) continue;  // tile entirely above this wave's diagonal
-    if (DOC && kv0 + KB <= w_min) continue;     // tile entirely before every query's document
-
-    // ---- S^T = K Q^T  (two 32-key blocks)
+  const float c = a.scale_log2;
+  const int key_hi = CAUSAL ? min(my_q, a.S - 1) : a.S - 1;  // last key this lane's row sees
+  // retire the Q loads here: the first in-loop use would otherwise carry a compiler vmcnt(0)
+  // on every iteration, i.e. wait for the just-issued DMA of the next tile
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
+  // one K/V tile: S^T = K Q^T, online softmax, O^T += V^T P^T.  MASK: per-score visibility
+  auto tile = [&](bool need_mask, const unsigned char* Ks, const unsigned char* Vs, int kv0) __attribute__((always_inline)) {
     f32x16 s[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8_t kf = lds_read_b128(Ks, row_off<HD>(kb * 32 + r, 2 * ks + hh));
-        s[kb] = mfma32(kf, qf[ks], s[kb]);
-      }
+      for (int ks = 0; ks < NKS; ++ks) s[kb] = mfma32(lds_read_b128(Ks, row_off<HD>(kb * 32 + r, 2 * ks + hh)), qf[ks], s[kb]);
     }
-    // ---- scale, mask, online softmax (exp2 domain)
-    const bool need_mask = (CAUSAL && kv0 + KB - 1 > q_row0) || (kv0 + KB > a.S) || (DOC && kv0 < w_max);
-    float mx = -INFINITY;
+    if (need_mask) {  // wave-uniform: a scalar branch around branch-free selects
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kv0 + kb * 32 + acc_row(i, hh);
+          bool ok = key <= key_hi;
+          if constexpr (DOC) ok = ok && key >= my_start;
+          s[kb][i] = ok ? s[kb][i] : -INFINITY;
+        }
+    }
+    float mx = s[0][0];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = s[kb][i] * a.scale_log2;
-        if (need_mask) {
-          const int key = kv0 + kb * 32 + acc_row(i, hh);
-          if ((CAUSAL && key > my_q) || key >= a.S || (DOC && key < my_start)) x = -INFINITY;
-        }
-        s[kb][i] = x;
-        mx = fmaxf(mx, x);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+      for (int i = (kb == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[kb][i]);
+    mx = xor32_max(mx) * c;
     // deferred rescale: keep the running max while no row's max grew by more than kRescaleTh
     // (p = 2^(s - m) then stays <= 2^kRescaleTh, exact in fp32 and well inside bf16 range); the
     // decision is wave-uniform, and O, l and the LSE all use the same (possibly stale) m, so the
     // result is the exact softmax.  Skips the 16*NDB O multiplies and the alpha exp per tile.
     const bool grow = __builtin_amdgcn_ballot_w64(mx > m_i + kRescaleTh) != 0;
     const float m_new = grow ? fmaxf(m_i, mx) : m_i;
-    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float nm = (m_new == -INFINITY) ? 0.f : -m_new;
     float rs = 0.f;
     bf16x8_t pb[2][2];
 #pragma unroll
@@ -195,15 +217,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
       float p[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        p[i] = fast_exp2(s[kb][i] - m_use);
+        p[i] = fast_exp2(__builtin_fmaf(s[kb][i], c, nm));
         rs += p[i];
       }
       pb[kb][0] = to_bf16x8(p);
       pb[kb][1] = to_bf16x8(p + 8);
     }
-    rs += __shfl_xor(rs, 32);
+    rs = xor32_add(rs);
     if (grow) {
-      const float alpha = fast_exp2(m_i - m_use);
+      const float alpha = fast_exp2(m_i + nm);
       l_i *= alpha;
 #pragma unroll
       for (int d = 0; d < NDB; ++d)
@@ -212,19 +234,49 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     }
     l_i += rs;
     m_i = m_new;
-    // ---- O^T += V^T P^T
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int d = 0; d < NDB; ++d) {
-          const bf16x8_t vf = tr_frag<HD>(Vs, kb * 32 + 16 * st, d * 32, lane);
-          o[d] = mfma32(vf, pb[kb][st], o[d]);
-        }
+        for (int d = 0; d < NDB; ++d) o[d] = mfma32(tr_frag<HD>(Vs, kb * 32 + 16 * st, d * 32, lane), pb[kb][st], o[d]);
+  };
+
+  __syncthreads();  // ring zeroed before any DMA lands in it
+  // tile t lives in ring slot (t - t0) % NBUF, NBUF-1 tiles in flight; the slot is a template
+  // constant (LDS offsets fold into the reads' immediates instead of costing address registers)
+  auto step = [&](auto slot_c, int t) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot_c)::value;
+    // this wave's pieces of tile t landed (the younger tiles' 2*PPW-instruction groups may
+    // still fly) ... and, after the barrier, every wave's; everyone is done with tile t-1
+    if constexpr (NBUF == 3) {
+      if (t + 1 < ntiles) vm_wait_n<2 * PPW>();
+      else vm_wait_n<0>();
+    } else {
+      vm_wait_n<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1);  // into tile t-1's slot
+    const int kv0 = t * KB;
+    bool live = true;
+    if constexpr (CAUSAL) live = kv0 <= q_row0 + 31;      // else: wholly above the wave's diagonal
+    if constexpr (DOC) live = live && kv0 + KB > w_min;   // else: before every query's document
+    if (live) {
+      const bool need_mask = (CAUSAL && kv0 + KB - 1 > q_row0) || (kv0 + KB > a.S) || (DOC && kv0 < w_max);
+      tile(need_mask, smem + SL * SLOT, smem + SL * SLOT + TILE, kv0);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (t0 + i < ntiles) issue(t0 + i);
+  for (int t = t0; t < ntiles; t += NBUF) {
+    step(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
+    if constexpr (NBUF == 3)
+      if (t + 2 < ntiles) step(std::integral_constant<int, 2>{}, t + 2);
   }
 
-  // ---- epilogue: O = O^T^T / l ; LSE
+  // ---- epilogue: O = O^T^T / l ; LSE (natural log)
   if constexpr (SPLIT) {
     if (my_q < a.S) {
       const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
@@ -306,6 +358,62 @@ __global__ __launch_bounds__(256) void fa_combine_kernel(const float* __restrict
   if (sub == 0) lse[li] = l;
 }
 
+template <int NW, int NBUF>
+std::tuple<at::Tensor, at::Tensor> fwd_launch(const at::Tensor& q, at::Tensor& o, at::Tensor& lse, FwdArgs& a, int B,
+                                              int S, int Hq, int D, bool causal,
+                                              const c10::optional<at::Tensor>& doc_start) {
+  constexpr int QB = NW * 32, WG_PER_CU = NW == 4 ? 2 : 1;
+  const int nqb = (S + QB - 1) / QB;
+  dim3 grid((unsigned)(B * Hq * nqb)), block(NW * 64);
+  auto s = stream();
+  // a grid that the CUs hold in one residency round finishes when its heaviest causal block
+  // does: split every block's K/V range over two workgroups
+  bool split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 4 &&
+               (long)B * Hq * nqb <= (long)WG_PER_CU * num_cus();
+  // LLMCTL_FA_SPLIT=0 / =1 override the heuristic (autotuner knob, llmctl.plugins.autotuning)
+  if (const char* e = std::getenv("LLMCTL_FA_SPLIT")) {
+    if (e[0] == '0') split = false;
+    else if (e[0] == '1') split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 2;
+  }
+  if (split) {
+    auto o_part = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
+    auto lse_part = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));
+    a.o_part = o_part.data_ptr<float>();
+    a.lse_part = lse_part.data_ptr<float>();
+    dim3 g2((unsigned)(2 * B * Hq * nqb));
+    const long threads = (long)B * S * Hq * (D / 8);
+    if (D == 128) {
+      hipLaunchKernelGGL((fa_fwd_kernel<128, true, false, true, NW, NBUF>), g2, block, 0, s, a);
+      hipLaunchKernelGGL(fa_combine_kernel<128>, dim3((threads + 255) / 256), dim3(256), 0, s, a.o_part, a.lse_part,
+                         bf_mut(o), lse.data_ptr<float>(), B, S, Hq, o.stride(0), o.stride(1), o.stride(2));
+    } else {
+      hipLaunchKernelGGL((fa_fwd_kernel<64, true, false, true, NW, NBUF>), g2, block, 0, s, a);
+      hipLaunchKernelGGL(fa_combine_kernel<64>, dim3((threads + 255) / 256), dim3(256), 0, s, a.o_part, a.lse_part,
+                         bf_mut(o), lse.data_ptr<float>(), B, S, Hq, o.stride(0), o.stride(1), o.stride(2));
+    }
+    return {o, lse};
+  }
+  if (doc_start.has_value() && doc_start->defined()) {
+    const at::Tensor& ds = *doc_start;
+    LLMCTL_CHECK(causal, "flash_attn_fwd: doc_start (packed sequences) needs causal attention");
+    LLMCTL_CHECK(ds.is_cuda() && ds.scalar_type() == at::kInt && ds.is_contiguous() && ds.dim() == 2 &&
+                     ds.size(0) == B && ds.size(1) == S,
+                 "flash_attn_fwd: doc_start must be contiguous int32 [B,S]");
+    a.doc = ds.data_ptr<int>();
+    if (D == 128) hipLaunchKernelGGL((fa_fwd_kernel<128, true, true, false, NW, NBUF>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<64, true, true, false, NW, NBUF>), grid, block, 0, s, a);
+    return {o, lse};
+  }
+  if (D == 128) {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<128, true, false, false, NW, NBUF>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<128, false, false, false, NW, NBUF>), grid, block, 0, s, a);
+  } else {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<64, true, false, false, NW, NBUF>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<64, false, false, false, NW, NBUF>), grid, block, 0, s, a);
+  }
+  return {o, lse};
+}
+
 }  // namespace
 
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -335,55 +443,14 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
             (float)(scale * 1.4426950408889634), nullptr, nullptr, nullptr};
-  const int nqb = (S + QB - 1) / QB;
-  dim3 grid((unsigned)(B * Hq * nqb)), block(256);
-  auto s = stream();
-  // a grid that the CUs hold in one residency round (2 workgroups per CU) finishes when its
-  // heaviest causal block does: split every block's K/V range over two workgroups
-  bool split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 4 &&
-               (long)B * Hq * nqb <= 2L * num_cus();
-  // LLMCTL_FA_SPLIT=0 / =1 override the heuristic (autotuner knob, llmctl.plugins.autotuning)
-  if (const char* e = std::getenv("LLMCTL_FA_SPLIT")) {
-    if (e[0] == '0') split = false;
-    else if (e[0] == '1') split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 2;
-  }
-  if (split) {
-    auto o_part = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
-    auto lse_part = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));
-    a.o_part = o_part.data_ptr<float>();
-    a.lse_part = lse_part.data_ptr<float>();
-    dim3 g2((unsigned)(2 * B * Hq * nqb));
-    const long threads = (long)B * S * Hq * (D / 8);
-    if (D == 128) {
-      hipLaunchKernelGGL((fa_fwd_kernel<128, true, false, true>), g2, block, 0, s, a);
-      hipLaunchKernelGGL(fa_combine_kernel<128>, dim3((threads + 255) / 256), dim3(256), 0, s, a.o_part, a.lse_part,
-                         bf_mut(o), lse.data_ptr<float>(), B, S, Hq, o.stride(0), o.stride(1), o.stride(2));
-    } else {
-      hipLaunchKernelGGL((fa_fwd_kernel<64, true, false, true>), g2, block, 0, s, a);
-      hipLaunchKernelGGL(fa_combine_kernel<64>, dim3((threads + 255) / 256), dim3(256), 0, s, a.o_part, a.lse_part,
-                         bf_mut(o), lse.data_ptr<float>(), B, S, Hq, o.stride(0), o.stride(1), o.stride(2));
-    }
-    return {o, lse};
-  }
-  if (doc_start.has_value() && doc_start->defined()) {
-    const at::Tensor& ds = *doc_start;
-    LLMCTL_CHECK(causal, "flash_attn_fwd: doc_start (packed sequences) needs causal attention");
-    LLMCTL_CHECK(ds.is_cuda() && ds.scalar_type() == at::kInt && ds.is_contiguous() && ds.dim() == 2 &&
-                     ds.size(0) == B && ds.size(1) == S,
-                 "flash_attn_fwd: doc_start must be contiguous int32 [B,S]");
-    a.doc = ds.data_ptr<int>();
-    if (D == 128) hipLaunchKernelGGL((fa_fwd_kernel<128, true, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fa_fwd_kernel<64, true, true>), grid, block, 0, s, a);
-    return {o, lse};
-  }
-  if (D == 128) {
-    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<128, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fa_fwd_kernel<128, false>), grid, block, 0, s, a);
-  } else {
-    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<64, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fa_fwd_kernel<64, false>), grid, block, 0, s, a);
-  }
-  return {o, lse};
+  // workgroup shape: LLMCTL_FA_NW=8 -> 8 waves (256 rows) with a 3-slot ring, one workgroup per
+  // CU; default 4 waves (128 rows) with a 2-slot ring, two per CU (A/B knob, tools/attn_bench.py)
+  static const int nw = [] {
+    const char* e = std::getenv("LLMCTL_FA_NW");
+    return (e && e[0] == '8') ? 8 : 4;
+  }();
+  if (nw == 8) return fwd_launch<8, 3>(q, o, lse, a, B, S, Hq, D, causal, doc_start);
+  return fwd_launch<4, 2>(q, o, lse, a, B, S, Hq, D, causal, doc_start);
 }
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("flash_attn_fwd", &flash_attn_fwd); }
