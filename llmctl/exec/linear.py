@@ -228,6 +228,25 @@ def data_grad(dy: torch.Tensor, w: torch.nn.Parameter) -> torch.Tensor:
     return F.linear(dy, wt) if wt is not None else dy.matmul(w)
 
 
+def swiglu_data_grad(dy: torch.Tensor, w: torch.nn.Parameter, gu: torch.Tensor) -> torch.Tensor:
+    """``swiglu_bwd(dy @ w, gu)`` for the MLP down projection: on gemm64 the SwiGLU backward runs
+    in the data-gradient GEMM's epilogue (``gemm64_swiglu_dgrad``: dgate / dup from the fp32 dAct
+    tile, no dAct tensor); otherwise the data gradient and the elementwise kernel separately."""
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    gu2 = gu.reshape(-1, gu.shape[-1])
+    if (dgrad64_ok(dy2, w) and gu2.is_contiguous() and gu2.data_ptr() % 16 == 0
+            and os.environ.get("LLMCTL_FUSED_SWIGLU", "1") != "0"):  # =0: unfused (A/B)
+        from llmctl.ops._lib import native
+
+        cfg = gemm64_config("dgrad", dy2.shape[0], w.shape[1], w.shape[0])
+        return native().gemm64_swiglu_dgrad(dy2, w, gu2, cfg).view(gu.shape)
+    from llmctl.ops._lib import native, use_native
+    from llmctl.ops import ref
+
+    dact = data_grad(dy, w)
+    return native().swiglu_bwd(dact, gu) if use_native(gu) else ref.swiglu_bwd(dact, gu)
+
+
 def weight_grad(w: torch.nn.Parameter, dy2: torch.Tensor, x2: torch.Tensor) -> Optional[torch.Tensor]:
     """For hand-written backward passes: route ``dy2^T x2`` through ``w``'s sink (returns
     None) or return it as an ordinary gradient."""

@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from llmctl import ops
-from llmctl.exec.linear import data_grad, linear, weight_grad
+from llmctl.exec.linear import data_grad, linear, swiglu_data_grad, weight_grad
 from llmctl.parallel import async_tp
 from llmctl.parallel import context_parallel as cp
 from llmctl.parallel import tensor_parallel as tp
@@ -75,33 +75,41 @@ def _init_linear(w: torch.Tensor, std: float) -> None:
 
 
 class _SwiGLUDown(torch.autograd.Function):
-    """Selective recompute: ``down(swiglu(gu))`` saving only ``gu`` (the [T, ffn]
-    activation is recomputed by the swiglu kernel in backward — one extra memory-bound
-    pass in exchange for T*ffn*2 bytes per layer)."""
+    """``down(swiglu(gu))`` with the SwiGLU backward fused into the down projection's data
+    gradient (``swiglu_data_grad``: gemm64's store pass computes dgate / dup from the fp32 dAct
+    tile, so dAct never round-trips through HBM).  ``recompute`` (selective activation
+    checkpointing): save only ``gu`` and recompute the [T, ffn] activation in backward — one extra
+    memory-bound pass in exchange for T*ffn*2 bytes per layer."""
 
     @staticmethod
-    def forward(ctx, gu, w_down):
+    def forward(ctx, gu, w_down, recompute=False):
         from llmctl.ops._lib import native, use_native
         from llmctl.ops import ref
 
         act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
         out = F.linear(act, w_down)
-        ctx.save_for_backward(gu, w_down)
+        ctx.recompute = recompute
+        if recompute:
+            ctx.save_for_backward(gu, w_down)
+        else:
+            ctx.save_for_backward(gu, w_down, act)
         ctx.wparam = w_down  # the Parameter (carries the grad sink)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        gu, w_down = ctx.saved_tensors
         from llmctl.ops._lib import native, use_native
         from llmctl.ops import ref
 
-        act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
+        if ctx.recompute:
+            gu, w_down = ctx.saved_tensors
+            act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
+        else:
+            gu, w_down, act = ctx.saved_tensors
         dout2 = dout.reshape(-1, dout.shape[-1])
         dw = weight_grad(ctx.wparam, dout2, act.reshape(-1, act.shape[-1]))
-        dact = data_grad(dout, ctx.wparam)
-        dgu = native().swiglu_bwd(dact, gu) if use_native(gu) else ref.swiglu_bwd(dact, gu)
-        return dgu, dw
+        dgu = swiglu_data_grad(dout, ctx.wparam, gu)
+        return dgu, dw, None
 
 
 class DecoderLayer(nn.Module):
@@ -224,10 +232,7 @@ class DecoderLayer(nn.Module):
             x = self._col_in(xn)
             if self.cfg.gated_mlp:
                 gu = linear(x, self.w_up, self.b_up)
-                if self.pc.activation_checkpoint == "selective":
-                    out = _SwiGLUDown.apply(gu, self.w_down)
-                else:
-                    out = linear(ops.swiglu(gu), self.w_down)
+                out = _SwiGLUDown.apply(gu, self.w_down, self.pc.activation_checkpoint == "selective")
             else:
                 hdn = ops.gelu(linear(x, self.w_up, self.b_up))
                 out = linear(hdn, self.w_down)

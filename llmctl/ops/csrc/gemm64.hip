@@ -63,7 +63,10 @@ constexpr int NTHR = 512;
 enum : int { A_LO = 0, A_HI = 1, B_H0 = 2, B_H1 = 3 };
 
 // epilogues
-enum : int { EPI_STORE = 0, EPI_ACC = 1 };
+// EPI_SWIGLU_BWD (down-projection data gradient): C = dAct is not stored; with gate / up read from
+// aux = gu [M, 2N] (ld = ldc), the epilogue writes dgate to C[:, n] and dup to C[:, N + n] (C = dgu),
+// i.e. the SwiGLU backward rides on the GEMM's store pass (no dAct round trip through HBM)
+enum : int { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU_BWD = 2 };
 template <int V>
 using K_ = std::integral_constant<int, V>;
 
@@ -78,7 +81,15 @@ struct G64Args {
   int splits;   // K-ranges per split tile (1: no split items)
   int kt_part;  // K-tiles per split item (even)
   float* ws;    // [n_tail][splits][256][256] fp32 partials
+  const unsigned short* aux;  // EPI_SWIGLU_BWD: gu [M, 2N], leading dimension ldc
 };
+
+// SwiGLU backward of one element: d = dL/dact, act = silu(g) * u
+__device__ __forceinline__ void swiglu_bwd1(float d, float g, float u, float& dg, float& du) {
+  const float sg = 1.f / (1.f + __expf(-g));
+  dg = d * u * (sg * (1.f + g * (1.f - sg)));
+  du = d * (g * sg);
+}
 
 __device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -343,6 +354,37 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     return;
   }
   unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 64 + 4 * g;
+  if constexpr (EPI == EPI_SWIGLU_BWD) {
+    const unsigned short* Gb = args.aux + (Cb - args.c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s2_t gv[4], uv[4];  // this row block's gate / up, loaded ahead of the math
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const unsigned short* gp = Gb + (long)(16 * i) * args.ldc + 16 * j;
+        gv[j] = *reinterpret_cast<const s2_t*>(gp);
+        uv[j] = *reinterpret_cast<const s2_t*>(gp + args.N);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        unsigned short* p = Cb + (long)(16 * i) * args.ldc + 16 * j;
+        const f32x4_t v = acc[i][j];
+        const float gf[4] = {bf2f(gv[j][0] & 0xffff), bf2f(gv[j][0] >> 16), bf2f(gv[j][1] & 0xffff), bf2f(gv[j][1] >> 16)};
+        const float uf[4] = {bf2f(uv[j][0] & 0xffff), bf2f(uv[j][0] >> 16), bf2f(uv[j][1] & 0xffff), bf2f(uv[j][1] >> 16)};
+        float dg[4], du[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) swiglu_bwd1(v[e], gf[e], uf[e], dg[e], du[e]);
+        s2_t og, ou;
+        og[0] = (unsigned)f2bf(dg[0]) | ((unsigned)f2bf(dg[1]) << 16);
+        og[1] = (unsigned)f2bf(dg[2]) | ((unsigned)f2bf(dg[3]) << 16);
+        ou[0] = (unsigned)f2bf(du[0]) | ((unsigned)f2bf(du[1]) << 16);
+        ou[1] = (unsigned)f2bf(du[2]) | ((unsigned)f2bf(du[3]) << 16);
+        *reinterpret_cast<s2_t*>(p) = og;
+        *reinterpret_cast<s2_t*>(p + args.N) = ou;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -389,6 +431,17 @@ __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
     }
   }
   unsigned short* p = args.c + (long)(tm * TM + row) * args.ldc + tn * TN + col;
+  if constexpr (EPI == EPI_SWIGLU_BWD) {
+    const unsigned short* gp = args.aux + (p - args.c);
+    float gf[8], uf[8], dg[8], du[8];
+    load8(gp, gf);
+    load8(gp + args.N, uf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) swiglu_bwd1(v[j], gf[j], uf[j], dg[j], du[j]);
+    store8(p, dg);
+    store8(p + args.N, du);
+    return;
+  }
   if constexpr (EPI == EPI_ACC) {
     float old[8];
     load8(p, old);
@@ -493,7 +546,7 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   const c10::DeviceGuard dg(a.device());
   G64Args g{reinterpret_cast<const unsigned short*>(a.data_ptr()), reinterpret_cast<const unsigned short*>(b.data_ptr()),
             reinterpret_cast<unsigned short*>(out.data_ptr()), a.stride(0), b.stride(0), out.stride(0),
-            (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr};
+            (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr, nullptr};
   plan_split(g, (int)(config / 1000));
   at::Tensor ws;
   if (g.splits > 1) {
@@ -514,6 +567,46 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   }
 }
 
-TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("gemm64_ex", &gemm64_ex); }
+// Down-projection data gradient fused with the SwiGLU backward:
+//   dAct = dy · W_down  (dy [M, H], W_down [H, F]; gemm64's dgrad layout, W read K-major)
+//   dgu[:, :F] = dAct * u * sig(g) * (1 + g (1 - sig(g))),  dgu[:, F:] = dAct * silu(g)
+// with g = gu[:, :F], u = gu[:, F:].  Returns dgu [M, 2F].
+at::Tensor gemm64_swiglu_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& gu, int64_t config) {
+  LLMCTL_CHECK(dy.dim() == 2 && w.dim() == 2 && gu.dim() == 2, "gemm64_swiglu_dgrad: 2-D operands");
+  LLMCTL_CHECK(dy.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && gu.scalar_type() == at::kBFloat16,
+               "gemm64_swiglu_dgrad: bf16 operands");
+  LLMCTL_CHECK(dy.is_cuda() && w.is_cuda() && gu.is_cuda(), "gemm64_swiglu_dgrad: GPU tensors");
+  LLMCTL_CHECK(dy.stride(1) == 1 && w.stride(1) == 1 && gu.is_contiguous(), "gemm64_swiglu_dgrad: row-major operands");
+  const long M = dy.size(0), K = dy.size(1), N = w.size(1);
+  LLMCTL_CHECK(w.size(0) == K, "gemm64_swiglu_dgrad: dy [M,H] vs W [H,F]");
+  LLMCTL_CHECK(gu.size(0) == M && gu.size(1) == 2 * N, "gemm64_swiglu_dgrad: gu must be [M, 2F]");
+  LLMCTL_CHECK(gemm64_supported(M, N, K), "gemm64_swiglu_dgrad: M,F multiples of 256, H of 128 (got ", M, "x", N, "x", K,
+               ")");
+  LLMCTL_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(gu.data_ptr()) & 15) == 0,
+               "gemm64_swiglu_dgrad: 16-byte aligned operand rows");
+  const long a_span = (long)TM * dy.stride(0) * 2, b_span = K * w.stride(0) * 2;
+  LLMCTL_CHECK(a_span < (1L << 31) && b_span < (1L << 31), "gemm64_swiglu_dgrad: operand too large for 32-bit offsets");
+  const c10::DeviceGuard dg(dy.device());
+  auto dgu = at::empty_like(gu);
+  G64Args g{reinterpret_cast<const unsigned short*>(dy.data_ptr()), reinterpret_cast<const unsigned short*>(w.data_ptr()),
+            reinterpret_cast<unsigned short*>(dgu.data_ptr()), dy.stride(0), w.stride(0), 2 * N,
+            (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr,
+            reinterpret_cast<const unsigned short*>(gu.data_ptr())};
+  plan_split(g, (int)(config / 1000));
+  at::Tensor ws;
+  if (g.splits > 1) {
+    ws = at::empty({(long)(g.tiles_m * g.tiles_n - g.n_main) * g.splits * TM * TN}, dy.options().dtype(at::kFloat));
+    g.ws = ws.data_ptr<float>();
+  }
+  launch<false, true, EPI_SWIGLU_BWD>(g, (int)(config % 1000));
+  return dgu;
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("gemm64_ex", &gemm64_ex);
+  m.impl("gemm64_swiglu_dgrad", &gemm64_swiglu_dgrad);
+}
 
 }  // namespace llmctl

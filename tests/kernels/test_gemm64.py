@@ -105,3 +105,39 @@ def test_linear_backward_on_gemm64(native_lib):
     y.backward(dy)
     assert row_err(x.grad, dy.float() @ w.detach().float()) < TOL
     assert row_err(w.grad, dy.float().t() @ x.detach().float()) < TOL
+
+
+@pytest.mark.parametrize("M,H,F", [(256, 256, 256), (512, 384, 768), (2304, 1024, 1280)])
+@pytest.mark.parametrize("config", [104, 1104, 2104])
+def test_gemm64_swiglu_dgrad(native_lib, M, H, F, config):
+    """Down-projection data gradient with the SwiGLU backward in the store epilogue (and in the
+    tail-split reduction, config 2104): dgu vs fp32 swiglu_bwd(dy @ W, gu)."""
+    dy, w, gu = _bf(M, H, seed=81), _bf(H, F, seed=82) * 0.05, _bf(M, 2 * F, seed=83)
+    dgu = native_lib.gemm64_swiglu_dgrad(dy, w, gu, config)
+    dact = dy.float() @ w.float()
+    g, u = gu[:, :F].float(), gu[:, F:].float()
+    sg = torch.sigmoid(g)
+    want = torch.cat([dact * u * sg * (1 + g * (1 - sg)), dact * g * sg], dim=1)
+    assert torch.isfinite(dgu.float()).all()
+    assert row_err(dgu[:, :F], want[:, :F]) < TOL and row_err(dgu[:, F:], want[:, F:]) < TOL
+
+
+def test_swiglu_down_autograd_fused_matches_unfused(native_lib):
+    """The MLP's _SwiGLUDown (fused dgrad, saved activation) and its selective-recompute form
+    give the gradients of swiglu -> linear through plain autograd (fp32 reference)."""
+    from llmctl.models.transformer import _SwiGLUDown
+
+    T, H, F = 512, 512, 768
+    gu = (_bf(T, 2 * F, seed=91)).requires_grad_(True)
+    w = (_bf(H, F, seed=92) * 0.05).requires_grad_(True)
+    dy = _bf(T, H, seed=93)
+    g32, w32 = gu.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    f = g32.shape[1] // 2
+    ref_out = torch.nn.functional.linear(torch.nn.functional.silu(g32[:, :f]) * g32[:, f:], w32)
+    ref_out.backward(dy.float())
+    for recompute in (False, True):
+        gu.grad = w.grad = None
+        out = _SwiGLUDown.apply(gu, w, recompute)
+        out.backward(dy)
+        assert row_err(out, ref_out.detach()) < 2e-2
+        assert row_err(gu.grad, g32.grad) < 2e-2 and row_err(w.grad, w32.grad) < 2e-2
