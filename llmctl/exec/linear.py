@@ -39,7 +39,7 @@ import torch.nn.functional as F
 # — the fastest of the A/B in profiles/gemm64_variants_r2.jsonl on every GPT-7B shape.  A
 # tuning cache (llmctl.plugins.tuning_cache) can override it per layout or per exact shape.
 GEMM64_CONFIG = int(os.environ.get("LLMCTL_GEMM64_CONFIG", "104"))
-GEMM64_CONFIGS = {"dgrad": GEMM64_CONFIG, "wgrad": GEMM64_CONFIG}
+GEMM64_CONFIGS = {"dgrad": GEMM64_CONFIG, "wgrad": GEMM64_CONFIG, "fwd": GEMM64_CONFIG}
 GEMM64_SHAPE_CONFIGS: dict = {}  # (layout, M, N, K) -> config
 
 
@@ -68,6 +68,39 @@ def _gemm64_ok(M: int, N: int, K: int, *ts: torch.Tensor) -> bool:
     from llmctl.ops._lib import use_native
 
     return use_native(ts[0]) and _rows_ok(*ts)
+
+
+def fwd64_pick(M: int, N: int, K: int) -> bool:
+    """Forward ``x W^T`` shapes routed to gemm64: the wide up-projection up to 8192 tokens and the
+    QKV / down projections at <= 2048 tokens (serving prefill chunks); hipBLASLt keeps the
+    training shapes (24576 tokens) and the rest.  Standalone sweep:
+    profiles/gemm64_fwd_small_m_r2.jsonl (up at 2048: 0.278 vs 0.422 ms); in situ, inside a
+    GPT-7B 2k prefill, hipBLASLt picks a better up-projection kernel (0.268 ms) and the gain is
+    ~1.5 ms per prefill (TTFT p50 28.0 vs 29.5 ms, profiles/ttft_fwd64_r2.txt).
+    ``LLMCTL_FWD64=0`` disables, ``=all`` forces every supported shape (A/B)."""
+    mode = os.environ.get("LLMCTL_FWD64", "1")
+    if mode == "0" or not _gemm64_enabled():
+        return False
+    if mode == "all":
+        return True
+    return (N >= 16384 and M <= 8192) or (M <= 2048 and (N >= 8192 or K >= 8192))
+
+
+def forward_linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x @ w^T (+ b)``: gemm64 for the shapes ``fwd64_pick`` selects, hipBLASLt otherwise."""
+    N, K = w.shape
+    M = x.numel() // K if x.shape[-1] == K else 0
+    if M and fwd64_pick(M, N, K) and x.dtype == torch.bfloat16:
+        x2 = x.reshape(M, K)
+        if _gemm64_ok(M, N, K, x2, w) and 256 * x2.stride(0) * 2 < 2**31 and 256 * w.stride(0) * 2 < 2**31:
+            from llmctl.ops._lib import native
+
+            y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+            native().gemm64_ex(x2, w, y, False, False, False, gemm64_config("fwd", M, N, K))
+            if b is not None:
+                y += b
+            return y.view(*x.shape[:-1], N)
+    return F.linear(x, w, b)
 
 
 def dgrad64_shape_ok(tokens: int, w: torch.Tensor) -> bool:
@@ -186,7 +219,7 @@ class _Linear(torch.autograd.Function):
         ctx.wt = None
         if sink is not None and ctx.needs_input_grad[0] and not dgrad64_shape_ok(x.numel() // x.shape[-1], w):
             ctx.wt = sink.weight_t(w)
-        return F.linear(x, w, b)
+        return forward_linear(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
@@ -213,7 +246,7 @@ class _Linear(torch.autograd.Function):
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``x @ w^T (+ b)`` on hipBLASLt; weight grads go through the parameter's sink if any."""
     if getattr(w, "_llmctl_grad_sink", None) is None or not torch.is_grad_enabled():
-        return F.linear(x, w, b)
+        return forward_linear(x, w, b)
     return _Linear.apply(x, w, b)
 
 

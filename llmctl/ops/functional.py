@@ -391,7 +391,9 @@ def decode_linear(x, w, b=None):
             and x.is_contiguous() and w.is_contiguous() and (b is None or b.is_contiguous())
             and (mode == "all" or M <= 4 or (w.shape[0] <= 4096 and (M <= 16 or x.shape[1] <= 4096)))):
         return native().skinny_linear(x, w, b)
-    return torch.nn.functional.linear(x, w, b)
+    from llmctl.exec.linear import forward_linear
+
+    return forward_linear(x, w, b)
 
 
 def sample(logits, temperature, top_k, top_p, uniform):
