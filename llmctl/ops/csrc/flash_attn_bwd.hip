@@ -274,6 +274,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
     //      dV^T += dO^T P and dK^T += Q^T dS (sum over the half's rows = the registers).
     //      One wave per SIMD: nothing else hides LDS latency, so each phase's fragments are read
     //      as a batch ahead of its MFMAs (the transposed ones before the softmax VALU).
+    //      (Interleaving half 1's S/dP MFMAs with half 0's softmax through sched_group_barrier
+    //      measured 2 % slower: 1.31 vs 1.28 ms at B12 S2048.)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x16 s, dp;

@@ -59,6 +59,7 @@ struct FwdArgs {
   const int* doc;    // [B, S] document start per token, or nullptr
   float* o_part;     // SPLIT: [2, B, S, Hq, HD] fp32 normalised partial outputs
   float* lse_part;   // SPLIT: [2, B, Hq, S] natural-log partial LSEs
+  int prio;          // raise the wave priority over its MFMA phases (A/B knob LLMCTL_FA_PRIO)
 };
 
 template <int HD, bool CAUSAL, bool DOC = false, bool SPLIT = false, int NW = 4, int NBUF = 2>
@@ -178,6 +179,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
   for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
   // one K/V tile: S^T = K Q^T, online softmax, O^T += V^T P^T.  MASK: per-score visibility
   auto tile = [&](bool need_mask, const unsigned char* Ks, const unsigned char* Vs, int kv0) __attribute__((always_inline)) {
+    // MFMA phases run at raised wave priority: when both waves of a SIMD are ready, the one
+    // feeding the matrix pipe issues first and the other's softmax VALU fills the gaps
+    if (a.prio) __builtin_amdgcn_s_setprio(1);
     f32x16 s[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -197,6 +201,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
           s[kb][i] = ok ? s[kb][i] : -INFINITY;
         }
     }
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
     float mx = s[0][0];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -234,12 +239,14 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
     }
     l_i += rs;
     m_i = m_new;
+    if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int d = 0; d < NDB; ++d) o[d] = mfma32(tr_frag<HD>(Vs, kb * 32 + 16 * st, d * 32, lane), pb[kb][st], o[d]);
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
   };
 
   __syncthreads();  // ring zeroed before any DMA lands in it
@@ -442,7 +449,12 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   FwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_mut(o), lse.data_ptr<float>(), B, S, Hq, Hkv,
             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
-            (float)(scale * 1.4426950408889634), nullptr, nullptr, nullptr};
+            (float)(scale * 1.4426950408889634), nullptr, nullptr, nullptr, 0};
+  static const int prio = [] {  // default on: 2-3 % at B12 S2048 (LLMCTL_FA_PRIO=0: off, A/B)
+    const char* e = std::getenv("LLMCTL_FA_PRIO");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  a.prio = prio;
   // workgroup shape: LLMCTL_FA_NW=8 -> 8 waves (256 rows) with a 3-slot ring, one workgroup per
   // CU; default 4 waves (128 rows) with a 2-slot ring, two per CU (A/B knob, tools/attn_bench.py)
   static const int nw = [] {
