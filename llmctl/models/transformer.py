@@ -16,6 +16,7 @@ Parallelism hooks (see ``llmctl.parallel``):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -193,6 +194,10 @@ class DecoderLayer(nn.Module):
             qkv = async_tp.column_parallel_sp(xn, self.wqkv, self.bqkv, self.pc.tp_group)
         else:
             qkv = linear(self._col_in(xn), self.wqkv, self.bqkv)
+        if rope is not None and self.pc.cp_size == 1 and os.environ.get("LLMCTL_FUSED_ROPE_ATTN", "1") != "0":
+            # RoPE + attention with the RoPE backward fused into the attention backward's stores
+            o = ops.rope_flash_attention(qkv, rope[0], rope[1], self.nq, self.nkv, B, S, positions, doc_start)
+            return self._attn_out(o, B, S)
         if rope is not None:
             q, k, v = ops.rope_qkv(qkv, rope[0], rope[1], self.nq, self.nkv, S, positions)
         else:
@@ -211,6 +216,9 @@ class DecoderLayer(nn.Module):
                                                    cp.seq_to_head(v, g), causal=True), g)
         else:
             o = ops.flash_attention(q, k, v, causal=True, doc_start=doc_start)
+        return self._attn_out(o, B, S)
+
+    def _attn_out(self, o, B, S):
         if self._async_sp():  # o-proj GEMM with the SP reduce-scatter overlapped
             out = async_tp.row_parallel_sp(o.reshape(B * S, self.nq * self.D), self.wo, self.pc.tp_group)
         else:

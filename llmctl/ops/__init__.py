@@ -24,6 +24,7 @@ from .functional import (
     prefill_work_list,
     rmsnorm,
     rope_qkv,
+    rope_flash_attention,
     rope_qkv_cache,
     sample,
     swiglu,
@@ -34,5 +35,5 @@ __all__ = [
     "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy", "decode_linear",
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
     "paged_prefill_attention", "prefill_work_list", "attn_merge_",
-    "rmsnorm", "rope_qkv", "rope_qkv_cache", "sample", "swiglu", "transpose_",
+    "rmsnorm", "rope_qkv", "rope_flash_attention", "rope_qkv_cache", "sample", "swiglu", "transpose_",
 ]

@@ -37,6 +37,7 @@ TORCH_LIBRARY(llmctl, m) {
   // attention (flash_attn_fwd.hip / flash_attn_bwd.hip)
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, Tensor? doc_start=None) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, Tensor? doc_start=None) -> (Tensor, Tensor, Tensor)");
+  m.def("flash_attn_bwd_qkv(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, Tensor? doc_start, Tensor cos, Tensor sin, Tensor? positions, int seq_len) -> Tensor");
   m.def("fa_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor delta, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int abl) -> ()");
   // serving (paged_attn.hip, sampling.hip)
   m.def("kv_cache_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot_mapping) -> ()");

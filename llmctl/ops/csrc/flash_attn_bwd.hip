@@ -50,6 +50,16 @@ struct BwdArgs {
   long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, do_sb, do_ss, do_sh;
   float scale, scale_log2;
   const int* doc;  // [B, S] document start per token (packed sequences), or nullptr
+  // outputs: element strides per token (b*S + s) and per head of dq / dk / dv ([B,S,H,HD]
+  // contiguous: H*HD and HD; straight into the QKV-projection gradient [T, (Hq+2Hkv)*HD]:
+  // (Hq+2Hkv)*HD and HD with dk / dv offset to their head ranges)
+  long dq_st, dk_st, dv_st;
+  // RoPE backward fused into the stores (cos_t != nullptr): dq / dk rows rotated back by
+  // position pos[token] (int32, or token % rope_S), table rows [pos][HD/2] fp32
+  const float* cos_t;
+  const float* sin_t;
+  const int* rope_pos;
+  int rope_S;
 };
 
 template <int HD>
@@ -125,6 +135,46 @@ __device__ __forceinline__ void store_bf16x4(unsigned short* p, const float* x, 
   for (int j = 0; j < 4; ++j) w[j] = f2bf(x[j] * mul);
   *reinterpret_cast<uint2*>(p) =
       make_uint2((unsigned)w[0] | ((unsigned)w[1] << 16), (unsigned)w[2] | ((unsigned)w[3] << 16));
+}
+
+// Inverse rotate-half RoPE of one output row held as acc[d][4g + j] = x[32d + 8g + 4h + j] (HD =
+// 128: d-blocks 0/1 pair with 2/3, i.e. column c with c + 64 in the same lane), then the bf16
+// stores; rotation and softmax scale commute (both linear).
+template <int HD, typename AccT>
+__device__ __forceinline__ void store_row(unsigned short* dst, const AccT* acc, float mul, int hh,
+                                          const float* cos_row, const float* sin_row) {
+  constexpr int NDB = HD / 32;
+  if (cos_row != nullptr) {
+    constexpr int HB = NDB / 2;  // d-blocks per half
+#pragma unroll
+    for (int d = 0; d < HB; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = d * 32 + 8 * g + 4 * hh;  // < HD/2
+        const float4 cs = *reinterpret_cast<const float4*>(cos_row + c);
+        const float4 sn = *reinterpret_cast<const float4*>(sin_row + c);
+        const float cv[4] = {cs.x, cs.y, cs.z, cs.w}, sv[4] = {sn.x, sn.y, sn.z, sn.w};
+        float lo[4], hi[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x1 = acc[d][4 * g + j], x2 = acc[d + HB][4 * g + j];
+          lo[j] = x1 * cv[j] + x2 * sv[j];
+          hi[j] = x2 * cv[j] - x1 * sv[j];
+        }
+        store_bf16x4(dst + c, lo, mul);
+        store_bf16x4(dst + c + HD / 2, hi, mul);
+      }
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < NDB; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = acc[d][4 * g + j];
+      store_bf16x4(dst + d * 32 + 8 * g + 4 * hh, x, mul);
+    }
 }
 
 // =============================================================================================
@@ -372,22 +422,17 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
 #pragma unroll
   for (int d = 0; d < NDB; ++d) asm volatile("s_nop 7\n\ts_nop 7" : "+a"(dk[d]), "+a"(dv[d]));
   if (my_key < a.S) {
-    unsigned short* dkp = a.dk + ((long)b * a.S + my_key) * a.Hkv * HD + (long)hk * HD;
-    unsigned short* dvp = a.dv + ((long)b * a.S + my_key) * a.Hkv * HD + (long)hk * HD;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int col = d * 32 + 8 * gq + 4 * hh;
-        float kx[4], vx[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          kx[j] = dk[d][4 * gq + j];
-          vx[j] = dv[d][4 * gq + j];
-        }
-        store_bf16x4(dkp + col, kx, a.scale);
-        store_bf16x4(dvp + col, vx, 1.f);
-      }
+    const long tok = (long)b * a.S + my_key;
+    unsigned short* dkp = a.dk + tok * a.dk_st + (long)hk * HD;
+    unsigned short* dvp = a.dv + tok * a.dv_st + (long)hk * HD;
+    const float *cr = nullptr, *sr = nullptr;
+    if (a.cos_t != nullptr) {
+      const long p = a.rope_pos ? (long)a.rope_pos[tok] : tok % a.rope_S;
+      cr = a.cos_t + p * (HD / 2);
+      sr = a.sin_t + p * (HD / 2);
+    }
+    store_row<HD>(dkp, dk, a.scale, hh, cr, sr);
+    store_row<HD>(dvp, dv, 1.f, hh, nullptr, nullptr);
   }
 }
 
@@ -555,16 +600,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   }
   // ---- dQ = scale * (dQ^T)^T: lane = q row, registers = d
   if (my_q < a.S) {
-    unsigned short* Op = a.dq + ((long)b * a.S + my_q) * a.Hq * HD + (long)hq * HD;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float x[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) x[j] = dq[d][4 * g + j];
-        store_bf16x4(Op + d * 32 + 8 * g + 4 * hh, x, a.scale);
-      }
+    const long tok = (long)b * a.S + my_q;
+    const float *cr = nullptr, *sr = nullptr;
+    if (a.cos_t != nullptr) {
+      const long p = a.rope_pos ? (long)a.rope_pos[tok] : tok % a.rope_S;
+      cr = a.cos_t + p * (HD / 2);
+      sr = a.sin_t + p * (HD / 2);
+    }
+    store_row<HD>(a.dq + tok * a.dq_st + (long)hq * HD, dq, a.scale, hh, cr, sr);
   }
 }
 
@@ -602,7 +645,9 @@ BwdArgs make_args(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
                  bf_mut(dq), bf_mut(dk), bf_mut(dv), (int)q.size(0), (int)q.size(1), (int)q.size(2),
                  (int)k.size(2), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
                  v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2),
-                 (float)scale, (float)(scale * 1.4426950408889634), nullptr};
+                 (float)scale, (float)(scale * 1.4426950408889634), nullptr,
+                 (long)dq.size(2) * dq.size(3), (long)dk.size(2) * dk.size(3), (long)dv.size(2) * dv.size(3),
+                 nullptr, nullptr, nullptr, 0};
 }
 
 }  // namespace
@@ -658,6 +703,78 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
   return {dq, dk, dv};
 }
 
+// Attention backward with the RoPE backward fused into the dQ / dK stores: returns the gradient of
+// the QKV projection output dqkv [B*S, (Hq + 2 Hkv) * D] directly (dq / dk rotated back by their
+// positions, dv copied), the layout ``rope_qkv`` split the projection from.  cos / sin: fp32
+// [>= max position, D/2]; positions: int32 [B*S] or none (position = token % seq_len).
+at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                              const at::Tensor& o, const at::Tensor& lse, double scale, bool causal,
+                              const c10::optional<at::Tensor>& doc_start, const at::Tensor& cos_t,
+                              const at::Tensor& sin_t, const c10::optional<at::Tensor>& positions, int64_t seq_len) {
+  LLMCTL_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4 && o.dim() == 4 && dout.dim() == 4,
+               "flash_attn_bwd_qkv: [B,S,H,D] tensors");
+  const int B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int Hkv = k.size(2);
+  LLMCTL_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128");
+  LLMCTL_CHECK(Hkv > 0 && Hq % Hkv == 0, "Hq must be a multiple of Hkv");
+  LLMCTL_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && k.sizes() == v.sizes() && k.size(0) == B &&
+                   k.size(1) == S && k.size(3) == D,
+               "shape mismatch");
+  LLMCTL_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (long)B * Hq * S,
+               "lse must be contiguous fp32 [B,Hq,S]");
+  for (const at::Tensor* t : {&dout, &q, &k, &v, &o})
+    LLMCTL_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->stride(3) == 1 && t->stride(0) % 8 == 0 &&
+                     t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0 &&
+                     (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                 "flash_attn_bwd_qkv: bf16, d-contiguous, 16-B aligned rows");
+  LLMCTL_CHECK(cos_t.is_cuda() && sin_t.is_cuda() && cos_t.scalar_type() == at::kFloat &&
+                   sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() && sin_t.is_contiguous() &&
+                   cos_t.dim() == 2 && cos_t.size(1) == D / 2 && sin_t.sizes() == cos_t.sizes(),
+               "flash_attn_bwd_qkv: cos/sin fp32 contiguous [P, D/2]");
+  const bool has_pos = positions.has_value() && positions->defined();
+  if (has_pos) {
+    LLMCTL_CHECK(positions->is_cuda() && positions->scalar_type() == at::kInt && positions->is_contiguous() &&
+                     positions->numel() == (long)B * S,
+                 "flash_attn_bwd_qkv: positions int32 [B*S]");
+  } else {
+    LLMCTL_CHECK(seq_len > 0 && seq_len <= cos_t.size(0), "flash_attn_bwd_qkv: seq_len within the tables");
+  }
+  const c10::DeviceGuard g(q.device());
+  const long W = (long)(Hq + 2 * Hkv) * D;
+  auto dqkv = at::empty({(long)B * S, W}, q.options());
+  if ((long)B * S * Hq == 0) return dqkv;
+  auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  auto s = stream();
+  const long threads = (long)B * S * Hq * (D / 8);
+  if (D == 128)
+    hipLaunchKernelGGL(delta_kernel<128>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
+                       delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
+                       o.stride(1), o.stride(2));
+  else
+    hipLaunchKernelGGL(delta_kernel<64>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
+                       delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
+                       o.stride(1), o.stride(2));
+  unsigned short* base = bf_mut(dqkv);
+  BwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
+            base, base + (long)Hq * D, base + (long)(Hq + Hkv) * D, B, S, Hq, Hkv,
+            q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+            v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2),
+            (float)scale, (float)(scale * 1.4426950408889634), nullptr, W, W, W,
+            cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), has_pos ? positions->data_ptr<int>() : nullptr,
+            (int)(has_pos ? 1 : seq_len)};
+  bool doc = false;
+  if (doc_start.has_value() && doc_start->defined()) {
+    const at::Tensor& ds = *doc_start;
+    LLMCTL_CHECK(causal && ds.is_cuda() && ds.scalar_type() == at::kInt && ds.is_contiguous() && ds.dim() == 2 &&
+                     ds.size(0) == B && ds.size(1) == S,
+                 "flash_attn_bwd_qkv: doc_start must be contiguous int32 [B,S] (causal)");
+    a.doc = ds.data_ptr<int>();
+    doc = true;
+  }
+  dispatch_bwd(a, D, causal, doc, s);
+  return dqkv;
+}
+
 // timing-only entry for tools/attn_ablate.py (causal, no documents): abl 0 = both kernels,
 // 1 = dK/dV kernel only, 2 = dQ kernel only.  ``delta`` is taken as given.
 void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -675,6 +792,7 @@ void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("flash_attn_bwd", &flash_attn_bwd);
+  m.impl("flash_attn_bwd_qkv", &flash_attn_bwd_qkv);
   m.impl("fa_bwd_ablate", &fa_bwd_ablate);
 }
 

@@ -213,6 +213,42 @@ def flash_attention(q, k, v, causal: bool = True, softmax_scale: Optional[float]
     return _FlashAttn.apply(q, k, v, scale, causal, doc_start)
 
 
+class _RopeFlashAttn(torch.autograd.Function):
+    """``rope_qkv`` + ``flash_attention`` with the RoPE backward fused into the attention
+    backward's dQ / dK stores (``flash_attn_bwd_qkv``): the backward writes the QKV-projection
+    gradient dqkv [T, (nq+2nkv)*D] directly — no dq/dk/dv tensors and no rope_bwd pass."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, nq, nkv, B, S, positions, doc_start):
+        q, k, v = native().rope_qkv_fwd(qkv, cos, sin, nq, nkv, S, positions)
+        D = q.shape[-1]
+        q, k, v = q.view(B, S, nq, D), k.view(B, S, nkv, D), v.view(B, S, nkv, D)
+        scale = D ** -0.5
+        o, lse = native().flash_attn_fwd(q, k, v, scale, True, doc_start)
+        pos = positions.reshape(-1).int().contiguous() if positions is not None else None
+        ctx.save_for_backward(q, k, v, o, lse, cos, sin, pos if pos is not None else torch.empty(0))
+        ctx.has_pos, ctx.S, ctx.scale, ctx.doc_start = pos is not None, S, scale, doc_start
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, cos, sin, pos = ctx.saved_tensors
+        dqkv = native().flash_attn_bwd_qkv(do.contiguous(), q, k, v, o, lse, ctx.scale, True, ctx.doc_start, cos, sin,
+                                           pos if ctx.has_pos else None, ctx.S)
+        return dqkv, None, None, None, None, None, None, None, None
+
+
+def rope_flash_attention(qkv, cos, sin, nq: int, nkv: int, B: int, S: int, positions=None, doc_start=None):
+    """Causal attention on the QKV projection output: RoPE(q, k) -> flash attention -> o
+    ``[B,S,nq,D]``; the backward returns d(qkv) in one fused pass on the HIP path."""
+    if use_native(qkv) and qkv.is_contiguous():
+        return _RopeFlashAttn.apply(qkv, cos, sin, nq, nkv, B, S, positions, doc_start)
+    q, k, v = rope_qkv(qkv, cos, sin, nq, nkv, S, positions)
+    D = q.shape[-1]
+    return flash_attention(q.view(B, S, nq, D), k.view(B, S, nkv, D), v.view(B, S, nkv, D), causal=True,
+                           doc_start=doc_start)
+
+
 # =============================================================================== MLP
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
@@ -404,7 +440,8 @@ def sample(logits, temperature, top_k, top_p, uniform):
 
 __all__ = [
     "transpose_",
-    "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "swiglu",
+    "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "rope_flash_attention",
+    "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
     "sample", "decode_linear", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
 ]
