@@ -27,7 +27,8 @@
 //   masking (only diagonal / sequence-end tiles run the selects); "swapped" products keep the
 //   key on the registers so dS^T is directly the B operand of dQ^T += K^T dS^T.  dQ is written
 //   once, in bf16.
-// A pre-kernel computes delta.
+// delta = rowsum(dO * O) is computed by the dQ kernel (its dO rows are in registers) and read by
+// the dK/dV kernel launched after it.
 #include "attn_common.h"
 
 namespace llmctl {
@@ -60,35 +61,12 @@ struct BwdArgs {
   const float* sin_t;
   const int* rope_pos;
   int rope_S;
+  // delta = rowsum(dO * O) computed by the dQ kernel (which holds the dO rows in registers) and
+  // written to delta_w for the dK/dV kernel launched after it; o == nullptr: delta given
+  const unsigned short* o;
+  long o_sb, o_ss, o_sh;
+  float* delta_w;
 };
-
-template <int HD>
-__global__ __launch_bounds__(256) void delta_kernel(const unsigned short* __restrict__ dout,
-                                                     const unsigned short* __restrict__ o, float* __restrict__ delta,
-                                                     int B, int S, int Hq, long do_sb, long do_ss, long do_sh,
-                                                     long o_sb, long o_ss, long o_sh) {
-  constexpr int LPR = HD / 8;  // lanes per row
-  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-  const long row = gid / LPR;
-  const int sub = gid % LPR;
-  const long R = (long)B * S * Hq;
-  float s = 0.f;
-  int b = 0, hq = 0, sq = 0;
-  if (row < R) {
-    b = row / ((long)S * Hq);
-    const long rem = row % ((long)S * Hq);
-    sq = rem / Hq;
-    hq = rem % Hq;
-    float x[8], y[8];
-    load8(dout + b * do_sb + sq * do_ss + hq * do_sh + sub * 8, x);
-    load8(o + b * o_sb + sq * o_ss + hq * o_sh + sub * 8, y);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += x[j] * y[j];
-  }
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
-  if (row < R && sub == 0) delta[((long)b * Hq + hq) * S + sq] = s;
-}
 
 // dK^T / dV^T accumulation pinned to AGPRs: through the builtin, hipcc kept these 128 registers
 // in VGPRs and shuttled the S / dP accumulators through AGPRs instead (~500 v_accvgpr moves per
@@ -491,7 +469,21 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   }
   const long rc = ((long)b * a.Hq + hq) * a.S + qc;
   const float nlse2 = -a.lse[rc] * LOG2E;
-  const float dlt = a.delta[rc];
+  float dlt;
+  if (a.o != nullptr) {  // delta of this lane's row: its 64 columns . dO, then the other half-wave's
+    const unsigned short* Op = a.o + b * a.o_sb + hq * a.o_sh + (long)qc * a.o_ss + 8 * hh;
+    float acc = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8_t of = __builtin_bit_cast(bf16x8_t, gload16(Op + 16 * ks));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += (float)of[j] * (float)df[ks][j];
+    }
+    dlt = xor32_add(acc);
+    if (hh == 0 && my_q < a.S) a.delta_w[rc] = dlt;
+  } else {
+    dlt = a.delta[rc];
+  }
   // retire the loads here (a first use inside the loop would carry a per-iteration vmcnt(0) that
   // also drains the next tile's DMA)
 #pragma unroll
@@ -647,7 +639,7 @@ BwdArgs make_args(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
                  v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2),
                  (float)scale, (float)(scale * 1.4426950408889634), nullptr,
                  (long)dq.size(2) * dq.size(3), (long)dk.size(2) * dk.size(3), (long)dv.size(2) * dv.size(3),
-                 nullptr, nullptr, nullptr, 0};
+                 nullptr, nullptr, nullptr, 0, nullptr, 0, 0, 0, nullptr};
 }
 
 }  // namespace
@@ -680,16 +672,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
   auto dv = at::empty({B, S, Hkv, D}, q.options());
   if ((long)B * S * Hq == 0) return {dq, dk, dv};
   auto s = stream();
-  const long threads = (long)B * S * Hq * (D / 8);
-  if (D == 128)
-    hipLaunchKernelGGL(delta_kernel<128>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
-                       delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
-                       o.stride(1), o.stride(2));
-  else
-    hipLaunchKernelGGL(delta_kernel<64>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
-                       delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
-                       o.stride(1), o.stride(2));
   BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, scale);
+  a.o = bf_ptr(o);
+  a.o_sb = o.stride(0);
+  a.o_ss = o.stride(1);
+  a.o_sh = o.stride(2);
+  a.delta_w = delta.data_ptr<float>();
   bool doc = false;
   if (doc_start.has_value() && doc_start->defined()) {
     const at::Tensor& ds = *doc_start;
@@ -745,15 +733,6 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& q, const
   if ((long)B * S * Hq == 0) return dqkv;
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   auto s = stream();
-  const long threads = (long)B * S * Hq * (D / 8);
-  if (D == 128)
-    hipLaunchKernelGGL(delta_kernel<128>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
-                       delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
-                       o.stride(1), o.stride(2));
-  else
-    hipLaunchKernelGGL(delta_kernel<64>, dim3((threads + 255) / 256), dim3(256), 0, s, bf_ptr(dout), bf_ptr(o),
-                       delta.data_ptr<float>(), B, S, Hq, dout.stride(0), dout.stride(1), dout.stride(2), o.stride(0),
-                       o.stride(1), o.stride(2));
   unsigned short* base = bf_mut(dqkv);
   BwdArgs a{bf_ptr(q), bf_ptr(k), bf_ptr(v), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
             base, base + (long)Hq * D, base + (long)(Hq + Hkv) * D, B, S, Hq, Hkv,
@@ -761,7 +740,8 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& q, const
             v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2),
             (float)scale, (float)(scale * 1.4426950408889634), nullptr, W, W, W,
             cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), has_pos ? positions->data_ptr<int>() : nullptr,
-            (int)(has_pos ? 1 : seq_len)};
+            (int)(has_pos ? 1 : seq_len), bf_ptr(o), o.stride(0), o.stride(1), o.stride(2),
+            delta.data_ptr<float>()};
   bool doc = false;
   if (doc_start.has_value() && doc_start->defined()) {
     const at::Tensor& ds = *doc_start;
