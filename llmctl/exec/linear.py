@@ -107,6 +107,8 @@ def dgrad64_shape_ok(tokens: int, w: torch.Tensor) -> bool:
     """Will ``dx = dy W`` for ``tokens`` rows run on gemm64?  (Decided at forward time: the
     weight's W^T copy is only kept for layers whose data gradient cannot.)"""
     out, inn = w.shape
+    if os.environ.get("LLMCTL_DGRAD64", "1") == "0":  # =0: W^T copy + hipBLASLt forward layout (A/B)
+        return False
     return _gemm64_ok(tokens, inn, out, w) and out * w.stride(0) * 2 < 2**31
 
 

@@ -51,7 +51,7 @@ def compile_flags(arch: str, save_temps: bool = False):
 # the S / dP products AGPR destinations (occupancy-1 kernel, AGPRs free) and then moved every
 # element back with v_accvgpr_read for the softmax VALU (~120 moves per tile); the dK/dV
 # accumulators are pinned to AGPRs by their inline-asm MFMAs instead.
-FILE_FLAGS = {"flash_attn_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+FILE_FLAGS = {"flash_attn_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
 
 
 def file_flags(src: Path, flags):

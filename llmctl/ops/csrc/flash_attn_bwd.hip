@@ -66,6 +66,12 @@ struct BwdArgs {
   const unsigned short* o;
   long o_sb, o_ss, o_sh;
   float* delta_w;
+  // row constants of the dK/dV kernel, written by the dQ kernel launched before it:
+  // rck_w[rc] = -lse / scale, rck_w[rc_n + rc] = -delta; the dK/dV kernel starts its S and dP
+  // accumulators from them (S' = Q K^T - lse/scale, dP' = dO V^T - delta: p = exp2(c S'),
+  // dS = p dP', no per-element subtract or LSE scaling)
+  float* rck_w;
+  long rc_n;
 };
 
 // dK^T / dV^T accumulation pinned to AGPRs: through the builtin, hipcc kept these 128 registers
@@ -249,17 +255,28 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
     vq[i] = (unsigned)((row * a.q_ss + lch * 8) * 2);
     vd[i] = (unsigned)((row * a.do_ss + lch * 8) * 2);
   }
-  const float* rc_src = wave == 1 ? a.delta : a.lse;  // wave 0: lse, 1: delta, 2: doc (DOC), 3: pad
-  auto issue = [&](int t, int g, int qi) __attribute__((always_inline)) {
-    const int q0 = q_start + qi * KV_QT;
-    const int hq = hk * group + g;
-    const int nr = min(KV_QT, a.S - q0);
-    i32x4_t rq = buf_rsrc(a.q + b * a.q_sb + hq * a.q_sh + (long)q0 * a.q_ss, (unsigned)(((nr - 1) * a.q_ss + HD) * 2));
-    i32x4_t rd = buf_rsrc(a.dout + b * a.do_sb + hq * a.do_sh + (long)q0 * a.do_ss,
-                          (unsigned)(((nr - 1) * a.do_ss + HD) * 2));
-    const long rc0 = ((long)b * a.Hq + hq) * a.S + q0;
-    i32x4_t rr = (DOC && wave == 2) ? buf_rsrc(a.doc + (long)b * a.S + q0, (unsigned)(nr * 4))
-                                    : buf_rsrc(rc_src + rc0, (unsigned)(nr * 4));
+  // wave 0: -lse/scale, 1: -delta (rck_w, from the dQ kernel), 2: doc (DOC), 3: pad.  The row
+  // constants land in accumulator-register order: LDS word 32h + 16hh + 4gq + j holds row
+  // 32h + 8gq + 4hh + j (the row of register 4gq+j of lane half hh in half-tile h)
+  const float* rc_src = a.rck_w + (wave == 1 ? a.rc_n : 0);
+  const unsigned rc_off =
+      (DOC && wave == 2) ? lane * 4
+                         : (unsigned)((32 * (lane >> 5) + 8 * ((lane >> 2) & 3) + 4 * ((lane >> 4) & 1) + (lane & 3)) * 4);
+  // scalar state of the tile being issued, advanced incrementally (a 64-row step, or the next
+  // q-head of the group at the end of the block's query range): no per-tile 64-bit products
+  int iq0 = q_start;  // its first row
+  const unsigned short* qh = a.q + b * a.q_sb + (long)(hk * group) * a.q_sh;  // head rows 0
+  const unsigned short* dh = a.dout + b * a.do_sb + (long)(hk * group) * a.do_sh;
+  const float* rh = rc_src + ((long)b * a.Hq + hk * group) * a.S;
+  const unsigned short* qc = qh + (long)q_start * a.q_ss;  // its first row in each operand
+  const unsigned short* dc = dh + (long)q_start * a.do_ss;
+  const long q_step = (long)KV_QT * a.q_ss, d_step = (long)KV_QT * a.do_ss;
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    const int nr = min(KV_QT, a.S - iq0);
+    i32x4_t rq = buf_rsrc(qc, (unsigned)(((nr - 1) * a.q_ss + HD) * 2));
+    i32x4_t rd = buf_rsrc(dc, (unsigned)(((nr - 1) * a.do_ss + HD) * 2));
+    i32x4_t rr = (DOC && wave == 2) ? buf_rsrc(a.doc + (long)b * a.S + iq0, (unsigned)(nr * 4))
+                                    : buf_rsrc(rh + iq0, (unsigned)(nr * 4));
     // descriptor SGPRs may come from v_readfirstlane: 5 wait states before a VMEM reads them
     asm volatile("s_nop 4" : "+s"(rq), "+s"(rd), "+s"(rr));
     const unsigned slot = lds0 + (unsigned)((t & 1) * BUF_B);
@@ -268,24 +285,29 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
       buf_dma16(rq, vq[i], slot + (i * 4 + wave) * 1024);
       buf_dma16(rd, vd[i], slot + TILE_B + (i * 4 + wave) * 1024);
     }
-    buf_dma4(rr, lane * 4, slot + 2 * TILE_B + wave * RC_B);
+    buf_dma4(rr, rc_off, slot + 2 * TILE_B + wave * RC_B);
+    iq0 += KV_QT;
+    qc += q_step;
+    dc += d_step;
+    if (iq0 >= q_end) {  // next q-head of the group
+      iq0 = q_start;
+      qh += a.q_sh;
+      dh += a.do_sh;
+      rh += a.S;
+      qc = qh + (long)q_start * a.q_ss;
+      dc = dh + (long)q_start * a.do_ss;
+    }
   };
 
-  // tile counters (g, qi) of the tile being issued: scalar, incremental (no per-tile division)
-  int ig = 0, iq = 0;
-  if (ntiles > 0) {
-    issue(0, ig, iq);
-    if (++iq == nq) { iq = 0; ++ig; }
-  }
+  if (ntiles > 0) issue(0);
   int qi = 0;  // q-tile index of tile t
   auto step = [&](auto slot_c, int t) __attribute__((always_inline)) {
     constexpr int SL = decltype(slot_c)::value;
     vm_wait_n<0>();                     // this wave's DMA of tile t (and of the K/V block) landed
     __builtin_amdgcn_s_barrier();       // ... and every other wave's; everyone is done with t-1
-    if (t + 1 < ntiles) {               // into tile t-1's slot; lands under this tile's MFMAs
-      issue(t + 1, ig, iq);
-      if (++iq == nq) { iq = 0; ++ig; }
-    }
+    // tile t+1 goes into tile t-1's slot and lands under this tile's MFMAs
+    const bool more = t + 1 < ntiles;
+    if (more) issue(t + 1);
     const int q0 = q_start + qi * KV_QT;
     if (++qi == nq) qi = 0;
     // wave-uniform tile classes: all of this wave's keys after all of the tile's rows -> nothing
@@ -314,8 +336,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
           qa[ks] = lds_read_b128(Qs, tr_off<HD>(32 * h + r, 2 * ks + hh));
           da[ks] = lds_read_b128(Ds, tr_off<HD>(32 * h + r, 2 * ks + hh));
         }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
+        // accumulators start at the row constants -lse/scale and -delta: the DMA stored them in
+        // register order (see rc_off), so each is one 64-B read straight into the tuple
+        s = *reinterpret_cast<const f32x16*>(lse_s + 32 * h + 16 * hh);
+        dp = *reinterpret_cast<const f32x16*>(del_s + 32 * h + 16 * hh);
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
           s = mfma32(qa[ks], kf[ks], s);
@@ -355,19 +379,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
       }
       float p[16], dsv[16];
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int row0 = 32 * h + 8 * gq + 4 * hh;
-        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + row0);
-        const float4 d4 = *reinterpret_cast<const float4*>(del_s + row0);
-        const float nl[4] = {-l4.x * LOG2E, -l4.y * LOG2E, -l4.z * LOG2E, -l4.w * LOG2E};
-        const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = 4 * gq + j;
-          const float pv = fast_exp2(__builtin_fmaf(s[i], a.scale_log2, nl[j]));
-          p[i] = pv;
-          dsv[i] = pv * (dp[i] - dv4[j]);
-        }
+      for (int i = 0; i < 16; ++i) {
+        const float pv = fast_exp2(s[i] * a.scale_log2);
+        p[i] = pv;
+        dsv[i] = pv * dp[i];
       }
       bf16x8_t pb[2], sb[2];
       pb[0] = to_bf16x8(p);
@@ -483,6 +498,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     if (hh == 0 && my_q < a.S) a.delta_w[rc] = dlt;
   } else {
     dlt = a.delta[rc];
+  }
+  if (hh == 0 && my_q < a.S) {
+    a.rck_w[rc] = -a.lse[rc] / a.scale;
+    a.rck_w[a.rc_n + rc] = -dlt;
   }
   // retire the loads here (a first use inside the loop would carry a per-iteration vmcnt(0) that
   // also drains the next tile's DMA)
@@ -639,7 +658,15 @@ BwdArgs make_args(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
                  v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2),
                  (float)scale, (float)(scale * 1.4426950408889634), nullptr,
                  (long)dq.size(2) * dq.size(3), (long)dk.size(2) * dk.size(3), (long)dv.size(2) * dv.size(3),
-                 nullptr, nullptr, nullptr, 0, nullptr, 0, 0, 0, nullptr};
+                 nullptr, nullptr, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, 0};
+}
+
+// the dQ kernel's [2, B*Hq*S] row-constant output for the dK/dV kernel (BwdArgs::rck_w)
+at::Tensor row_consts(BwdArgs& a, const at::Tensor& lse) {
+  auto rck = at::empty({2 * lse.numel()}, lse.options());
+  a.rck_w = rck.data_ptr<float>();
+  a.rc_n = lse.numel();
+  return rck;
 }
 
 }  // namespace
@@ -678,6 +705,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_attn_bwd(const at::Tensor& 
   a.o_ss = o.stride(1);
   a.o_sh = o.stride(2);
   a.delta_w = delta.data_ptr<float>();
+  auto rck = row_consts(a, lse);
   bool doc = false;
   if (doc_start.has_value() && doc_start->defined()) {
     const at::Tensor& ds = *doc_start;
@@ -741,7 +769,8 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& q, const
             (float)scale, (float)(scale * 1.4426950408889634), nullptr, W, W, W,
             cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), has_pos ? positions->data_ptr<int>() : nullptr,
             (int)(has_pos ? 1 : seq_len), bf_ptr(o), o.stride(0), o.stride(1), o.stride(2),
-            delta.data_ptr<float>()};
+            delta.data_ptr<float>(), nullptr, 0};
+  auto rck = row_consts(a, lse);
   bool doc = false;
   if (doc_start.has_value() && doc_start->defined()) {
     const at::Tensor& ds = *doc_start;
@@ -756,7 +785,8 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& q, const
 }
 
 // timing-only entry for tools/attn_ablate.py (causal, no documents): abl 0 = both kernels,
-// 1 = dK/dV kernel only, 2 = dQ kernel only.  ``delta`` is taken as given.
+// 1 = dK/dV kernel only (its row constants prepared by two small torch ops), 2 = dQ kernel only.
+// ``delta`` is taken as given.
 void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                    const at::Tensor& delta, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
                    int64_t abl) {
@@ -766,7 +796,13 @@ void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
                    dv.sizes() == k.sizes() && delta.numel() == lse.numel(),
                "fa_bwd_ablate: bf16 dq/dk/dv, fp32 delta");
   const c10::DeviceGuard g(q.device());
-  BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, 1.0 / std::sqrt((double)D));
+  const double scale = 1.0 / std::sqrt((double)D);
+  BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, scale);
+  auto rck = row_consts(a, lse);
+  if (abl == 1) {  // no dQ kernel to write them
+    rck.narrow(0, 0, lse.numel()).copy_(lse.reshape(-1) * (-1.0 / scale));
+    rck.narrow(0, lse.numel(), lse.numel()).copy_(-delta.reshape(-1));
+  }
   dispatch_bwd(a, D, true, false, stream(), abl != 1, abl != 2);
 }
 

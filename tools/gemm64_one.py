@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run one GEMM configuration a few times (for rocprofv3 --pmc runs), GPT-7B QKV shape at
-24576 tokens.  Usage: gemm64_one.py {fwd|dgrad|wgrad|torch_fwd|torch_dgrad|torch_wgrad} [config] [iters]"""
+24576 tokens.  Usage: gemm64_one.py {fwd|dgrad|wgrad|w4_*|torch_*} [config] [iters]"""
 import sys
 
 import torch
@@ -24,6 +24,9 @@ fns = {
     "fwd": lambda: ops.gemm64_ex(x, W, y, False, False, False, cfg),
     "dgrad": lambda: ops.gemm64_ex(dy, W, dx, False, True, False, cfg),
     "wgrad": lambda: ops.gemm64_ex(dy, x, g, True, True, False, cfg),
+    "w4_fwd": lambda: ops.gemm_w4_ex(x, W, y, False, False, False, cfg),
+    "w4_dgrad": lambda: ops.gemm_w4_ex(dy, W, dx, False, True, False, cfg),
+    "w4_wgrad": lambda: ops.gemm_w4_ex(dy, x, g, True, True, False, cfg),
     "torch_fwd": lambda: torch.nn.functional.linear(x, W),
     "torch_dgrad": lambda: dy.matmul(W),
     "torch_wgrad": lambda: torch.mm(dy.t(), x, out=g),
