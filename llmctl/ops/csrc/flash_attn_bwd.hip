@@ -38,7 +38,15 @@ namespace {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int KV_KB = 128;  // keys per dK/dV workgroup
 constexpr int KV_QT = 64;   // query rows per streamed tile
-constexpr int KV_NBUF = 3;  // LDS ring depth
+#ifndef LLMCTL_DKV_NBUF
+#define LLMCTL_DKV_NBUF 2
+#endif
+// LDS ring depth of the dK/dV kernel (NB-1 Q/dO tiles in flight behind the one being computed;
+// 33 KB per slot, one workgroup per CU either way: its registers allow one wave per SIMD).
+// Measured at B12 S2048: 3 and 4 slots 1.5 % slower than 2 (2.015-2.021 vs 1.99 ms): its waits are
+// LDS-read latency, not DMA (PMC: SQ_WAIT_ANY 21 % of wave cycles with either depth).
+constexpr int KV_NBUF = LLMCTL_DKV_NBUF;
+static_assert(KV_NBUF >= 2 && KV_NBUF <= 4, "dK/dV ring depth 2-4");
 constexpr int DQ_QB = 128;  // query rows per dQ workgroup
 constexpr int DQ_KB = 64;   // keys per dQ tile
 
@@ -173,7 +181,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
   constexpr int NP = TILE_B / 1024 / 4;    // 1-KiB DMA pieces per wave per operand
   constexpr int RC_B = KV_QT * 4;          // one row-constant vector
   constexpr int BUF_B = 2 * TILE_B + 4 * RC_B;  // Q | dO | lse | delta | doc | (pad)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF_B];  // 2-slot ring
+  constexpr int NB = KV_NBUF;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NB * BUF_B];  // NB-slot ring
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -198,10 +207,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
 
   // zero the ring (rows past S may stay unwritten by the DMA; every value read must be finite)
 #pragma unroll
-  for (int i = 0; i < 2 * BUF_B / 4096; ++i)
+  for (int i = 0; i < NB * BUF_B / 4096; ++i)
     *reinterpret_cast<uint4*>(smem + i * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
-  if (tid < (2 * BUF_B % 4096) / 16)
-    *reinterpret_cast<uint4*>(smem + (2 * BUF_B / 4096) * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
+  if (tid < (NB * BUF_B % 4096) / 16)
+    *reinterpret_cast<uint4*>(smem + (NB * BUF_B / 4096) * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
 
   const unsigned lds0 = lds_addr(smem);
@@ -243,7 +252,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
   }
   const int nq = q_end > q_start ? (q_end - q_start + KV_QT - 1) / KV_QT : 0;
   const int ntiles = group * nq;
-  // ---- DMA of tile (g, qi) into ring slot t & 1: every wave issues exactly 2*NP+1 instructions;
+  // ---- DMA of tile (g, qi) into ring slot t % NB: every wave issues exactly 2*NP+1 instructions;
   //      buffer descriptors re-based per tile (SALU), per-lane offsets fixed: the tr image is
   //      built by permuting the source rows/chunks; rows past S read as zeros
   unsigned vq[NP], vd[NP];
@@ -271,7 +280,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
   const unsigned short* qc = qh + (long)q_start * a.q_ss;  // its first row in each operand
   const unsigned short* dc = dh + (long)q_start * a.do_ss;
   const long q_step = (long)KV_QT * a.q_ss, d_step = (long)KV_QT * a.do_ss;
-  auto issue = [&](int t) __attribute__((always_inline)) {
+  constexpr int PT = 2 * NP + 1;  // DMA instructions per wave per tile
+  auto issue = [&](auto slot_c) __attribute__((always_inline)) {
+    constexpr int SLC = decltype(slot_c)::value;
     const int nr = min(KV_QT, a.S - iq0);
     i32x4_t rq = buf_rsrc(qc, (unsigned)(((nr - 1) * a.q_ss + HD) * 2));
     i32x4_t rd = buf_rsrc(dc, (unsigned)(((nr - 1) * a.do_ss + HD) * 2));
@@ -279,7 +290,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
                                     : buf_rsrc(rh + iq0, (unsigned)(nr * 4));
     // descriptor SGPRs may come from v_readfirstlane: 5 wait states before a VMEM reads them
     asm volatile("s_nop 4" : "+s"(rq), "+s"(rd), "+s"(rr));
-    const unsigned slot = lds0 + (unsigned)((t & 1) * BUF_B);
+    const unsigned slot = lds0 + (unsigned)(SLC * BUF_B);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       buf_dma16(rq, vq[i], slot + (i * 4 + wave) * 1024);
@@ -299,15 +310,22 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
     }
   };
 
-  if (ntiles > 0) issue(0);
+  if (ntiles > 0) issue(std::integral_constant<int, 0>{});
+  if constexpr (NB >= 3)
+    if (ntiles > 1) issue(std::integral_constant<int, 1>{});
+  if constexpr (NB >= 4)
+    if (ntiles > 2) issue(std::integral_constant<int, 2>{});
   int qi = 0;  // q-tile index of tile t
   auto step = [&](auto slot_c, int t) __attribute__((always_inline)) {
     constexpr int SL = decltype(slot_c)::value;
-    vm_wait_n<0>();                     // this wave's DMA of tile t (and of the K/V block) landed
+    // this wave's DMA of tile t landed (those of the younger tiles in flight may not have) ...
+    const int younger = min(NB - 2, ntiles - 1 - t);
+    if (NB >= 4 && younger >= 2) vm_wait_n<(NB >= 4 ? 2 * PT : 0)>();
+    else if (NB >= 3 && younger >= 1) vm_wait_n<(NB >= 3 ? PT : 0)>();
+    else vm_wait_n<0>();
     __builtin_amdgcn_s_barrier();       // ... and every other wave's; everyone is done with t-1
-    // tile t+1 goes into tile t-1's slot and lands under this tile's MFMAs
-    const bool more = t + 1 < ntiles;
-    if (more) issue(t + 1);
+    // tile t+NB-1 goes into tile t-1's slot
+    if (t + NB - 1 < ntiles) issue(std::integral_constant<int, (SL + NB - 1) % NB>{});
     const int q0 = q_start + qi * KV_QT;
     if (++qi == nq) qi = 0;
     // wave-uniform tile classes: all of this wave's keys after all of the tile's rows -> nothing
@@ -406,9 +424,13 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
       dvdk_step<NDB>(dv, dk, dfr1, qfr1, pb[1], sb[1]);
     }
   };
-  for (int t = 0; t < ntiles; t += 2) {
+  for (int t = 0; t < ntiles; t += NB) {
     step(std::integral_constant<int, 0>{}, t);
     if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
+    if constexpr (NB >= 3)
+      if (t + 2 < ntiles) step(std::integral_constant<int, 2 % NB>{}, t + 2);
+    if constexpr (NB >= 4)
+      if (t + 3 < ntiles) step(std::integral_constant<int, 3 % NB>{}, t + 3);
   }
   // ---- write dK (scaled), dV: lane = key, registers = d.  The asm MFMAs' results are read by
   //      compiler code below: 8-pass XDL D -> non-MFMA reader needs 12 wait states (unpadded by hipcc)

@@ -155,20 +155,29 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
     vv[i] = (unsigned)((row * a.v_ss + ((pch ^ swz_tr<HD>(row)) << 3)) * 2);
   }
   const unsigned lds0 = lds_addr(smem);
-  auto issue = [&](int t) __attribute__((always_inline)) {
-    const int key0 = t * KB;
-    const int nk = min(KB, a.S - key0);
-    i32x4_t rk = buf_rsrc(Kp + (long)key0 * a.k_ss, (unsigned)(((nk - 1) * a.k_ss + HD) * 2));
-    i32x4_t rv = buf_rsrc(Vp + (long)key0 * a.v_ss, (unsigned)(((nk - 1) * a.v_ss + HD) * 2));
+  // tiles are issued in order; the next one's key row and K / V row pointers advance by one tile
+  // per issue (no per-tile 64-bit products), its ring slot is a template constant
+  int ik0 = t0 * KB;
+  const unsigned short* kc = Kp + (long)ik0 * a.k_ss;
+  const unsigned short* vc = Vp + (long)ik0 * a.v_ss;
+  const long k_step = (long)KB * a.k_ss, v_step = (long)KB * a.v_ss;
+  auto issue = [&](auto slot_c) __attribute__((always_inline)) {
+    constexpr int SLC = decltype(slot_c)::value;
+    const int nk = min(KB, a.S - ik0);
+    i32x4_t rk = buf_rsrc(kc, (unsigned)(((nk - 1) * a.k_ss + HD) * 2));
+    i32x4_t rv = buf_rsrc(vc, (unsigned)(((nk - 1) * a.v_ss + HD) * 2));
     // descriptor SGPRs may come from v_readfirstlane: VALU-written SGPR -> VMEM read needs 5
     // wait states, which hipcc does not pad into the asm below (guide §5.7 item 2)
     asm volatile("s_nop 4" : "+s"(rk), "+s"(rv));
-    const unsigned slot = lds0 + (unsigned)(((t - t0) % NBUF) * SLOT) + wave * 1024;
+    const unsigned slot = lds0 + (unsigned)(SLC * SLOT) + wave * 1024;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       buf_dma16(rk, vk[i], slot + i * NW * 1024);
       buf_dma16(rv, vv[i], slot + TILE + i * NW * 1024);
     }
+    ik0 += KB;
+    kc += k_step;
+    vc += v_step;
   };
 
   const float c = a.scale_log2;
@@ -263,7 +272,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
       vm_wait_n<0>();
     }
     __builtin_amdgcn_s_barrier();
-    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1);  // into tile t-1's slot
+    if (t + NBUF - 1 < ntiles) issue(std::integral_constant<int, (SL + NBUF - 1) % NBUF>{});  // tile t-1's slot
     const int kv0 = t * KB;
     bool live = true;
     if constexpr (CAUSAL) live = kv0 <= q_row0 + 31;      // else: wholly above the wave's diagonal
@@ -273,9 +282,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
       tile(need_mask, smem + SL * SLOT, smem + SL * SLOT + TILE, kv0);
     }
   };
-#pragma unroll
-  for (int i = 0; i < NBUF - 1; ++i)
-    if (t0 + i < ntiles) issue(t0 + i);
+  if (t0 < ntiles) issue(std::integral_constant<int, 0>{});
+  if constexpr (NBUF == 3)
+    if (t0 + 1 < ntiles) issue(std::integral_constant<int, 1>{});
   for (int t = t0; t < ntiles; t += NBUF) {
     step(std::integral_constant<int, 0>{}, t);
     if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
