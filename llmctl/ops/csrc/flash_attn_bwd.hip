@@ -559,20 +559,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     vv[i] = (unsigned)((row * a.v_ss + ((pch ^ swz_row<HD>(row)) << 3)) * 2);
   }
   const unsigned lds0 = lds_addr(smem);
-  auto issue = [&](int t) __attribute__((always_inline)) {
-    const int key0 = t * DQ_KB;
-    const int nk = min(DQ_KB, a.S - key0);
-    i32x4_t rk = buf_rsrc(Kp + (long)key0 * a.k_ss, (unsigned)(((nk - 1) * a.k_ss + HD) * 2));
-    i32x4_t rv = buf_rsrc(Vp + (long)key0 * a.v_ss, (unsigned)(((nk - 1) * a.v_ss + HD) * 2));
+  // tiles are issued in order: the next one's key row and K / V pointers advance incrementally,
+  // its ring slot is a template constant
+  int ik0 = t0 * DQ_KB;
+  const unsigned short* kc = Kp + (long)ik0 * a.k_ss;
+  const unsigned short* vc = Vp + (long)ik0 * a.v_ss;
+  const long k_step = (long)DQ_KB * a.k_ss, v_step = (long)DQ_KB * a.v_ss;
+  auto issue = [&](auto slot_c) __attribute__((always_inline)) {
+    constexpr int SLC = decltype(slot_c)::value;
+    const int nk = min(DQ_KB, a.S - ik0);
+    i32x4_t rk = buf_rsrc(kc, (unsigned)(((nk - 1) * a.k_ss + HD) * 2));
+    i32x4_t rv = buf_rsrc(vc, (unsigned)(((nk - 1) * a.v_ss + HD) * 2));
     // descriptor SGPRs may come from v_readfirstlane: VALU-written SGPR -> VMEM read needs 5
     // wait states, which hipcc does not pad into the asm below (guide §5.7 item 2)
     asm volatile("s_nop 4" : "+s"(rk), "+s"(rv));
-    const unsigned slot = lds0 + (unsigned)(((t - t0) & 1) * SLOT) + wave * 1024;
+    const unsigned slot = lds0 + (unsigned)(SLC * SLOT) + wave * 1024;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       buf_dma16(rk, vk[i], slot + i * 4096);
       buf_dma16(rv, vv[i], slot + TILE + i * 4096);
     }
+    ik0 += DQ_KB;
+    kc += k_step;
+    vc += v_step;
   };
 
   auto tile = [&](bool need_mask, const unsigned char* Ks, const unsigned char* Vs, int kv0)
@@ -615,7 +624,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     constexpr int SL = decltype(slot_c)::value;
     vm_wait_n<0>();
     __builtin_amdgcn_s_barrier();
-    if (t + 1 < ntiles) issue(t + 1);
+    if (t + 1 < ntiles) issue(std::integral_constant<int, 1 - SL>{});
     const int kv0 = t * DQ_KB;
     bool live = true;
     if constexpr (CAUSAL) live = kv0 <= q_row0 + 31;
@@ -626,7 +635,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
       tile(need_mask, smem + SL * SLOT, smem + SL * SLOT + TILE, kv0);
     }
   };
-  if (t0 < ntiles) issue(t0);
+  if (t0 < ntiles) issue(std::integral_constant<int, 0>{});
   for (int t = t0; t < ntiles; t += 2) {
     step(std::integral_constant<int, 0>{}, t);
     if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
