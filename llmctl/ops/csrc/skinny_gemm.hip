@@ -131,7 +131,132 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
   }
 }
 
+// ---- x staged in LDS (v2, M <= 16) ---------------------------------------------------------------
+// skinny_gemm_kernel gives every wave its own K range, so each wave also streams the 16 token
+// rows of that range: at 16 tokens the token loads equal the weight loads (L2 traffic = the HBM
+// stream; 2.5-2.9 TB/s vs 4.2-4.6 at one token).  Here a workgroup = 4 waves on 64 weight rows
+// (one 16-row tile each, the 1-token streaming pattern: 64 B of a row per lane per K block, GB
+// blocks in flight) and ONE K chunk of KC; the chunk's token rows are staged once in LDS (row
+// stride KC*2 + 16 B: conflict-free ds_read_b128 across the 16 token rows) and shared by the 4
+// waves, so token traffic is 1/4 of the weight stream.  K chunks = gridDim.y workgroups per row
+// tile write fp32 partial tiles to ws [KS][M][N]; decode_finalize_kernel sums them (+ bias).
+template <int GB>
+__global__ __launch_bounds__(256) void decode_gemm_kernel(const unsigned short* __restrict__ x,
+                                                          const unsigned short* __restrict__ w,
+                                                          const unsigned short* __restrict__ bias,
+                                                          unsigned short* __restrict__ y, float* __restrict__ ws,
+                                                          int M, int N, int K, int KC) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char xs_raw[];
+  unsigned short* xs = reinterpret_cast<unsigned short*>(xs_raw);
+  const int XST = KC + 8;  // LDS row stride (elements)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 64 + wave * 16;
+  const int kc0 = blockIdx.y * KC;
+  const int kc = min(KC, K - kc0);  // this chunk's depth (multiple of 128)
+  // token rows of the chunk -> LDS (rows >= M as zeros)
+  const int c8 = kc >> 3;
+  for (int i = threadIdx.x; i < 16 * c8; i += 256) {
+    const int m = i / c8, c = i - m * c8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (m < M) v = *reinterpret_cast<const uint4*>(x + (long)m * K + kc0 + c * 8);
+    *reinterpret_cast<uint4*>(xs + m * XST + c * 8) = v;
+  }
+  __syncthreads();
+  const unsigned short* wrow = w + (long)(n0 + r) * K + kc0 + 32 * g;
+  const unsigned short* xrow = xs + r * XST + 32 * g;
+  f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int nb = kc / KBLK;
+  int b = 0;
+  for (; b + GB <= nb; b += GB) {
+    bf16x8_t a[GB][4];
+#pragma unroll
+    for (int u = 0; u < GB; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[u][s] = ld16(wrow + (b + u) * KBLK + 8 * s);
+    // every block of the batch in flight before the first MFMA (hipcc otherwise interleaves
+    // loads and MFMAs to save registers: ~4 loads in flight, latency-bound)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < GB; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc = mfma16(a[u][s], *reinterpret_cast<const bf16x8_t*>(xrow + (b + u) * KBLK + 8 * s), acc);
+  }
+  for (; b < nb; ++b) {
+    bf16x8_t a[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a[s] = ld16(wrow + b * KBLK + 8 * s);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma16(a[s], *reinterpret_cast<const bf16x8_t*>(xrow + b * KBLK + 8 * s), acc);
+  }
+  // D: lane holds [weight row n0 + 4g + i][token r]
+  if (r >= M) return;
+  const int n = n0 + 4 * g;
+  if (gridDim.y == 1) {
+    float o[4] = {acc[0], acc[1], acc[2], acc[3]};
+    if (bias != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += bf2f(bias[n + j]);
+    }
+    ushort4 pk;
+    pk.x = f2bf(o[0]);
+    pk.y = f2bf(o[1]);
+    pk.z = f2bf(o[2]);
+    pk.w = f2bf(o[3]);
+    *reinterpret_cast<ushort4*>(y + (long)r * N + n) = pk;
+  } else {
+    *reinterpret_cast<f32x4_t*>(ws + ((long)blockIdx.y * M + r) * N + n) = acc;
+  }
+}
+
+// y[m][n] = bf16(sum_s ws[s][m][n] + bias[n]), 4 columns per thread
+__global__ __launch_bounds__(256) void decode_finalize_kernel(const float* __restrict__ ws,
+                                                              const unsigned short* __restrict__ bias,
+                                                              unsigned short* __restrict__ y, int M, int N, int KS) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const long MN = (long)M * N;
+  if (i >= MN) return;
+  f32x4_t v = *reinterpret_cast<const f32x4_t*>(ws + i);
+  for (int sidx = 1; sidx < KS; ++sidx) v += *reinterpret_cast<const f32x4_t*>(ws + sidx * MN + i);
+  const int n = (int)(i % N);
+  float o[4] = {v[0], v[1], v[2], v[3]};
+  if (bias != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] += bf2f(bias[n + j]);
+  }
+  ushort4 pk;
+  pk.x = f2bf(o[0]);
+  pk.y = f2bf(o[1]);
+  pk.z = f2bf(o[2]);
+  pk.w = f2bf(o[3]);
+  *reinterpret_cast<ushort4*>(y + i) = pk;
+}
+
 }  // namespace
+
+// v2 launch: KC = K chunk per workgroup (multiple of 128), GB = K blocks in flight per wave
+template <int GB>
+void launch_decode(const at::Tensor& x, const at::Tensor& w, const unsigned short* bp, at::Tensor& y, int M, int N,
+                   int K, int KC) {
+  LLMCTL_CHECK(M <= 16 && N % 64 == 0 && KC % KBLK == 0, "decode_gemm: M <= 16, N % 64 == 0");
+  KC = std::min(KC, K);
+  const int KS = (K + KC - 1) / KC;
+  const size_t lds = (size_t)16 * (KC + 8) * 2;
+  at::Tensor ws;
+  float* wsp = nullptr;
+  if (KS > 1) {
+    ws = at::empty({(long)KS * M * N}, x.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  hipLaunchKernelGGL((decode_gemm_kernel<GB>), dim3(N / 64, KS), dim3(256), lds, stream(), bf_ptr(x), bf_ptr(w), bp,
+                     bf_mut(y), wsp, M, N, K, KC);
+  if (KS > 1) {
+    const long n4 = (long)M * N / 4;
+    hipLaunchKernelGGL(decode_finalize_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream(), wsp, bp,
+                       bf_mut(y), M, N, KS);
+  }
+}
 
 template <int NT, int MT, int GB, int NW>
 void launch_skinny(const at::Tensor& x, const at::Tensor& w, const unsigned short* bp, at::Tensor& y, int M, int N,
@@ -141,8 +266,8 @@ void launch_skinny(const at::Tensor& x, const at::Tensor& w, const unsigned shor
                      bf_ptr(w), bp, bf_mut(y), M, N, K);
 }
 
-// config: 0 = automatic (measured best per shape, tools/skinny_sweep.py); otherwise
-// 1 + index into {NT, GB, NW} of the table below (MT follows M: 1 for M <= 16, else 2)
+// config: 0 = automatic (measured best per shape, tools/skinny_sweep.py); 1-14: {NT, GB, NW} of
+// skinny_gemm_kernel (MT follows M: 1 for M <= 16, else 2); 20-24: the LDS-staged v2 (M <= 16)
 at::Tensor skinny_linear_cfg(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                              int64_t config) {
   LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(), "skinny_linear: 2-D contiguous");
@@ -158,10 +283,15 @@ at::Tensor skinny_linear_cfg(const at::Tensor& x, const at::Tensor& w, const c10
   const c10::DeviceGuard guard(x.device());
   auto y = at::empty({M, N}, x.options());
   int c = (int)config;
-  // automatic choice from tools/skinny_sweep.py (profiles/skinny_sweep_r2.jsonl, uncached GPT-7B
-  // weights): 4 waves x 8 K-blocks each in flight (c3) everywhere except 5..16 tokens on the
-  // narrow projections, where 2 waves x 8 blocks (c7) wins
-  if (c == 0) c = (M > 4 && M <= 16 && N <= 4096) ? 7 : 3;
+  // automatic choice from tools/skinny_sweep.py (profiles/skinny_sweep_r2*.jsonl, uncached GPT-7B
+  // weights): 4 waves x 8 K-blocks each in flight (c3) at <= 4 tokens and 17-32; at 5..16 tokens
+  // the LDS-staged v2 (c23: QKV 3.78, up 3.89, down 3.16, LM head 4.2 TB/s at 16 tokens vs
+  // hipBLASLt 3.55 / 3.35 / 2.07 / 4.16) except the 4096 x 4096 o-projection (2 waves x 8
+  // blocks, c7)
+  if (c == 0) {
+    if (M > 4 && M <= 16) c = (N <= 4096 && K <= 4096) ? 7 : (N % 64 == 0 ? 23 : 3);
+    else c = 3;
+  }
   const bool m1 = M <= 16;
   switch (c) {
     case 1: m1 ? launch_skinny<1, 1, 4, 8>(x, w, bp, y, M, N, K) : launch_skinny<1, 2, 2, 8>(x, w, bp, y, M, N, K); break;
@@ -178,6 +308,12 @@ at::Tensor skinny_linear_cfg(const at::Tensor& x, const at::Tensor& w, const c10
     case 12: m1 ? launch_skinny<8, 1, 1, 8>(x, w, bp, y, M, N, K) : launch_skinny<8, 2, 1, 8>(x, w, bp, y, M, N, K); break;
     case 13: m1 ? launch_skinny<2, 1, 4, 8>(x, w, bp, y, M, N, K) : launch_skinny<2, 2, 2, 8>(x, w, bp, y, M, N, K); break;
     case 14: m1 ? launch_skinny<4, 1, 2, 2>(x, w, bp, y, M, N, K) : launch_skinny<4, 2, 1, 2>(x, w, bp, y, M, N, K); break;
+    // v2 (token rows staged in LDS per K chunk, M <= 16): KC 1024 / 512 / 2048, 8 or 4 K blocks in flight
+    case 20: launch_decode<8>(x, w, bp, y, M, N, K, 1024); break;
+    case 21: launch_decode<4>(x, w, bp, y, M, N, K, 512); break;
+    case 22: launch_decode<8>(x, w, bp, y, M, N, K, 2048); break;
+    case 23: launch_decode<4>(x, w, bp, y, M, N, K, 1024); break;
+    case 24: launch_decode<8>(x, w, bp, y, M, N, K, 4096); break;
     default: LLMCTL_CHECK(false, "skinny_linear: unknown config ", config);
   }
   return y;

@@ -407,13 +407,15 @@ SKINNY_CONFIGS: dict = {}  # (M, N, K) -> tuned config (0 = hipBLASLt), from a t
 
 
 def decode_linear(x, w, b=None):
-    """``x @ w^T (+ b)`` for decode-shaped inputs: the weight-streaming MFMA kernel
-    (``csrc/skinny_gemm.hip``) where it beats hipBLASLt on uncached weights
-    (``profiles/skinny_sweep_r2.jsonl``): every projection at <= 4 tokens (GPT-7B QKV 21.9 vs
-    28.0 us, up 39.9 vs 53.2 us, LM head 54.4 vs 60.9 us at 1 token) and the NARROW ones
-    (out features <= 4096: o-proj, down-proj, TP shards) up to 32 tokens (o-proj at 16 tokens:
-    13.5 vs 22.0 us); wide projections at 5-32 tokens stay on hipBLASLt's small-M kernels.
-    ``LLMCTL_SKINNY_GEMM=0`` / ``=all`` force the library / kernel path (A/B)."""
+    """``x @ w^T (+ b)`` for decode-shaped inputs: the weight-streaming MFMA kernels
+    (``csrc/skinny_gemm.hip``) where they beat hipBLASLt on uncached weights
+    (``profiles/skinny_sweep_r2*.jsonl``): every projection up to 16 tokens (at 16 tokens the
+    LDS-staged v2 kernel: QKV 3.78 vs 3.55 TB/s, up 3.89 vs 3.35, down 3.16 vs 2.07) and the
+    4096 x 4096 o-projection up to 32; wide projections at 17-32 tokens stay on hipBLASLt.
+    ``LLMCTL_SKINNY_GEMM=0`` / ``=all`` force the library / kernel path, ``=narrow`` the earlier
+    routing (wide projections at 5-16 tokens on hipBLASLt) for A/B."""
+    from llmctl.exec.linear import forward_linear
+
     mode = os.environ.get("LLMCTL_SKINNY_GEMM", "1")
     M = x.shape[0] if x.dim() == 2 else 0
     tuned = SKINNY_CONFIGS.get((M, w.shape[0], w.shape[1])) if SKINNY_CONFIGS and x.dim() == 2 else None
@@ -425,10 +427,14 @@ def decode_linear(x, w, b=None):
     if (mode != "0" and use_native(x) and x.dim() == 2 and M <= 32 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and w.shape[0] % 16 == 0 and x.shape[1] % 128 == 0
             and x.is_contiguous() and w.is_contiguous() and (b is None or b.is_contiguous())
-            and (mode == "all" or M <= 4 or (w.shape[0] <= 4096 and (M <= 16 or x.shape[1] <= 4096)))):
+            and (mode == "all" or M <= 16 or (w.shape[0] <= 4096 and x.shape[1] <= 4096))):
+        if mode == "narrow":  # A/B: the previous routing (round-2 r1 kernel only, narrow projections)
+            if M <= 4:
+                return native().skinny_linear_cfg(x, w, b, 3)
+            if w.shape[0] <= 4096:
+                return native().skinny_linear_cfg(x, w, b, 7 if M <= 16 else 3)
+            return forward_linear(x, w, b)
         return native().skinny_linear(x, w, b)
-    from llmctl.exec.linear import forward_linear
-
     return forward_linear(x, w, b)
 
 

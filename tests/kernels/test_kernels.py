@@ -464,6 +464,21 @@ def test_skinny_linear_decode_gemm(native_lib, M, N, K, bias):
     assert _row_err(y, ref_y) < 1.5e-2, _row_err(y, ref_y)
 
 
+@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 24])
+@pytest.mark.parametrize("M", [1, 7, 16])
+@pytest.mark.parametrize("N,K,bias", [(192, 1024, False), (1024, 4224, True), (4096, 11008, False)])
+def test_decode_gemm_lds_staged(native_lib, cfg, M, N, K, bias):
+    """LDS-staged decode GEMM (token rows staged per K chunk, fp32 chunk partials summed by the
+    finalize kernel; chunk counts incl. a partial last chunk) vs the fp32 product."""
+    x = _bf(M, K, seed=74)
+    w = _bf(N, K, scale=0.05, seed=75)
+    b = _bf(N, seed=76) if bias else None
+    y = native_lib.skinny_linear_cfg(x, w, b, cfg)
+    ref_y = x.float() @ w.float().t() + (b.float() if bias else 0.0)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert _row_err(y, ref_y) < 1.5e-2, _row_err(y, ref_y)
+
+
 @pytest.mark.parametrize("with_pos", [False, True])
 def test_rope_qkv_cache_fused_write(native_lib, with_pos):
     """RoPE + paged-KV write in one pass == rope_qkv_fwd followed by kv_cache_write."""
