@@ -16,6 +16,8 @@
 // projections (o-proj, down-proj), slower than it on the wide ones at M >= 8, which is why
 // ops.decode_linear routes only out_features <= 4096 here.
 // Weights are read with plain loads (they are not reused within a step; the L2/MALL decides).
+#include <cstdlib>
+
 #include "attn_common.h"
 
 namespace llmctl {
@@ -193,7 +195,72 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(const unsigned short* 
   // D: lane holds [weight row n0 + 4g + i][token r]
   if (r >= M) return;
   const int n = n0 + 4 * g;
-  if (gridDim.y == 1) {
+  if (ws == nullptr) {
+    float o[4] = {acc[0], acc[1], acc[2], acc[3]};
+    if (bias != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += bf2f(bias[n + j]);
+    }
+    ushort4 pk;
+    pk.x = f2bf(o[0]);
+    pk.y = f2bf(o[1]);
+    pk.z = f2bf(o[2]);
+    pk.w = f2bf(o[3]);
+    *reinterpret_cast<ushort4*>(y + (long)r * N + n) = pk;
+  } else {
+    *reinterpret_cast<f32x4_t*>(ws + ((long)blockIdx.y * M + r) * N + n) = acc;
+  }
+}
+
+// v3 (round 2): decode_gemm_kernel with the whole chunk's weight loads (NB <= 8 K blocks, 512 B per
+// lane) issued BEFORE the token rows are staged, so the x-staging latency (L2 -> LDS, barrier)
+// overlaps the first HBM round trip of the weight stream instead of preceding it; the block
+// count is clamped on the load side (a short last chunk re-loads its last block, no per-load
+// branch) and the MFMAs of past-the-end blocks are skipped (wave-uniform).
+template <int NB>
+__global__ __launch_bounds__(256) void decode_gemm_pre_kernel(const unsigned short* __restrict__ x,
+                                                              const unsigned short* __restrict__ w,
+                                                              const unsigned short* __restrict__ bias,
+                                                              unsigned short* __restrict__ y, float* __restrict__ ws,
+                                                              int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char xs_raw[];
+  unsigned short* xs = reinterpret_cast<unsigned short*>(xs_raw);
+  constexpr int KC = NB * KBLK, XST = KC + 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 64 + wave * 16;
+  const int kc0 = blockIdx.y * KC;
+  const int kc = min(KC, K - kc0);
+  const int nb = kc / KBLK;
+  const unsigned short* wrow = w + (long)(n0 + r) * K + kc0 + 32 * g;
+  bf16x8_t a[NB][4];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int bu = u < nb ? u : nb - 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a[u][s] = ld16(wrow + bu * KBLK + 8 * s);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const int c8 = kc >> 3;
+  for (int i = threadIdx.x; i < 16 * c8; i += 256) {
+    const int m = i / c8, c = i - m * c8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (m < M) v = *reinterpret_cast<const uint4*>(x + (long)m * K + kc0 + c * 8);
+    *reinterpret_cast<uint4*>(xs + m * XST + c * 8) = v;
+  }
+  __syncthreads();
+  const unsigned short* xrow = xs + r * XST + 32 * g;
+  f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    if (u < nb) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma16(a[u][s], *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 8 * s), acc);
+    }
+  }
+  if (r >= M) return;
+  const int n = n0 + 4 * g;
+  if (ws == nullptr) {
     float o[4] = {acc[0], acc[1], acc[2], acc[3]};
     if (bias != nullptr) {
 #pragma unroll
@@ -233,7 +300,159 @@ __global__ __launch_bounds__(256) void decode_finalize_kernel(const float* __res
   *reinterpret_cast<ushort4*>(y + i) = pk;
 }
 
+
+// ---- fused decode epilogues (round 2): the finalize pass that sums the v2 K-chunk partials also
+// runs the elementwise op that followed the projection, so a decode layer launches 3 fewer
+// kernels and never round-trips the projection output through HBM.  Every epilogue first rounds
+// the projection output to bf16 exactly as the unfused path stores it (sum + bias -> bf16), so
+// the results match the unfused kernels (rope_fwd_kernel, swiglu_fwd_kernel: bit for bit;
+// norm_fwd_kernel: up to the order of the sum of squares).
+__device__ __forceinline__ f32x4_t sum_parts(const float* __restrict__ ws, long MN, int KS, long i) {
+  f32x4_t v = *reinterpret_cast<const f32x4_t*>(ws + i);
+  for (int s = 1; s < KS; ++s) v += *reinterpret_cast<const f32x4_t*>(ws + s * MN + i);
+  return v;
+}
+// projection output element as the unfused GEMM stores it
+__device__ __forceinline__ void round_out(const f32x4_t v, const unsigned short* __restrict__ bias, int n, float* o) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = bf2f(f2bf(v[j] + (bias != nullptr ? bf2f(bias[n + j]) : 0.f)));
+}
+
+// QKV projection -> RoPE (rotate-half) -> q out, K/V rows into the paged cache (slot < 0: skipped).
+// thread = (token t, head h, 8-column slice c of each half of the head)
+__global__ __launch_bounds__(256) void decode_fin_rope_kernel(const float* __restrict__ ws,
+                                                              const unsigned short* __restrict__ bias,
+                                                              const float* __restrict__ cosT,
+                                                              const float* __restrict__ sinT,
+                                                              const int* __restrict__ pos,
+                                                              const int64_t* __restrict__ slots,
+                                                              unsigned short* __restrict__ q,
+                                                              unsigned short* __restrict__ kc,
+                                                              unsigned short* __restrict__ vc, int M, int nq, int nkv,
+                                                              int D, int KS) {
+  const int CH = D >> 4, NH = nq + 2 * nkv, half = D >> 1;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)M * NH * CH) return;
+  const int c = idx % CH;
+  const int h = (idx / CH) % NH;
+  const int t = idx / ((long)CH * NH);
+  const long N = (long)NH * D, MN = (long)M * N;
+  const int na = h * D + c * 8, nb = na + half;
+  float a[8], b[8], o1[8], o2[8];
+  round_out(sum_parts(ws, MN, KS, t * N + na), bias, na, a);
+  round_out(sum_parts(ws, MN, KS, t * N + na + 4), bias, na + 4, a + 4);
+  round_out(sum_parts(ws, MN, KS, t * N + nb), bias, nb, b);
+  round_out(sum_parts(ws, MN, KS, t * N + nb + 4), bias, nb + 4, b + 4);
+  if (h < nq + nkv) {
+    const long p = pos[t];
+    const float4* cp = reinterpret_cast<const float4*>(cosT + p * half + c * 8);
+    const float4* sp = reinterpret_cast<const float4*>(sinT + p * half + c * 8);
+    float cs[8], sn[8];
+    *reinterpret_cast<float4*>(cs) = cp[0];
+    *reinterpret_cast<float4*>(cs + 4) = cp[1];
+    *reinterpret_cast<float4*>(sn) = sp[0];
+    *reinterpret_cast<float4*>(sn + 4) = sp[1];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = a[j] * cs[j] - b[j] * sn[j];
+      o2[j] = b[j] * cs[j] + a[j] * sn[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = a[j];
+      o2[j] = b[j];
+    }
+  }
+  unsigned short* dst;
+  if (h < nq) {
+    dst = q + ((long)t * nq + h) * D;
+  } else {
+    const long sl = slots[t];
+    if (sl < 0) return;
+    const bool isk = h < nq + nkv;
+    dst = (isk ? kc : vc) + (sl * nkv + (isk ? h - nq : h - nq - nkv)) * (long)D;
+  }
+  store8(dst + c * 8, o1);
+  store8(dst + half + c * 8, o2);
+}
+
+// gate/up projection [M, 2F] -> act = silu(g) * u [M, F]; thread = 4 columns of one token
+__global__ __launch_bounds__(256) void decode_fin_swiglu_kernel(const float* __restrict__ ws,
+                                                                const unsigned short* __restrict__ bias,
+                                                                unsigned short* __restrict__ act, int M, int F,
+                                                                int KS) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;  // index into act [M][F]
+  if (i >= (long)M * F) return;
+  const int m = i / F, n = i % F;
+  const long N = 2L * F, MN = (long)M * N;
+  float gv[4], uv[4];
+  round_out(sum_parts(ws, MN, KS, m * N + n), bias, n, gv);
+  round_out(sum_parts(ws, MN, KS, m * N + F + n), bias, F + n, uv);
+  ushort4 pk;
+  pk.x = f2bf(gv[0] * (1.f / (1.f + __expf(-gv[0]))) * uv[0]);
+  pk.y = f2bf(gv[1] * (1.f / (1.f + __expf(-gv[1]))) * uv[1]);
+  pk.z = f2bf(gv[2] * (1.f / (1.f + __expf(-gv[2]))) * uv[2]);
+  pk.w = f2bf(gv[3] * (1.f / (1.f + __expf(-gv[3]))) * uv[3]);
+  *reinterpret_cast<ushort4*>(act + i) = pk;
+}
+
+// row-parallel projection [M, N] + residual add + RMSNorm (the next sub-layer's input norm):
+//   s = bf16(bf16(x W^T + b) + res) -> res_out,  y = bf16(s * rsqrt(mean(s^2) + eps) * w)
+// workgroup = one token row of 1024 threads (4 columns each at N = 4096: all KS partial loads of a
+// thread in flight at once; 256 threads ran latency-bound at ~12 us); the rounded row is kept in
+// LDS between the two passes
+__global__ __launch_bounds__(1024) void decode_fin_add_rmsnorm_kernel(const float* __restrict__ ws,
+                                                                     const unsigned short* __restrict__ bias,
+                                                                     const unsigned short* __restrict__ res,
+                                                                     const unsigned short* __restrict__ nw,
+                                                                     unsigned short* __restrict__ y,
+                                                                     unsigned short* __restrict__ res_out, int M, int N,
+                                                                     int KS, float eps) {
+  extern __shared__ __attribute__((aligned(16))) float srow[];
+  __shared__ float red[16];
+  const int m = blockIdx.x;
+  const long MN = (long)M * N, base = (long)m * N;
+  float ss = 0.f;
+  for (int n = threadIdx.x * 4; n < N; n += 4096) {
+    float o[4];
+    round_out(sum_parts(ws, MN, KS, base + n), bias, n, o);
+    const ushort4 rv = *reinterpret_cast<const ushort4*>(res + base + n);
+    const unsigned short r4[4] = {rv.x, rv.y, rv.z, rv.w};
+    ushort4 pk;
+    unsigned short* pp = reinterpret_cast<unsigned short*>(&pk);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pp[j] = f2bf(o[j] + bf2f(r4[j]));
+      const float sv = bf2f(pp[j]);
+      srow[n + j] = sv;
+      ss += sv * sv;
+    }
+    *reinterpret_cast<ushort4*>(res_out + base + n) = pk;
+  }
+  const float rs = rsqrtf(block_sum<16>(ss, red) / (float)N + eps);  // (barrier: srow complete)
+  for (int n = threadIdx.x * 4; n < N; n += 4096) {
+    const ushort4 wv = *reinterpret_cast<const ushort4*>(nw + n);
+    ushort4 pk;
+    pk.x = f2bf(srow[n] * rs * bf2f(wv.x));
+    pk.y = f2bf(srow[n + 1] * rs * bf2f(wv.y));
+    pk.z = f2bf(srow[n + 2] * rs * bf2f(wv.z));
+    pk.w = f2bf(srow[n + 3] * rs * bf2f(wv.w));
+    *reinterpret_cast<ushort4*>(y + base + n) = pk;
+  }
+}
+
 }  // namespace
+
+// v3 (weight loads issued before the x staging) for the fused decode projections and config 25;
+// LLMCTL_DECODE_V3=0 keeps the v2 kernel there (A/B)
+bool decode_v3() {
+  static const bool on = [] {
+    const char* e = std::getenv("LLMCTL_DECODE_V3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // v2 launch: KC = K chunk per workgroup (multiple of 128), GB = K blocks in flight per wave
 template <int GB>
@@ -251,6 +470,27 @@ void launch_decode(const at::Tensor& x, const at::Tensor& w, const unsigned shor
   }
   hipLaunchKernelGGL((decode_gemm_kernel<GB>), dim3(N / 64, KS), dim3(256), lds, stream(), bf_ptr(x), bf_ptr(w), bp,
                      bf_mut(y), wsp, M, N, K, KC);
+  if (KS > 1) {
+    const long n4 = (long)M * N / 4;
+    hipLaunchKernelGGL(decode_finalize_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream(), wsp, bp,
+                       bf_mut(y), M, N, KS);
+  }
+}
+
+// v3 launch (KC = 1024): chunk partials + decode_finalize_kernel
+void launch_decode_v3(const at::Tensor& x, const at::Tensor& w, const unsigned short* bp, at::Tensor& y, int M, int N,
+                      int K) {
+  LLMCTL_CHECK(M <= 16 && N % 64 == 0, "decode_gemm: M <= 16, N % 64 == 0");
+  constexpr int KC = 1024;
+  const int KS = (K + KC - 1) / KC;
+  at::Tensor ws;
+  float* wsp = nullptr;
+  if (KS > 1) {
+    ws = at::empty({(long)KS * M * N}, x.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  hipLaunchKernelGGL((decode_gemm_pre_kernel<KC / KBLK>), dim3(N / 64, KS), dim3(256), (size_t)16 * (KC + 8) * 2,
+                     stream(), bf_ptr(x), bf_ptr(w), bp, bf_mut(y), wsp, M, N, K);
   if (KS > 1) {
     const long n4 = (long)M * N / 4;
     hipLaunchKernelGGL(decode_finalize_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream(), wsp, bp,
@@ -289,7 +529,7 @@ at::Tensor skinny_linear_cfg(const at::Tensor& x, const at::Tensor& w, const c10
   // hipBLASLt 3.55 / 3.35 / 2.07 / 4.16) except the 4096 x 4096 o-projection (2 waves x 8
   // blocks, c7)
   if (c == 0) {
-    if (M > 4 && M <= 16) c = (N <= 4096 && K <= 4096) ? 7 : (N % 64 == 0 ? 23 : 3);
+    if (M > 4 && M <= 16) c = (N <= 4096 && K <= 4096) ? 7 : (N % 64 == 0 ? (decode_v3() ? 25 : 23) : 3);
     else c = 3;
   }
   const bool m1 = M <= 16;
@@ -314,6 +554,7 @@ at::Tensor skinny_linear_cfg(const at::Tensor& x, const at::Tensor& w, const c10
     case 22: launch_decode<8>(x, w, bp, y, M, N, K, 2048); break;
     case 23: launch_decode<4>(x, w, bp, y, M, N, K, 1024); break;
     case 24: launch_decode<8>(x, w, bp, y, M, N, K, 4096); break;
+    case 25: launch_decode_v3(x, w, bp, y, M, N, K); break;
     default: LLMCTL_CHECK(false, "skinny_linear: unknown config ", config);
   }
   return y;
@@ -323,9 +564,122 @@ at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w, const c10::op
   return skinny_linear_cfg(x, w, bias, 0);
 }
 
+// ---- fused decode projections (v2 GEMM partials + epilogue finalize), M <= 16 ------------------
+namespace {
+constexpr int kFusedKC = 1024;  // K chunk of the fused projections (config 23's)
+
+void check_decode_operands(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                           const char* who) {
+  LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(), who, ": 2-D contiguous");
+  LLMCTL_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+               who, ": bf16 GPU operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  LLMCTL_CHECK(w.size(1) == K && M >= 1 && M <= 16 && N % 64 == 0 && K % KBLK == 0, who,
+               ": needs M <= 16, N % 64 == 0, K % 128 == 0 (got ", M, "x", N, "x", K, ")");
+  if (bias.has_value() && bias->defined())
+    LLMCTL_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N, who,
+                 ": bias [N] bf16");
+}
+
+const unsigned short* bias_ptr(const c10::optional<at::Tensor>& bias) {
+  return bias.has_value() && bias->defined() ? bf_ptr(*bias) : nullptr;
+}
+
+// x W^T as fp32 K-chunk partials ws [KS][M][N]; returns KS
+int decode_partials(const at::Tensor& x, const at::Tensor& w, at::Tensor& ws) {
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  const int KC = std::min(kFusedKC, K);
+  const int KS = (K + KC - 1) / KC;
+  ws = at::empty({(long)KS * M * N}, x.options().dtype(at::kFloat));
+  if (decode_v3())  // (its LDS row stride is the full chunk's, whatever K is)
+    hipLaunchKernelGGL((decode_gemm_pre_kernel<kFusedKC / KBLK>), dim3(N / 64, KS), dim3(256),
+                       (size_t)16 * (kFusedKC + 8) * 2, stream(), bf_ptr(x),
+                       bf_ptr(w), nullptr, nullptr, ws.data_ptr<float>(), M, N, K);
+  else
+    hipLaunchKernelGGL((decode_gemm_kernel<4>), dim3(N / 64, KS), dim3(256), (size_t)16 * (KC + 8) * 2, stream(),
+                       bf_ptr(x), bf_ptr(w), nullptr, nullptr, ws.data_ptr<float>(), M, N, K, KC);
+  return KS;
+}
+}  // namespace
+
+// q [M, nq, D] = RoPE(x Wqkv^T + b)[:, :nq]; K/V rows RoPE'd / copied into the paged cache at slots
+at::Tensor decode_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                                 const at::Tensor& cosT, const at::Tensor& sinT, int64_t nq, int64_t nkv,
+                                 const at::Tensor& positions, at::Tensor& k_cache, at::Tensor& v_cache,
+                                 const at::Tensor& slots) {
+  check_decode_operands(x, w, bias, "decode_qkv_rope_cache");
+  const int M = x.size(0), N = w.size(0);
+  const int NH = nq + 2 * nkv;
+  LLMCTL_CHECK(N % NH == 0, "decode_qkv_rope_cache: qkv width not divisible by heads");
+  const int D = N / NH;
+  LLMCTL_CHECK(D % 16 == 0, "decode_qkv_rope_cache: head_dim must be a multiple of 16");
+  LLMCTL_CHECK(cosT.is_cuda() && sinT.is_cuda() && cosT.scalar_type() == at::kFloat && sinT.scalar_type() == at::kFloat &&
+                   cosT.is_contiguous() && sinT.is_contiguous() && cosT.dim() == 2 && cosT.size(1) == D / 2 &&
+                   cosT.sizes() == sinT.sizes(),
+               "decode_qkv_rope_cache: cos/sin must be contiguous fp32 [P, D/2] GPU tables");
+  LLMCTL_CHECK(positions.scalar_type() == at::kInt && positions.is_contiguous() && positions.numel() == M,
+               "decode_qkv_rope_cache: positions int32 [M]");
+  LLMCTL_CHECK(slots.scalar_type() == at::kLong && slots.is_contiguous() && slots.numel() == M,
+               "decode_qkv_rope_cache: slots int64 [M]");
+  LLMCTL_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.scalar_type() == at::kBFloat16 &&
+                   v_cache.sizes() == k_cache.sizes() && k_cache.dim() == 4 && k_cache.size(2) == nkv &&
+                   k_cache.size(3) == D,
+               "decode_qkv_rope_cache: k/v cache contiguous bf16 [blocks, block_size, Hkv, D]");
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor ws;
+  const int KS = decode_partials(x, w, ws);
+  auto q = at::empty({M, nq, D}, x.options());
+  const long total = (long)M * NH * (D / 16);
+  hipLaunchKernelGGL(decode_fin_rope_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(),
+                     ws.data_ptr<float>(), bias_ptr(bias), cosT.data_ptr<float>(), sinT.data_ptr<float>(),
+                     positions.data_ptr<int>(), slots.data_ptr<int64_t>(), bf_mut(q), bf_mut(k_cache),
+                     bf_mut(v_cache), M, (int)nq, (int)nkv, D, KS);
+  return q;
+}
+
+// act [M, F] = silu(g) * u of the gate/up projection gu = x W^T + b  ([M, 2F], gate first)
+at::Tensor decode_up_swiglu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+  check_decode_operands(x, w, bias, "decode_up_swiglu");
+  const int M = x.size(0), N = w.size(0), F = N / 2;
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor ws;
+  const int KS = decode_partials(x, w, ws);
+  auto act = at::empty({M, F}, x.options());
+  const long n4 = (long)M * F / 4;
+  hipLaunchKernelGGL(decode_fin_swiglu_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream(),
+                     ws.data_ptr<float>(), bias_ptr(bias), bf_mut(act), M, F, KS);
+  return act;
+}
+
+// (y, res_out): res_out = (x W^T + b) + res, y = rmsnorm(res_out) * norm_w
+std::tuple<at::Tensor, at::Tensor> decode_linear_add_rmsnorm(const at::Tensor& x, const at::Tensor& w,
+                                                             const c10::optional<at::Tensor>& bias,
+                                                             const at::Tensor& res, const at::Tensor& norm_w,
+                                                             double eps) {
+  check_decode_operands(x, w, bias, "decode_linear_add_rmsnorm");
+  const int M = x.size(0), N = w.size(0);
+  LLMCTL_CHECK(res.is_contiguous() && res.scalar_type() == at::kBFloat16 && res.dim() == 2 && res.size(0) == M &&
+                   res.size(1) == N,
+               "decode_linear_add_rmsnorm: residual bf16 [M, N]");
+  LLMCTL_CHECK(norm_w.is_contiguous() && norm_w.scalar_type() == at::kBFloat16 && norm_w.numel() == N,
+               "decode_linear_add_rmsnorm: norm weight bf16 [N]");
+  LLMCTL_CHECK(N <= 16384, "decode_linear_add_rmsnorm: N <= 16384 (row staged in LDS)");
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor ws;
+  const int KS = decode_partials(x, w, ws);
+  auto y = at::empty({M, N}, x.options());
+  auto res_out = at::empty({M, N}, x.options());
+  hipLaunchKernelGGL(decode_fin_add_rmsnorm_kernel, dim3(M), dim3(1024), (size_t)N * 4, stream(), ws.data_ptr<float>(),
+                     bias_ptr(bias), bf_ptr(res), bf_ptr(norm_w), bf_mut(y), bf_mut(res_out), M, N, KS, (float)eps);
+  return {y, res_out};
+}
+
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("skinny_linear", &skinny_linear);
   m.impl("skinny_linear_cfg", &skinny_linear_cfg);
+  m.impl("decode_qkv_rope_cache", &decode_qkv_rope_cache);
+  m.impl("decode_up_swiglu", &decode_up_swiglu);
+  m.impl("decode_linear_add_rmsnorm", &decode_linear_add_rmsnorm);
 }
 
 }  // namespace llmctl

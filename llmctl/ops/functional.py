@@ -438,6 +438,42 @@ def decode_linear(x, w, b=None):
     return forward_linear(x, w, b)
 
 
+def decode_fused_ok(x, w) -> bool:
+    """Can this decode projection run with a fused epilogue (``csrc/skinny_gemm.hip``: the v2
+    weight-streaming GEMM's K-chunk partials summed by a finalize pass that also applies RoPE +
+    paged-cache write, SwiGLU or residual + RMSNorm)?  <= 16 tokens, bf16, out features a
+    multiple of 64, in features of 128.  ``LLMCTL_DECODE_FUSED=0`` disables (A/B)."""
+    return (os.environ.get("LLMCTL_DECODE_FUSED", "1") != "0" and use_native(x) and x.dim() == 2
+            and 1 <= x.shape[0] <= 16 and x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous()
+            and w.is_contiguous() and w.shape[0] % 64 == 0 and x.shape[1] % 128 == 0)
+
+
+def decode_qkv_rope_cache(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cache, v_cache, slots):
+    """Decode QKV projection + RoPE + paged-cache write of K/V in one finalize pass; returns
+    ``q [T, nq, D]``.  Same result as ``rope_qkv_cache(decode_linear(x, w, b), ...)[0]``."""
+    if decode_fused_ok(x, w):
+        return native().decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, positions.to(torch.int32).contiguous(),
+                                              k_cache, v_cache, slots)
+    return rope_qkv_cache(decode_linear(x, w, b), cos, sin, nq, nkv, 0, positions, k_cache, v_cache, slots)[0]
+
+
+def decode_up_swiglu(x, w, b=None):
+    """Decode gate/up projection with SwiGLU in its finalize pass: ``silu(g) * u`` of
+    ``x @ w^T (+ b)`` (gate = first half of the out features)."""
+    if decode_fused_ok(x, w):
+        return native().decode_up_swiglu(x, w, b)
+    return swiglu(decode_linear(x, w, b))
+
+
+def decode_linear_add_rmsnorm(x, w, b, residual, norm_w, eps: float):
+    """Decode row projection + residual add + RMSNorm in one finalize pass:
+    ``(rmsnorm(y + residual) * norm_w, y + residual)`` with ``y = x @ w^T (+ b)``."""
+    if decode_fused_ok(x, w) and w.shape[0] <= 16384:
+        return native().decode_linear_add_rmsnorm(x, w, b, residual, norm_w, eps)
+    y = decode_linear(x, w, b)
+    return add_rmsnorm(y, residual, norm_w, eps)
+
+
 def sample(logits, temperature, top_k, top_p, uniform):
     if use_native(logits):
         return native().sample(logits, temperature, top_k, top_p, uniform)
@@ -449,5 +485,6 @@ __all__ = [
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "rope_flash_attention",
     "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample", "decode_linear", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
+    "sample", "decode_linear", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu",
+    "decode_linear_add_rmsnorm", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
 ]

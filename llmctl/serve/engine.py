@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -232,7 +233,21 @@ class InferenceEngine:
         return self._final(x.index_select(0, last), res.index_select(0, last))
 
     # ------------------------------------------------------------------ decode
+    def _fused_decode(self) -> bool:
+        """Decode layers on the fused-epilogue projections (``ops.decode_qkv_rope_cache`` /
+        ``decode_up_swiglu`` / ``decode_linear_add_rmsnorm``): 7 kernels per layer instead of 10
+        (no separate RoPE/cache-write, SwiGLU or add+RMSNorm passes).  Needs the GPU path, TP=1
+        (the row-parallel all-reduce sits between a projection and the next norm), RMSNorm,
+        RoPE and a gated MLP; ``LLMCTL_DECODE_FUSED=0`` keeps the unfused layer (A/B)."""
+        cfg, m = self.cfg, self.model
+        return (self.device.type == "cuda" and self.tp == 1 and self.rope is not None and cfg.gated_mlp
+                and not cfg.is_moe and m.final_norm_b is None
+                and all(l.attn_norm_b is None and l.mlp_norm_b is None for l in m.layers)
+                and os.environ.get("LLMCTL_DECODE_FUSED", "1") != "0")
+
     def _decode_body(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
+        if self._fused_decode():
+            return self._decode_body_fused(ids, positions, slots, block_tables, ctx_lens)
         x = self._embed(ids, positions)
         res = None
         kc, vc = self.kv_cache.k, self.kv_cache.v
@@ -246,6 +261,24 @@ class InferenceEngine:
             xn, res = self._norm(layer, a, res, "mlp")
             x = self._mlp(layer, xn)
         return self._final(x, res)
+
+    def _decode_body_fused(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
+        m = self.model
+        eps = self.cfg.layer_norm_eps
+        layers = m.layers
+        kc, vc = self.kv_cache.k, self.kv_cache.v
+        x = self._embed(ids, positions)
+        xn, res = ops.rmsnorm(x, layers[0].attn_norm_w, eps), x
+        for li, layer in enumerate(layers):
+            q = ops.decode_qkv_rope_cache(xn, layer.wqkv, layer.bqkv, self.rope[0], self.rope[1], layer.nq,
+                                          layer.nkv, positions, kc[li], vc[li], slots)
+            o = ops.paged_attention_decode(q, kc[li], vc[li], block_tables, ctx_lens)
+            xn, res = ops.decode_linear_add_rmsnorm(o.view(o.shape[0], -1), layer.wo, layer.bo, res,
+                                                    layer.mlp_norm_w, eps)
+            act = ops.decode_up_swiglu(xn, layer.w_up, layer.b_up)
+            nw = layers[li + 1].attn_norm_w if li + 1 < len(layers) else m.final_norm_w
+            xn, res = ops.decode_linear_add_rmsnorm(act, layer.w_down, layer.b_down, res, nw, eps)
+        return self._gather_vocab(ops.decode_linear(xn, m.head_weight()))
 
     def _bucket(self, n: int) -> int:
         b = 1

@@ -464,9 +464,10 @@ def test_skinny_linear_decode_gemm(native_lib, M, N, K, bias):
     assert _row_err(y, ref_y) < 1.5e-2, _row_err(y, ref_y)
 
 
-@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 24])
+@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 24, 25])
 @pytest.mark.parametrize("M", [1, 7, 16])
-@pytest.mark.parametrize("N,K,bias", [(192, 1024, False), (1024, 4224, True), (4096, 11008, False)])
+@pytest.mark.parametrize("N,K,bias", [(192, 1024, False), (1024, 4224, True), (4096, 11008, False),
+                                      (256, 384, True)])
 def test_decode_gemm_lds_staged(native_lib, cfg, M, N, K, bias):
     """LDS-staged decode GEMM (token rows staged per K chunk, fp32 chunk partials summed by the
     finalize kernel; chunk counts incl. a partial last chunk) vs the fp32 product."""
@@ -558,3 +559,67 @@ def test_rope_flash_attention_fused_backward(native_lib, B, S, nq, nkv, D, with_
         tol = 8e-2 if name == "dq" else 4e-2
         err = _row_err(g[:, lo:hi], gr[:, lo:hi], floor=0.5)
         assert err < tol, (name, err)
+
+
+# ---- fused decode epilogues (skinny_gemm.hip: v2 partials + RoPE/cache, SwiGLU, add+RMSNorm) ----
+@pytest.mark.parametrize("M,K,bias", [(1, 4096, False), (5, 2048, True), (16, 4096, False), (16, 1024, True)])
+def test_decode_qkv_rope_cache_fused(native_lib, M, K, bias):
+    """QKV projection + RoPE + paged-cache write in the GEMM's finalize pass == the unfused
+    v2 GEMM (config 23) followed by rope_qkv_cache_fwd, bit for bit (q and both caches)."""
+    nq, nkv, D, bs, nb = 8, 2, 128, 16, 8
+    N = (nq + 2 * nkv) * D
+    x = _bf(M, K, seed=91)
+    w = _bf(N, K, scale=0.05, seed=92)
+    b = _bf(N, seed=93) if bias else None
+    cos, sin = ref.rope_tables(256, D, base=10000.0, device=DEV)
+    pos = torch.randint(0, 256, (M,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nb * bs, device=DEV)[:M]
+    if M > 1:
+        slots[1] = -1  # padded decode row: no cache write
+    kc = torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    q = native_lib.decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, pos, kc, vc, slots)
+    qkv = native_lib.skinny_linear_cfg(x, w, b, 23)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(kc)
+    q2, _, _ = native_lib.rope_qkv_cache_fwd(qkv, cos, sin, nq, nkv, 256, pos, kc2, vc2, slots)
+    assert q.shape == (M, nq, D)
+    assert torch.equal(q, q2) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    # and against the fp32 oracle of the whole chain
+    qr, kr, vr = ref.rope_qkv_fwd((x.float() @ w.float().t() + (b.float() if bias else 0.0)), cos, sin, nq, nkv,
+                                  256, pos)
+    assert _row_err(q.view(M, -1), qr.reshape(M, -1)) < 1.5e-2
+
+
+@pytest.mark.parametrize("M,F,K,bias", [(1, 11008, 4096, False), (7, 704, 256, True), (16, 11008, 4096, True)])
+def test_decode_up_swiglu_fused(native_lib, M, F, K, bias):
+    """Gate/up projection with SwiGLU in the finalize pass == v2 GEMM + swiglu_fwd, bit for bit."""
+    x = _bf(M, K, seed=94)
+    w = _bf(2 * F, K, scale=0.05, seed=95)
+    b = _bf(2 * F, seed=96) if bias else None
+    act = native_lib.decode_up_swiglu(x, w, b)
+    act2 = native_lib.swiglu_fwd(native_lib.skinny_linear_cfg(x, w, b, 23))
+    assert act.shape == (M, F) and torch.equal(act, act2)
+    gu = x.float() @ w.float().t() + (b.float() if bias else 0.0)
+    ref_act = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    assert _row_err(act, ref_act) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(1, 4096, 11008, False), (9, 4096, 4096, True), (16, 4096, 11008, False),
+                                        (16, 1024, 384, True)])
+def test_decode_linear_add_rmsnorm_fused(native_lib, M, N, K, bias):
+    """Row projection + residual + RMSNorm in the finalize pass: the residual output equals the
+    unfused v2 GEMM + add_rmsnorm_fwd bit for bit, the normalised output within one bf16 ulp
+    (the sum of squares is reduced in a different order); both vs the fp32 oracle."""
+    x = _bf(M, K, seed=97)
+    w = _bf(N, K, scale=0.05, seed=98)
+    b = _bf(N, seed=99) if bias else None
+    res = _bf(M, N, seed=100)
+    nw = (1.0 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    y, res_out = native_lib.decode_linear_add_rmsnorm(x, w, b, res, nw, 1e-5)
+    y2, res2, _ = native_lib.add_rmsnorm_fwd(native_lib.skinny_linear_cfg(x, w, b, 23), res, nw, 1e-5)
+    assert torch.equal(res_out, res2)
+    ulp = (y2.float().abs() * 2.0 ** -7).clamp_min(1e-30)
+    assert ((y.float() - y2.float()).abs() <= ulp).all()
+    s = (x.float() @ w.float().t() + (b.float() if bias else 0.0)) + res.float()
+    ref_y = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+    assert _row_err(res_out, s) < 1.5e-2 and _row_err(y, ref_y) < 2e-2

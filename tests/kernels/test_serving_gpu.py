@@ -179,3 +179,41 @@ def test_tp2_serving_two_processes_custom_ar_graphs(native_lib):
     assert [x[0] for x in a] == [y[0] for y in b]
     agree = sum(int(x == y) for p, q in zip(a, b) for x, y in zip(p, q))
     assert agree / sum(len(p) for p in b) >= 0.9, (a, b)
+
+
+def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
+    """The fused decode layer (QKV+RoPE+cache write, o-proj+add+RMSNorm, up+SwiGLU, down+add+
+    RMSNorm as GEMM epilogues) gives the unfused layer's logits and greedy tokens, in graphs."""
+    from llmctl.serve.engine import InferenceEngine
+    from llmctl.serve.scheduler import SamplingParams
+
+    prompts = [[1, 2, 3, 4, 5], [9] * 37, [7, 7], [3] * 70]
+    p = SamplingParams(max_tokens=12, temperature=0.0)
+    kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16, max_model_len=512, use_graphs=True)
+    monkeypatch.setenv("LLMCTL_DECODE_FUSED", "1")
+    ef = InferenceEngine("tiny", **kw)
+    assert ef._fused_decode()
+    a = ef.generate(prompts, p)
+    monkeypatch.setenv("LLMCTL_DECODE_FUSED", "0")
+    eu = InferenceEngine("tiny", **kw)
+    assert not eu._fused_decode()
+    b = eu.generate(prompts, p)
+    agree = sum(int(x == y) for sa, sb in zip(a, b) for x, y in zip(sa.output_ids, sb.output_ids))
+    assert agree / sum(len(s.output_ids) for s in a) > 0.9
+    assert [s.output_ids[0] for s in a] == [s.output_ids[0] for s in b]  # prefill path is shared
+    # one decode step from identical cache state: fused vs unfused logits
+    for pr in prompts:
+        ef.add_request(pr, SamplingParams(max_tokens=4, temperature=0.0))
+    while ef.scheduler.waiting or any(s.first_token_time is None for s in ef.scheduler.running):
+        ef.step()
+    out = ef.scheduler.schedule()
+    assert out.decode and not out.prefill
+    with torch.inference_mode():
+        plan = ef.decode_plan(out.decode)
+        d = ef.device
+        args = (torch.tensor(plan["ids"], device=d), torch.tensor(plan["positions"], dtype=torch.int32, device=d),
+                torch.tensor(plan["slots"], device=d), torch.from_numpy(plan["bt"]).to(d),
+                torch.tensor(plan["ctx"], dtype=torch.int32, device=d))
+        lu = ef._decode_body(*args).float()  # (LLMCTL_DECODE_FUSED=0 here)
+        lf = ef._decode_body_fused(*args).float()
+    assert torch.isfinite(lf).all() and (lf - lu).norm() / lu.norm() < 2e-2
