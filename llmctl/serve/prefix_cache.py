@@ -16,7 +16,7 @@ after preemption, which re-attach their computed blocks instead of recomputing t
 from __future__ import annotations
 
 from collections import OrderedDict
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 
 def _block_hash(parent: int, tokens: Sequence[int]) -> int:
@@ -56,11 +56,21 @@ class PrefixCache:
         self.stats["hit_tokens"] += len(blocks) * self.bs
         return blocks
 
-    def insert(self, ids: Sequence[int], table: Sequence[int], num_computed: int) -> None:
+    def insert(self, ids: Sequence[int], table: Sequence[int], num_computed: int,
+               hashes: Optional[List[int]] = None, start: int = 0) -> None:
         """Index every fully computed block of a sequence (``ids`` its tokens, ``table`` its block
-        table, ``num_computed`` the positions whose K/V are in the cache)."""
+        table, ``num_computed`` the positions whose K/V are in the cache).  ``hashes``: the
+        sequence's chain-hash list, extended in place (only new blocks are hashed); ``start``:
+        blocks before it are already indexed (a live sequence's blocks cannot be evicted)."""
         nfull = min(num_computed // self.bs, len(table))
-        for i, h in enumerate(self._hashes(ids, nfull)):
+        if hashes is None:
+            hashes = []
+        h = hashes[-1] if hashes else 0
+        for i in range(len(hashes), nfull):
+            h = _block_hash(h, ids[i * self.bs:(i + 1) * self.bs])
+            hashes.append(h)
+        for i in range(start, nfull):
+            h = hashes[i]
             b = table[i]
             if h in self._blocks:
                 self._blocks.move_to_end(h)

@@ -66,10 +66,18 @@ class Sequence:
     num_computed: int = 0  # leading positions whose K/V are in the paged cache
     cached_tokens: int = 0  # of those, re-attached from the prefix cache (not computed)
     kv_len: int = 0  # positions reserved in the block table (prefill target; +1 per decode)
+    # prefix-cache bookkeeping: chain hashes of this sequence's full token blocks (tokens only
+    # ever append, so they stay valid) and how many of its current blocks are indexed
+    block_hashes: List[int] = field(default_factory=list, repr=False)
+    indexed_blocks: int = 0
 
     @property
     def all_ids(self) -> List[int]:
         return self.prompt_ids + self.output_ids
+
+    @property
+    def last_id(self) -> int:
+        return self.output_ids[-1] if self.output_ids else self.prompt_ids[-1]
 
     @property
     def num_tokens(self) -> int:
@@ -213,8 +221,13 @@ class ContinuousBatchScheduler:
     def computed(self, seq: Sequence, count: int) -> None:
         """The engine ran ``count`` more positions of ``seq``: index its newly full blocks."""
         seq.num_computed += count
-        if self.prefix_cache is not None and seq.status == "running":
-            self.prefix_cache.insert(seq.all_ids, self.kv.block_table(seq.seq_id), seq.num_computed)
+        # index newly completed blocks only (a decode step completes one every block_size steps;
+        # re-hashing the whole prefix every step cost ~0.5 ms per 16 x 2k decode step)
+        if (self.prefix_cache is not None and seq.status == "running"
+                and seq.num_computed // self.block_size > seq.indexed_blocks):
+            self.prefix_cache.insert(seq.all_ids, self.kv.block_table(seq.seq_id), seq.num_computed,
+                                     hashes=seq.block_hashes, start=seq.indexed_blocks)
+            seq.indexed_blocks = seq.num_computed // self.block_size
 
     def kv_block_size(self) -> int:
         return self.block_size
@@ -232,6 +245,7 @@ class ContinuousBatchScheduler:
             self.running.remove(seq)
         seq.status = "waiting"
         seq.num_computed = seq.kv_len = 0
+        seq.indexed_blocks = 0  # its blocks were released: re-index against the next block table
         seq.preemptions += 1
         self.waiting.appendleft(seq)
 
@@ -244,7 +258,7 @@ class ContinuousBatchScheduler:
             except (KeyError, IndexError, RuntimeError):
                 table = []
             if table:
-                self.prefix_cache.insert(seq.all_ids, table, seq.num_computed)
+                self.prefix_cache.insert(seq.all_ids, table, seq.num_computed, hashes=seq.block_hashes)
         self.kv.free_sequence(seq.seq_id)
 
     def finish(self, seq: Sequence, reason: str) -> None:

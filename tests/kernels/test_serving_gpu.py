@@ -217,3 +217,30 @@ def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
         lu = ef._decode_body(*args).float()  # (LLMCTL_DECODE_FUSED=0 here)
         lf = ef._decode_body_fused(*args).float()
     assert torch.isfinite(lf).all() and (lf - lu).norm() / lu.norm() < 2e-2
+
+
+def test_fresh_prefill_flash_attention_matches_paged(native_lib, monkeypatch):
+    """Whole fresh prompts prefill through the packed-document flash-attention kernel; the logits
+    and the written KV cache match the paged-prefill kernel path."""
+    from llmctl.serve.engine import InferenceEngine
+    from llmctl.serve.scheduler import PrefillChunk, SamplingParams, Sequence
+
+    e = InferenceEngine("tiny", device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16,
+                        max_model_len=512, use_graphs=False)
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, 512, (n,), generator=g).tolist() for n in (5, 130, 64, 257)]
+    seqs = [Sequence(prompt_ids=p, params=SamplingParams(max_tokens=1)) for p in prompts]
+    for s in seqs:
+        assert e.kv.add_sequence_shared(s.seq_id, s.num_tokens, [])
+    plan = e.prefill_plan([PrefillChunk(s, 0, s.num_tokens) for s in seqs])
+    assert plan["doc"] is not None
+    monkeypatch.setenv("LLMCTL_PREFILL_FA", "1")
+    la = e.prefill_exec(plan).float()
+    kc_a = [t.clone() for t in e.kv_cache.k]
+    monkeypatch.setenv("LLMCTL_PREFILL_FA", "0")
+    lb = e.prefill_exec(plan).float()
+    assert la.shape == lb.shape == (4, e.cfg.vocab_size)
+    assert (la - lb).norm() / lb.norm() < 1e-2
+    assert torch.equal(kc_a[0], e.kv_cache.k[0])  # layer 0: the same RoPE'd K rows written
+    for a, b in zip(kc_a[1:], e.kv_cache.k[1:]):  # later layers see attention outputs that differ in rounding
+        assert (a.float() - b.float()).norm() / b.float().norm() < 1e-2
