@@ -26,7 +26,9 @@ def run_serving_benchmark(model: str = "gpt-7b", prompt_length: int = 2048, gen_
 
     max_len = prompt_length + gen_length + 16
     eng = InferenceEngine(model, device=device, max_batch_size=max_batch_size,
-                          max_batch_tokens=max_batch_tokens or max(prompt_length, 8192), max_model_len=max_len,
+                          max_batch_tokens=max_batch_tokens or max(prompt_length,
+                                                                   4096 if scheduler == "prefill_first" else 8192),
+                          max_model_len=max_len,
                           use_graphs=use_graphs, seed=seed, scheduler=scheduler)
     V = eng.cfg.vocab_size
     rng = random.Random(seed)

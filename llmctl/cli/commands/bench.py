@@ -47,10 +47,16 @@ def e2e(
     model: str = typer.Option("gpt-7b", help="Checkpoint dir or template"),
     max_batch_size: int = typer.Option(16, help="Max decode batch"),
     device: str = typer.Option("auto", help="auto | cuda | cpu"),
-    scheduler: str = typer.Option("dynamic", help="dynamic | prefill_first | static"),
-    max_batch_tokens: Optional[int] = typer.Option(None, help="Prefill token budget per step"),
+    scheduler: str = typer.Option("prefill_first", help="prefill_first | dynamic | static"),
+    max_batch_tokens: Optional[int] = typer.Option(None, help="Prefill token budget per step (default: 4096 "
+                                                                 "for prefill_first, 8192 otherwise)"),
 ) -> None:
-    """End-to-end serving benchmark (TTFT p50/p99, TPOT, tokens/s)."""
+    """End-to-end serving benchmark (TTFT p50/p99, TPOT, tokens/s).
+
+    Defaults to the ``prefill_first`` policy with a 4096-token prefill budget: on a burst of
+    2048-token prompts it gave the lowest TTFT p50 and TPOT of the measured policies/budgets
+    (``profiles/serve_r2_session6.txt``: p50 213 ms at 4096 vs 222 ms at 8192 tokens;
+    ``dynamic`` 300 ms)."""
     from llmctl.benchmarks.serving import run_serving_benchmark
 
     res = run_serving_benchmark(model=model, prompt_length=prompt_length, gen_length=gen_length, qps=qps,
