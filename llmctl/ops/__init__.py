@@ -12,6 +12,7 @@ from .functional import (
     add_layernorm,
     add_rmsnorm,
     cross_entropy,
+    decode_attention_qkv,
     decode_fused_ok,
     decode_linear,
     decode_linear_add_rmsnorm,
@@ -37,7 +38,7 @@ from .functional import (
 
 __all__ = [
     "ref", "native_available", "adamw_step_", "add_layernorm", "add_rmsnorm", "cross_entropy", "decode_linear",
-    "decode_fused_ok", "decode_linear_add_rmsnorm", "decode_qkv_rope_cache", "decode_up_swiglu",
+    "decode_attention_qkv", "decode_fused_ok", "decode_linear_add_rmsnorm", "decode_qkv_rope_cache", "decode_up_swiglu",
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
     "paged_prefill_attention", "prefill_work_list", "attn_merge_",
     "rmsnorm", "rope_qkv", "rope_flash_attention", "rope_qkv_cache", "sample", "swiglu", "transpose_",

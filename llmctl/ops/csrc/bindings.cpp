@@ -48,6 +48,8 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("skinny_linear_cfg(Tensor x, Tensor w, Tensor? bias, int config) -> Tensor");
   m.def("decode_qkv_rope_cache(Tensor x, Tensor w, Tensor? bias, Tensor cos, Tensor sin, int nq, int nkv, Tensor positions, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> Tensor");
   m.def("decode_up_swiglu(Tensor x, Tensor w, Tensor? bias) -> Tensor");
+  m.def("decode_linear_partials(Tensor x, Tensor w) -> Tensor");
+  m.def("paged_attention_decode_qkv(Tensor qkv_ws, Tensor? bias, Tensor cos, Tensor sin, Tensor positions, Tensor slots, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int nq, int nkv, float scale) -> Tensor");
   m.def("decode_linear_add_rmsnorm(Tensor x, Tensor w, Tensor? bias, Tensor residual, Tensor norm_w, float eps) -> (Tensor, Tensor)");
   m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor uniform) -> Tensor");
   // benchmarks / tuning (gemm_bf16.hip, hbm_stream.hip)

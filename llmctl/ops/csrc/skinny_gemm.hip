@@ -602,6 +602,16 @@ int decode_partials(const at::Tensor& x, const at::Tensor& w, at::Tensor& ws) {
 }
 }  // namespace
 
+// x W^T as fp32 K-chunk partials [KS, M, N] (the fused decode attention sums them itself)
+at::Tensor decode_linear_partials(const at::Tensor& x, const at::Tensor& w) {
+  check_decode_operands(x, w, c10::nullopt, "decode_linear_partials");
+  const int M = x.size(0), N = w.size(0);
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor ws;
+  const int KS = decode_partials(x, w, ws);
+  return ws.view({KS, M, N});
+}
+
 // q [M, nq, D] = RoPE(x Wqkv^T + b)[:, :nq]; K/V rows RoPE'd / copied into the paged cache at slots
 at::Tensor decode_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                  const at::Tensor& cosT, const at::Tensor& sinT, int64_t nq, int64_t nkv,
@@ -679,6 +689,7 @@ TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("skinny_linear_cfg", &skinny_linear_cfg);
   m.impl("decode_qkv_rope_cache", &decode_qkv_rope_cache);
   m.impl("decode_up_swiglu", &decode_up_swiglu);
+  m.impl("decode_linear_partials", &decode_linear_partials);
   m.impl("decode_linear_add_rmsnorm", &decode_linear_add_rmsnorm);
 }
 

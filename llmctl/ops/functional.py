@@ -457,6 +457,27 @@ def decode_qkv_rope_cache(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cac
     return rope_qkv_cache(decode_linear(x, w, b), cos, sin, nq, nkv, 0, positions, k_cache, v_cache, slots)[0]
 
 
+def decode_attention_qkv(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cache, v_cache, slots, block_tables,
+                         ctx_lens, scale: Optional[float] = None):
+    """Decode QKV projection -> RoPE -> paged-cache write -> paged attention, with the
+    projection's fp32 K-chunk partials summed inside the attention kernel (its prologue ropes q;
+    the workgroup whose context split holds the new token writes that token's K/V rows first):
+    no separate finalize pass.  Same result as ``decode_qkv_rope_cache`` followed by
+    ``paged_attention_decode`` (bit for bit).  Opt-in (``LLMCTL_DECODE_ATTN_QKV=1``): measured
+    0.1-0.2 ms SLOWER per 16 x 2k GPT-7B decode step than the two-step path
+    (``profiles/serve_r2_session6.txt``) — every one of the 2048 attention workgroups re-sums its
+    q head's partials on the critical path of its K/V stream, which costs more than the finalize
+    launch it removes."""
+    D = w.shape[0] // (nq + 2 * nkv)
+    scale = scale if scale is not None else D ** -0.5
+    if decode_fused_ok(x, w) and os.environ.get("LLMCTL_DECODE_ATTN_QKV", "0") == "1":
+        ws = native().decode_linear_partials(x, w)
+        return native().paged_attention_decode_qkv(ws, b, cos, sin, positions.to(torch.int32).contiguous(), slots,
+                                                   k_cache, v_cache, block_tables, ctx_lens, nq, nkv, scale)
+    q = decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, positions, k_cache, v_cache, slots)
+    return paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+
+
 def decode_up_swiglu(x, w, b=None):
     """Decode gate/up projection with SwiGLU in its finalize pass: ``silu(g) * u`` of
     ``x @ w^T (+ b)`` (gate = first half of the out features)."""
@@ -485,6 +506,6 @@ __all__ = [
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "rope_flash_attention",
     "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample", "decode_linear", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu",
+    "sample", "decode_linear", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu", "decode_attention_qkv",
     "decode_linear_add_rmsnorm", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
 ]

@@ -285,9 +285,8 @@ class InferenceEngine:
         x = self._embed(ids, positions)
         xn, res = ops.rmsnorm(x, layers[0].attn_norm_w, eps), x
         for li, layer in enumerate(layers):
-            q = ops.decode_qkv_rope_cache(xn, layer.wqkv, layer.bqkv, self.rope[0], self.rope[1], layer.nq,
-                                          layer.nkv, positions, kc[li], vc[li], slots)
-            o = ops.paged_attention_decode(q, kc[li], vc[li], block_tables, ctx_lens)
+            o = ops.decode_attention_qkv(xn, layer.wqkv, layer.bqkv, self.rope[0], self.rope[1], layer.nq,
+                                         layer.nkv, positions, kc[li], vc[li], slots, block_tables, ctx_lens)
             xn, res = ops.decode_linear_add_rmsnorm(o.view(o.shape[0], -1), layer.wo, layer.bo, res,
                                                     layer.mlp_norm_w, eps)
             act = ops.decode_up_swiglu(xn, layer.w_up, layer.b_up)

@@ -191,6 +191,7 @@ def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
     p = SamplingParams(max_tokens=12, temperature=0.0)
     kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16, max_model_len=512, use_graphs=True)
     monkeypatch.setenv("LLMCTL_DECODE_FUSED", "1")
+    monkeypatch.setenv("LLMCTL_DECODE_ATTN_QKV", "1")  # also the opt-in attention-side QKV finalize
     ef = InferenceEngine("tiny", **kw)
     assert ef._fused_decode()
     a = ef.generate(prompts, p)
