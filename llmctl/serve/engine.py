@@ -222,15 +222,18 @@ class InferenceEngine:
         # from the RoPE pass, ~1.4x the paged-prefill kernel's rate on 4 x 2k prompts);
         # LLMCTL_PREFILL_FA=0 keeps the paged kernel (A/B)
         doc = None
-        if plan.get("doc") is not None and d.type == "cuda" and os.environ.get("LLMCTL_PREFILL_FA", "1") != "0":
+        fa = plan.get("doc") is not None and d.type == "cuda" and os.environ.get("LLMCTL_PREFILL_FA", "1") != "0"
+        if fa and len(plan["cu"]) > 2:  # several prompts packed: document boundaries
             doc = torch.from_numpy(plan["doc"]).to(d, non_blocking=True).view(1, T)
+        # (one prompt: plain causal attention, which also lets the kernel split the K/V range of
+        # its few q-blocks over two workgroups — the split is off for packed documents)
         x = self._embed(ids, pos.long())
         res = None
         kc, vc = self.kv_cache.k, self.kv_cache.v
         for li, layer in enumerate(self.model.layers):
             xn, res = self._norm(layer, x, res, "attn")
             q, k, v = self._qkv(layer, xn, pos, self.max_model_len, kc[li], vc[li], slots)
-            if doc is not None:
+            if fa:
                 o = ops.flash_attention(q.view(1, T, layer.nq, layer.D), k.view(1, T, layer.nkv, layer.D),
                                         v.view(1, T, layer.nkv, layer.D), causal=True, doc_start=doc)
             else:
