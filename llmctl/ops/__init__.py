@@ -34,6 +34,7 @@ from .functional import (
     sample,
     swiglu,
     transpose_,
+    up_swiglu,
 )
 
 __all__ = [
@@ -41,5 +42,5 @@ __all__ = [
     "decode_attention_qkv", "decode_fused_ok", "decode_linear_add_rmsnorm", "decode_qkv_rope_cache", "decode_up_swiglu",
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
     "paged_prefill_attention", "prefill_work_list", "attn_merge_",
-    "rmsnorm", "rope_qkv", "rope_flash_attention", "rope_qkv_cache", "sample", "swiglu", "transpose_",
+    "rmsnorm", "rope_qkv", "rope_flash_attention", "rope_qkv_cache", "sample", "swiglu", "transpose_", "up_swiglu",
 ]

@@ -66,6 +66,7 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("gemm_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int variant=-1) -> ()");
   m.def("hbm_copy(Tensor src, Tensor(a!) dst) -> ()");
   m.def("gemm64_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int config=4) -> ()");
+  m.def("gemm64_swiglu_fwd(Tensor x, Tensor w, int config) -> Tensor");
   m.def("gemm64_swiglu_dgrad(Tensor dy, Tensor w, Tensor gu, int config=104) -> Tensor");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
 }

@@ -66,7 +66,12 @@ enum : int { A_LO = 0, A_HI = 1, B_H0 = 2, B_H1 = 3 };
 // EPI_SWIGLU_BWD (down-projection data gradient): C = dAct is not stored; with gate / up read from
 // aux = gu [M, 2N] (ld = ldc), the epilogue writes dgate to C[:, n] and dup to C[:, N + n] (C = dgu),
 // i.e. the SwiGLU backward rides on the GEMM's store pass (no dAct round trip through HBM)
-enum : int { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU_BWD = 2 };
+// EPI_SWIGLU_FWD (gate/up projection, forward layout, serving prefill): output tile tn covers gate
+// rows [128 tn, 128 tn + 128) of B = W_up [2F, K] in its left half and the matching up rows
+// F + [128 tn, ...) in its right half (the second B half-tile reads through its own buffer
+// resource); the up accumulators cross to the gate waves through LDS and only act = silu(g) * u
+// [M, F] is stored (C, ldc = F) — no gu tensor, no separate SwiGLU pass
+enum : int { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU_BWD = 2, EPI_SWIGLU_FWD = 3 };
 template <int V>
 using K_ = std::integral_constant<int, V>;
 
@@ -206,8 +211,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 
   const long lda = args.lda, ldb = args.ldb;
   const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
-  const unsigned short* Bb = BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
+  const unsigned short* Bb = EPI == EPI_SWIGLU_FWD ? args.b + (long)tn * (TN / 2) * ldb
+                             : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
   const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
+  // EPI_SWIGLU_FWD: B_H1 image rows 128 + ip -> up row N + 128 tn + ip (N = F)
+  const i32x4_t rb_hi = EPI == EPI_SWIGLU_FWD ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb)
+                                              : rb;
   // byte step of one K-tile in each operand
   const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
   const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
@@ -235,8 +244,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
       bdma16(ra, vo[kind][1], so, l + 8192);
     } else {
       const unsigned so = __builtin_amdgcn_readfirstlane(tc * b_kstep);
-      bdma16(rb, vo[kind][0], so, l);
-      bdma16(rb, vo[kind][1], so, l + 8192);
+      const i32x4_t r = kind == B_H1 ? rb_hi : rb;
+      bdma16(r, vo[kind][0], so, l);
+      bdma16(r, vo[kind][1], so, l + 8192);
     }
   };
 
@@ -345,6 +355,38 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 
   // ---- epilogue: lane holds C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3
   const int g = lane >> 4, i16 = lane & 15;
+  if constexpr (EPI == EPI_SWIGLU_FWD) {
+    // up waves (wc 2, 3) hand their tiles to the gate waves (wc 0, 1) with the same (wr, i, j, lane)
+    // through the now idle 128-KB LDS image: [wr][wc & 1][i][j][lane] f32x4
+    __syncthreads();
+    f32x4_t* xch = reinterpret_cast<f32x4_t*>(smem) + (wr * 2 + (wc & 1)) * (8 * 4 * 64) + lane;
+    if (wc >= 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xch[(i * 4 + j) * 64] = acc[i][j];
+    }
+    __syncthreads();
+    if (wc >= 2) return;
+    unsigned short* Ab2 = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * (TN / 2) + wc * 64 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_t gv = acc[i][j], uv = xch[(i * 4 + j) * 64];
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // as swiglu_fwd_kernel on the bf16-stored g / u
+          const float gg = bf2f(f2bf(gv[e])), uu = bf2f(f2bf(uv[e]));
+          o[e] = gg * (1.f / (1.f + __expf(-gg))) * uu;
+        }
+        s2_t pk;
+        pk[0] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+        pk[1] = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+        *reinterpret_cast<s2_t*>(Ab2 + (long)(16 * i) * args.ldc + 16 * j) = pk;
+      }
+    return;
+  }
   if (sp >= 0) {  // split item: fp32 partial tile, row-major 256 x 256
     float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 64 + 4 * g;
 #pragma unroll
@@ -604,7 +646,33 @@ at::Tensor gemm64_swiglu_dgrad(const at::Tensor& dy, const at::Tensor& w, const 
   return dgu;
 }
 
+// Gate/up projection fused with SwiGLU (serving prefill): act [M, F] = silu(x Wg^T) * (x Wu^T) with
+// W_up = [Wg; Wu] [2F, K] (forward layout, both operands K-contiguous); M % 256, F % 128, K % 128.
+at::Tensor gemm64_swiglu_fwd(const at::Tensor& x, const at::Tensor& w, int64_t config) {
+  LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                   x.is_cuda() && w.is_cuda() && x.stride(1) == 1 && w.is_contiguous(),
+               "gemm64_swiglu_fwd: bf16 GPU x [M, K] (unit inner stride), contiguous W_up [2F, K]");
+  const long M = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  LLMCTL_CHECK(w.size(1) == K && w.size(0) == 2 * F, "gemm64_swiglu_fwd: W_up must be [2F, K]");
+  LLMCTL_CHECK(M % TM == 0 && F % (TN / 2) == 0 && K % (2 * TK) == 0 && K > 0,
+               "gemm64_swiglu_fwd: M % 256, F % 128, K % 128 (got ", M, "x", F, "x", K, ")");
+  LLMCTL_CHECK(x.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
+               "gemm64_swiglu_fwd: 16-byte aligned operand rows");
+  LLMCTL_CHECK((long)TM * x.stride(0) * 2 < (1L << 31) && (long)TN * K * 2 < (1L << 31),
+               "gemm64_swiglu_fwd: operand too large for 32-bit offsets");
+  const c10::DeviceGuard dg(x.device());
+  auto act = at::empty({M, F}, x.options());
+  G64Args g{reinterpret_cast<const unsigned short*>(x.data_ptr()), reinterpret_cast<const unsigned short*>(w.data_ptr()),
+            reinterpret_cast<unsigned short*>(act.data_ptr()), x.stride(0), K, F,
+            (int)M, (int)F, (int)K, (int)(M / TM), (int)(F / (TN / 2)), 0, 1, 0, nullptr, nullptr};
+  plan_split(g, 1);  // whole tiles only (the pairing epilogue has no split-K reduction)
+  launch<false, false, EPI_SWIGLU_FWD>(g, (int)(config % 1000));
+  return act;
+}
+
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("gemm64_swiglu_fwd", &gemm64_swiglu_fwd);
   m.impl("gemm64_ex", &gemm64_ex);
   m.impl("gemm64_swiglu_dgrad", &gemm64_swiglu_dgrad);
 }

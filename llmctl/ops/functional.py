@@ -478,6 +478,27 @@ def decode_attention_qkv(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cach
     return paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
 
 
+def up_swiglu(x, w, b=None):
+    """``silu(gate) * up`` of the gate/up projection ``x @ w^T (+ b)`` (w = [W_gate; W_up]).
+    Serving prefill: tokens a multiple of 256 run the gemm64 kernel with the SwiGLU in its
+    epilogue (``gemm64_swiglu_fwd``: gate and matching up rows in one output tile, only the
+    [T, F] activation stored — no gu tensor, no SwiGLU pass).  ``LLMCTL_PREFILL_SWIGLU=0``
+    disables (A/B)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    T, F = x2.shape[0], w.shape[0] // 2
+    if (b is None and os.environ.get("LLMCTL_PREFILL_SWIGLU", "1") != "0" and use_native(x) and T % 256 == 0
+            and F % 128 == 0 and x2.shape[1] % 128 == 0 and x2.dtype == w.dtype == torch.bfloat16
+            and x2.stride(1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and w.is_contiguous()
+            and w.data_ptr() % 16 == 0):
+        from llmctl.exec.linear import gemm64_config
+
+        act = native().gemm64_swiglu_fwd(x2, w, gemm64_config("fwd", T, 2 * F, x2.shape[1]) % 1000)
+        return act.view(*x.shape[:-1], F)
+    from llmctl.exec.linear import forward_linear
+
+    return swiglu(forward_linear(x, w, b))
+
+
 def decode_up_swiglu(x, w, b=None):
     """Decode gate/up projection with SwiGLU in its finalize pass: ``silu(g) * u`` of
     ``x @ w^T (+ b)`` (gate = first half of the out features)."""
@@ -506,6 +527,6 @@ __all__ = [
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "rope_flash_attention",
     "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample", "decode_linear", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu", "decode_attention_qkv",
+    "sample", "decode_linear", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu", "decode_attention_qkv", "up_swiglu",
     "decode_linear_add_rmsnorm", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
 ]

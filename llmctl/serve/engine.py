@@ -160,7 +160,10 @@ class InferenceEngine:
         if layer.moe is not None:  # routed experts (host-side split sizes: eager, no graphs)
             return layer.moe(xn)
         if self.cfg.gated_mlp:
-            out = ops.decode_linear(ops.swiglu(ops.decode_linear(xn, layer.w_up, layer.b_up)), layer.w_down)
+            # prefill-sized (T % 256 == 0): the SwiGLU rides on the gate/up GEMM's epilogue
+            act = (ops.up_swiglu(xn, layer.w_up, layer.b_up) if xn.shape[0] >= 256 and xn.shape[0] % 256 == 0
+                   else ops.swiglu(ops.decode_linear(xn, layer.w_up, layer.b_up)))
+            out = ops.decode_linear(act, layer.w_down)
         else:
             out = ops.decode_linear(ops.gelu(ops.decode_linear(xn, layer.w_up, layer.b_up)), layer.w_down)
         out = self._reduce(out)  # row-parallel down projection

@@ -658,3 +658,19 @@ def test_paged_attention_decode_qkv_fused(native_lib, M, nq, nkv, D, K):
     assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
     live = [i for i in range(M) if int(slots[i]) >= 0]
     assert torch.equal(o[live], o2[live])
+
+
+@pytest.mark.parametrize("M,F,K", [(256, 128, 256), (2048, 11008, 4096), (512, 384, 1152)])
+def test_gemm64_swiglu_fwd(native_lib, M, F, K):
+    """Gate/up projection with the SwiGLU in the gemm64 epilogue (gate rows and the matching up
+    rows in one output tile, up accumulators exchanged through LDS) == gemm64 forward (whole
+    tiles) + swiglu_fwd bit for bit, and vs the fp32 oracle."""
+    x = _bf(M, K, seed=211)
+    w = _bf(2 * F, K, scale=0.05, seed=212)
+    act = native_lib.gemm64_swiglu_fwd(x, w, 104)
+    gu = torch.empty(M, 2 * F, dtype=torch.bfloat16, device=DEV)
+    native_lib.gemm64_ex(x, w, gu, False, False, False, 1104)
+    assert act.shape == (M, F) and torch.equal(act, native_lib.swiglu_fwd(gu))
+    g = x.float() @ w.float().t()
+    ref_act = torch.nn.functional.silu(g[:, :F]) * g[:, F:]
+    assert _row_err(act, ref_act) < 2e-2
