@@ -43,7 +43,29 @@ __global__ __launch_bounds__(256) void sample_kernel(const T* __restrict__ logit
   if (t <= 0.f) {  // greedy: argmax, lowest index on ties
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = tid; i < V; i += 256) {
+    int i0 = 0;
+    if constexpr (sizeof(T) == 2) {
+      // 16-B vectors (8 logits per lane, 4 loads in flight per unrolled step): a 32k-vocab row
+      // is 16 vector steps per thread instead of 125 dependent scalar loads (37 -> a few us)
+      if ((V & 7) == 0 && (reinterpret_cast<uintptr_t>(lr) & 15) == 0) {
+        const bf16x8* lv = reinterpret_cast<const bf16x8*>(lr);
+        const int V8 = V >> 3;
+#pragma unroll 4
+        for (int c = tid; c < V8; c += 256) {
+          const bf16x8 v = lv[c];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = bf2f(v[e]);
+            if (x > best) {  // in index order within the thread: strict > keeps the lowest index
+              best = x;
+              bi = c * 8 + e;
+            }
+          }
+        }
+        i0 = V;
+      }
+    }
+    for (int i = i0 + tid; i < V; i += 256) {
       const float x = ld(lr, i);
       if (x > best) {
         best = x;

@@ -674,3 +674,21 @@ def test_gemm64_swiglu_fwd(native_lib, M, F, K):
     g = x.float() @ w.float().t()
     ref_act = torch.nn.functional.silu(g[:, :F]) * g[:, F:]
     assert _row_err(act, ref_act) < 2e-2
+
+
+@pytest.mark.parametrize("V", [32000, 50257, 1003])
+def test_sampling_greedy_ties_and_odd_vocab(native_lib, V):
+    """Greedy rows (vectorised argmax for 8-aligned vocabularies, scalar otherwise): the lowest
+    index wins ties, including ties across lanes and across the two paths."""
+    N = 6
+    logits = (torch.randn(N, V, device=DEV) * 2).to(torch.bfloat16)
+    logits[0, 17] = logits[0, V - 5] = 30.0  # tie far apart
+    logits[1, 8] = logits[1, 9] = 30.0  # tie inside one 8-element vector
+    logits[2, min(255 * 8 + 3, V - 1)] = logits[2, 7] = 30.0  # tie across threads
+    temp = torch.zeros(N, device=DEV)
+    topk = torch.zeros(N, dtype=torch.int32, device=DEV)
+    topp = torch.ones(N, device=DEV)
+    u = torch.rand(N, device=DEV)
+    got = native_lib.sample(logits, temp, topk, topp, u)
+    exp = torch.tensor([int(torch.nonzero(r == r.max())[0]) for r in logits.float()], device=DEV)
+    assert torch.equal(got, exp)
