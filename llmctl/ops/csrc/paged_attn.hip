@@ -254,7 +254,7 @@ __global__ __launch_bounds__(D) void paged_combine_kernel(const float* __restric
   out[row * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
 }
 
-// Context splits per (sequence, kv-head): enough workgroups for ~8 per CU, at least 128
+// Context splits per (sequence, kv-head): enough workgroups for ~4-8 per CU, at least 128
 // context slots per split, at most 16.  The batch is rounded up to a power of two, as the
 // serving engine's decode-graph buckets are, so graph replay and eager decode pick the same
 // split.  LLMCTL_DECODE_SPLITS overrides (tests, A/B).
@@ -266,7 +266,11 @@ int decode_splits(int N, int Hkv, int max_ctx) {
   int np = 1;
   while (np < N) np *= 2;
   const int wgs = std::max(1, np * Hkv);
-  return std::max(1, std::min({(2048 + wgs - 1) / wgs, max_ctx / 128, 16}));
+  // once the (sequence, kv-head) grid alone is >= 512 workgroups, ~4 per CU is enough: GPT-7B,
+  // 16 x 2k decode step 7.04 ms at 2 splits vs 7.11 at 4 (the auto value before), 7.5 at 3,
+  // 8.6 at 1 (profiles/serve_r2_session6.txt); smaller grids keep ~8 per CU
+  const int target = wgs >= 512 ? 1024 : 2048;
+  return std::max(1, std::min({(target + wgs - 1) / wgs, max_ctx / 128, 16}));
 }
 
 }  // namespace
