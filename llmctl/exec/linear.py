@@ -18,11 +18,11 @@ used after an optimizer step (``GradSink.epoch``; under ZeRO-1/2 that is after t
 all-gather has landed), and the backward computes ``dX = F.linear(dY, W^T)``.  Cost: one
 bf16 copy of the projection weights and ~2 x 13.5 GB of HBM transpose traffic per step.
 
-Round 2: where the shapes fit (tokens a multiple of 256, in/out features of 256/128), the data
-gradient runs on the in-house 64-deep MFMA kernel (``gemm64_ex``, llmctl/ops/csrc/gemm64.hip),
-which reads ``W`` K-major through ``ds_read_b64_tr_b16`` — faster than hipBLASLt's NN and TN
-kernels on the GPT-7B shapes, and no ``W^T`` copy is kept (the copy remains the fallback for
-other shapes).  Weight gradients go to the same kernel family.
+Round 2: weight gradients run on the in-house 64-deep MFMA kernel (``gemm64_ex``,
+llmctl/ops/csrc/gemm64.hip; 20-40 % over hipBLASLt on the GPT-7B shapes).  Data gradients: the
+down projection's runs on gemm64 with the SwiGLU backward in its epilogue; the others run on
+hipBLASLt's forward layout through the ``W^T`` copies, which measured 0.7 % faster per step
+than gemm64 for all of them (``LLMCTL_DGRAD64``, see ``dgrad64_shape_ok``).
 """
 
 from __future__ import annotations
@@ -103,18 +103,25 @@ def forward_linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] =
     return F.linear(x, w, b)
 
 
-def dgrad64_shape_ok(tokens: int, w: torch.Tensor) -> bool:
+def dgrad64_shape_ok(tokens: int, w: torch.Tensor, fused: bool = False) -> bool:
     """Will ``dx = dy W`` for ``tokens`` rows run on gemm64?  (Decided at forward time: the
-    weight's W^T copy is only kept for layers whose data gradient cannot.)"""
+    weight's W^T copy is only kept for layers whose data gradient cannot.)  ``fused``: the
+    down-projection data gradient with the SwiGLU backward in its epilogue.
+    ``LLMCTL_DGRAD64``: fused (default) = only the SwiGLU-fused down-projection data gradient on
+    gemm64, the rest on hipBLASLt's forward layout through the W^T copies; 1 = every data
+    gradient on gemm64 (no W^T copies, ~10 GB less memory for GPT-7B); 0 = none.  Same-box GPT-7B
+    step A/B (profiles/bench_r2_dgrad_modes.txt): fused 832.0 / 833.9 ms, 0 833.9 / 832.7 ms,
+    1 837.7 / 839.7 ms."""
     out, inn = w.shape
-    if os.environ.get("LLMCTL_DGRAD64", "1") == "0":  # =0: W^T copy + hipBLASLt forward layout (A/B)
+    mode = os.environ.get("LLMCTL_DGRAD64", "fused")
+    if mode == "0" or (mode == "fused" and not fused):
         return False
     return _gemm64_ok(tokens, inn, out, w) and out * w.stride(0) * 2 < 2**31
 
 
-def dgrad64_ok(dy2: torch.Tensor, w: torch.Tensor) -> bool:
+def dgrad64_ok(dy2: torch.Tensor, w: torch.Tensor, fused: bool = False) -> bool:
     """``dx = dy W`` on gemm64 (W read K-major through ds_read_b64_tr_b16: no W^T copy)."""
-    return (dy2.dim() == 2 and dy2.shape[1] == w.shape[0] and dgrad64_shape_ok(dy2.shape[0], w)
+    return (dy2.dim() == 2 and dy2.shape[1] == w.shape[0] and dgrad64_shape_ok(dy2.shape[0], w, fused)
             and dy2.is_cuda and dy2.dtype == torch.bfloat16 and _rows_ok(dy2))
 
 
@@ -269,7 +276,7 @@ def swiglu_data_grad(dy: torch.Tensor, w: torch.nn.Parameter, gu: torch.Tensor) 
     tile, no dAct tensor); otherwise the data gradient and the elementwise kernel separately."""
     dy2 = dy.reshape(-1, dy.shape[-1])
     gu2 = gu.reshape(-1, gu.shape[-1])
-    if (dgrad64_ok(dy2, w) and gu2.is_contiguous() and gu2.data_ptr() % 16 == 0
+    if (dgrad64_ok(dy2, w, fused=True) and gu2.is_contiguous() and gu2.data_ptr() % 16 == 0
             and os.environ.get("LLMCTL_FUSED_SWIGLU", "1") != "0"):  # =0: unfused (A/B)
         from llmctl.ops._lib import native
 
