@@ -87,10 +87,14 @@ def test_gemm64_rejects_bad_shapes(native_lib):
         native_lib.gemm64_ex(a, b, out, False, False, False, 104)
 
 
-def test_linear_backward_on_gemm64(native_lib):
-    """exec.linear routes dgrad (no W^T copy) and wgrad (into the sink's flat view) through
-    gemm64 at eligible shapes; both match the fp32 reference."""
+@pytest.mark.parametrize("mode", ["1", "fused"])
+def test_linear_backward_on_gemm64(native_lib, monkeypatch, mode):
+    """exec.linear routes wgrad (into the sink's flat view) through gemm64 at eligible shapes and
+    dgrad through gemm64 (LLMCTL_DGRAD64=1: no W^T copy) or, by default (=fused: only the
+    SwiGLU-fused down projection stays on gemm64), hipBLASLt through the W^T copy; all match fp32."""
     from llmctl.exec.linear import GradSink, dgrad64_ok, linear
+
+    monkeypatch.setenv("LLMCTL_DGRAD64", mode)
 
     T, inn, out = 512, 768, 1024
     x = _bf(T, inn, seed=5).requires_grad_(True)
@@ -99,9 +103,13 @@ def test_linear_backward_on_gemm64(native_lib):
     sink = GradSink()
     sink.attach(w)
     y = linear(x, w)
-    assert getattr(w, "_llmctl_wt", None) is None  # gemm64 dgrad: no transposed copy kept
     dy = _bf(T, out, seed=7)
-    assert dgrad64_ok(dy, w)
+    if mode == "1":
+        assert getattr(w, "_llmctl_wt", None) is None  # gemm64 dgrad: no transposed copy kept
+        assert dgrad64_ok(dy, w)
+    else:
+        assert getattr(w, "_llmctl_wt", None) is not None and not dgrad64_ok(dy, w)
+        assert dgrad64_ok(dy, w, fused=True)
     y.backward(dy)
     assert row_err(x.grad, dy.float() @ w.detach().float()) < TOL
     assert row_err(w.grad, dy.float().t() @ x.detach().float()) < TOL
