@@ -195,9 +195,43 @@ class GradSink:
             w._llmctl_wt = wt
             w._llmctl_wt_epoch = -1
         if w._llmctl_wt_epoch != self.epoch:
-            native().transpose_(w.detach(), wt)
+            if self._side_stream_ok():
+                # the copy is only read by the backward's data-gradient GEMM: transpose on a side
+                # stream under the forward's compute-bound GEMMs; wait_weight_t() orders the
+                # backward after it (and, through the backward, the next optimizer step)
+                cur = torch.cuda.current_stream(w.device)
+                side = self._side_stream(w.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    native().transpose_(w.detach(), wt)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                w._llmctl_wt_event = ev
+            else:
+                native().transpose_(w.detach(), wt)
+                w._llmctl_wt_event = None
             w._llmctl_wt_epoch = self.epoch
         return wt
+
+    @staticmethod
+    def wait_weight_t(w: torch.nn.Parameter) -> None:
+        """Order the current stream after the side-stream refresh of ``w``'s W^T copy."""
+        ev = getattr(w, "_llmctl_wt_event", None)
+        if ev is not None:
+            torch.cuda.current_stream(w.device).wait_event(ev)
+
+    _streams: dict = {}
+
+    @staticmethod
+    def _side_stream_ok() -> bool:
+        return os.environ.get("LLMCTL_WT_SIDE_STREAM", "1") != "0" and not torch.cuda.is_current_stream_capturing()
+
+    @classmethod
+    def _side_stream(cls, device) -> "torch.cuda.Stream":
+        s = cls._streams.get(device)
+        if s is None:
+            s = cls._streams[device] = torch.cuda.Stream(device=device)
+        return s
 
     def attach(self, p: torch.nn.Parameter) -> None:
         p._llmctl_grad_sink = self
@@ -246,8 +280,11 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if dgrad64_ok(dy2, w):
                 dx = dgrad64(dy2, w).view(*dy.shape[:-1], w.shape[1])
+            elif ctx.wt is not None:
+                GradSink.wait_weight_t(ctx.wparam)
+                dx = F.linear(dy, ctx.wt)
             else:
-                dx = F.linear(dy, ctx.wt) if ctx.wt is not None else dy.matmul(w)
+                dx = dy.matmul(w)
         db = dy2.sum(0) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db
 
@@ -267,7 +304,10 @@ def data_grad(dy: torch.Tensor, w: torch.nn.Parameter) -> torch.Tensor:
         return dgrad64(dy2, w).view(*dy.shape[:-1], w.shape[1])
     sink = getattr(w, "_llmctl_grad_sink", None)
     wt = sink.weight_t(w) if sink is not None else None
-    return F.linear(dy, wt) if wt is not None else dy.matmul(w)
+    if wt is not None:
+        GradSink.wait_weight_t(w)
+        return F.linear(dy, wt)
+    return dy.matmul(w)
 
 
 def swiglu_data_grad(dy: torch.Tensor, w: torch.nn.Parameter, gu: torch.Tensor) -> torch.Tensor:
