@@ -221,9 +221,9 @@ class InferenceEngine:
         cu = torch.tensor(plan["cu"], dtype=torch.int32).to(d, non_blocking=True)
         ctx = torch.tensor(plan["ctx"], dtype=torch.int32).to(d, non_blocking=True)
         work = torch.tensor(plan["work"], dtype=torch.int32).to(d, non_blocking=True)
-        # fresh prompts: the training flash-attention kernel over packed documents (K/V straight
-        # from the RoPE pass, ~1.4x the paged-prefill kernel's rate on 4 x 2k prompts);
-        # LLMCTL_PREFILL_FA=0 keeps the paged kernel (A/B)
+        # fresh prompts: the training flash-attention kernel over packed documents, K/V straight
+        # from the RoPE pass (16 x 2k burst TTFT p50 224.6 -> 218.6 ms, single 2k prompt 27.5 ->
+        # 26.2 ms, profiles/serve_r2_session6.txt); LLMCTL_PREFILL_FA=0 keeps the paged kernel
         doc = None
         fa = plan.get("doc") is not None and d.type == "cuda" and os.environ.get("LLMCTL_PREFILL_FA", "1") != "0"
         if fa and len(plan["cu"]) > 2:  # several prompts packed: document boundaries
@@ -256,8 +256,8 @@ class InferenceEngine:
     # ------------------------------------------------------------------ decode
     def _fused_decode(self) -> bool:
         """Decode layers on the fused-epilogue projections (``ops.decode_qkv_rope_cache`` /
-        ``decode_up_swiglu`` / ``decode_linear_add_rmsnorm``): 7 kernels per layer instead of 10
-        (no separate RoPE/cache-write, SwiGLU or add+RMSNorm passes).  Needs the GPU path, TP=1
+        ``decode_up_swiglu`` / ``decode_linear_add_rmsnorm``): 10 kernels per layer instead of 13
+        (the RoPE/cache-write, SwiGLU and add+RMSNorm passes ride on the projections' finalize).  Needs the GPU path, TP=1
         (the row-parallel all-reduce sits between a projection and the next norm), RMSNorm,
         RoPE and a gated MLP; ``LLMCTL_DECODE_FUSED=0`` keeps the unfused layer (A/B)."""
         cfg, m = self.cfg, self.model
