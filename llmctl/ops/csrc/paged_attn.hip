@@ -266,10 +266,10 @@ int decode_splits(int N, int Hkv, int max_ctx) {
   int np = 1;
   while (np < N) np *= 2;
   const int wgs = std::max(1, np * Hkv);
-  // once the (sequence, kv-head) grid alone is >= 512 workgroups, ~4 per CU is enough: GPT-7B,
-  // 16 x 2k decode step 7.04 ms at 2 splits vs 7.11 at 4 (the auto value before), 7.5 at 3,
-  // 8.6 at 1 (profiles/serve_r2_session6.txt); smaller grids keep ~8 per CU
-  const int target = wgs >= 512 ? 1024 : 2048;
+  // a (sequence, kv-head) grid of 512-1023 workgroups needs only ~4 per CU: GPT-7B, 16 x 2k decode
+  // step 7.04 ms at 2 splits vs 7.11 at 4 (the auto value before), 7.5 at 3, 8.6 at 1
+  // (profiles/serve_r2_session6.txt); other grids (unmeasured against this) keep ~8 per CU
+  const int target = (wgs >= 512 && wgs < 1024) ? 1024 : 2048;
   return std::max(1, std::min({(target + wgs - 1) / wgs, max_ctx / 128, 16}));
 }
 
