@@ -68,7 +68,7 @@ class Sequence:
     kv_len: int = 0  # positions reserved in the block table (prefill target; +1 per decode)
     # prefix-cache bookkeeping: chain hashes of this sequence's full token blocks (tokens only
     # ever append, so they stay valid) and how many of its current blocks are indexed
-    block_hashes: List[int] = field(default_factory=list, repr=False)
+    block_hashes: List[bytes] = field(default_factory=list, repr=False)
     indexed_blocks: int = 0
 
     @property
@@ -139,22 +139,32 @@ class ContinuousBatchScheduler:
     def _can_admit(self) -> bool:
         if not self.waiting or len(self.running) >= self.max_batch_size:
             return False
-        return self.kv.can_allocate(self.waiting[0].num_tokens + self.kv_block_size())
+        n = self.waiting[0].num_tokens + self.kv_block_size()
+        if self.kv.can_allocate(n):
+            return True
+        # blocks held only by the prefix cache are free for admission purposes (_admit evicts
+        # them); without this a full cache would make prefill_first never pause the decodes
+        if self.prefix_cache is None:
+            return False
+        return self.kv.num_free_blocks + self.prefix_cache.num_evictable() >= self.kv.blocks_needed(n)
 
-    def _reserve(self, blocks: int) -> bool:
-        """``blocks`` free KV blocks, evicting unused prefix-cache blocks if needed."""
+    def _reserve(self, blocks: int, protect=()) -> bool:
+        """``blocks`` free KV blocks, evicting unused prefix-cache blocks (never those in
+        ``protect``) if needed."""
         if self.kv.num_free_blocks >= blocks:
             return True
         if self.prefix_cache is not None:
-            self.prefix_cache.evict(blocks)
+            self.prefix_cache.evict(blocks, protect)
         return self.kv.num_free_blocks >= blocks
 
     def _admit(self, seq: Sequence) -> bool:
-        """Reserve blocks for all known tokens of ``seq`` (re-attaching its cached prefix)."""
+        """Reserve blocks for all known tokens of ``seq`` (re-attaching its cached prefix).
+        The matched prefix blocks are held only by the cache until ``add_sequence_shared``
+        takes its references, so the reservation must not evict them."""
         n = seq.num_tokens  # a resumed sequence also re-covers its generated tokens
         prefix = self.prefix_cache.match(seq.all_ids) if self.prefix_cache is not None else []
         need = self.kv.blocks_needed(n + self.kv_block_size()) - len(prefix)
-        if not self._reserve(need):
+        if not self._reserve(need, protect=prefix):
             return False
         if not self.kv.add_sequence_shared(seq.seq_id, n, prefix):
             return False

@@ -142,6 +142,69 @@ def test_prefix_cache_reuses_blocks_and_evicts():
     assert _chunks(out) == [(25, 0, 25)] and pc.stats["evicted"] >= 1
 
 
+@pytest.mark.parametrize("impl", ["py", "native"])
+def test_admission_eviction_never_frees_its_own_prefix(impl):
+    """8 blocks of 4 slots, a cached 2-block prefix, one other running sequence and a 28-token
+    prompt sharing the prefix: reserving the prompt's 6 other blocks must not evict the 2 blocks
+    match() just returned (they are held only by the cache until the sequence is added) — the
+    admission waits instead, and succeeds with the prefix re-attached once space frees up."""
+    from llmctl.serve.prefix_cache import PrefixCache
+
+    kv = PyKVManager(8, 4) if impl == "py" else make_kv_manager(8, 4, prefer_native=True)
+    pc = PrefixCache(kv, 4)
+    s = ContinuousBatchScheduler(kv, max_batch_size=4, max_batch_tokens=64, block_size=4, prefix_cache=pc)
+    a = Sequence(prompt_ids=list(range(1, 11)), params=SamplingParams())
+    s.add(a)
+    _run(s, s.schedule())
+    s.finish(a, "length")
+    assert len(pc) == 2 and kv.num_free_blocks == 6
+    r = Sequence(prompt_ids=[50] * 3, params=SamplingParams())
+    s.add(r)
+    _run(s, s.schedule())
+    c = Sequence(prompt_ids=list(range(1, 9)) + [99] * 20, params=SamplingParams())
+    s.add(c)
+    out = s.schedule()  # must not raise ("incref of a free block")
+    assert c.status == "waiting" and all(q.seq is not c for q in out.prefill)
+    assert len(pc) == 2 and pc.stats["evicted"] == 0
+    s.finish(r, "length")
+    out = s.schedule()
+    assert c.status == "running" and c.cached_tokens == 8
+    assert [(q.start, q.count) for q in out.prefill if q.seq is c] == [(8, 20)]
+
+
+def test_can_admit_counts_evictable_cached_blocks():
+    """prefill_first: blocks held only by the prefix cache count as free, so a full cache does
+    not stop the policy from pausing decodes for an admission."""
+    from llmctl.serve.prefix_cache import PrefixCache
+
+    kv = PyKVManager(8, 4)
+    pc = PrefixCache(kv, 4)
+    s = ContinuousBatchScheduler(kv, max_batch_size=4, max_batch_tokens=64, block_size=4, prefix_cache=pc,
+                                 policy="prefill_first")
+    a = Sequence(prompt_ids=list(range(1, 18)), params=SamplingParams())  # 4 full blocks
+    s.add(a)
+    _run(s, s.schedule())
+    s.finish(a, "length")
+    r = Sequence(prompt_ids=[5] * 3, params=SamplingParams())
+    s.add(r)
+    _run(s, s.schedule())
+    assert kv.num_free_blocks == 3 and len(pc) == 4 and not kv.can_allocate(14)
+    s.add(Sequence(prompt_ids=[9] * 10, params=SamplingParams()))  # needs 4 blocks
+    assert s._can_admit()
+    out = s.schedule()
+    assert not out.decode and _chunks(out) == [(10, 0, 10)]
+
+
+def test_prefix_keys_are_keyed_digests():
+    from llmctl.serve.prefix_cache import PrefixCache, _block_hash
+
+    h1 = _block_hash(b"", [1, 2, 3, 4])
+    assert isinstance(h1, bytes) and len(h1) == 16
+    assert _block_hash(h1, [5, 6, 7, 8]) != _block_hash(b"", [5, 6, 7, 8])
+    pc = PrefixCache(PyKVManager(4, 4), 4)
+    assert pc._hashes([1, 2, 3, 4, 5, 6, 7, 8], 2) == [h1, _block_hash(h1, [5, 6, 7, 8])]
+
+
 def test_preempted_sequence_resumes_from_cached_blocks():
     """A sequence preempted after its prompt was computed re-attaches its full blocks when it
     is readmitted: only the tail past the last full block is recomputed."""
