@@ -235,6 +235,11 @@ MODEL_TEMPLATES: Dict[str, Dict[str, Dict[str, Any]]] = {
             "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
             "rope": {"base": 10000, "scaling": "linear"},
         },
+        "wide": {  # 8 query / 8 KV heads: enough heads for TP=8 (BASELINE config #5's degree)
+            "name": "tiny-wide", "arch": "decoder-only", "layers": 2, "hidden": 256, "ffn": 768,
+            "heads": 8, "kv_heads": 8, "vocab_size": 512, "max_position_embeddings": 512,
+            "rope": {"base": 10000, "scaling": "linear"},
+        },
         "tied": {  # GPT-2 style (layernorm, GELU, learned positions, tied LM head)
             "name": "tiny-tied", "arch": "decoder-only", "layers": 2, "hidden": 256, "ffn": 1024,
             "heads": 4, "vocab_size": 512, "norm": "layernorm", "activation": "gelu",
@@ -249,7 +254,7 @@ ALIASES = {
     "llama-13b": ("llama", "13b"), "llama-30b": ("llama", "30b"), "llama3-70b": ("llama", "70b"),
     "llama-70b": ("llama", "70b"), "tiny": ("tiny", "test"), "tiny-test": ("tiny", "test"),
     "mixtral-8x7b": ("mixtral", "8x7b"), "tiny-moe": ("tiny", "moe"),
-    "tiny-tied": ("tiny", "tied"), "tiny-deep": ("tiny", "deep"),
+    "tiny-tied": ("tiny", "tied"), "tiny-deep": ("tiny", "deep"), "tiny-wide": ("tiny", "wide"),
 }
 
 

@@ -31,7 +31,7 @@ from llmctl.models import ParallelContext
 from llmctl.utils.env import dist_env
 
 from .engine import InferenceEngine
-from .scheduler import Sequence
+from .scheduler import PrefillChunk, Sequence
 
 log = logging.getLogger("llmctl.serve.tp")
 

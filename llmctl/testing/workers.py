@@ -116,9 +116,11 @@ def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: in
 PROMPTS = [[1, 2, 3, 4, 5], [9] * 13, [7, 7], [3, 1, 4, 1, 5, 9, 2, 6]]
 
 
-def serve_generate(rank: int, world: int, max_tokens: int = 8) -> dict:
+def serve_generate(rank: int, world: int, max_tokens: int = 8, model: str = "tiny") -> dict:
     """Greedy generation through the serving engine: TP=world (TPInferenceEngine) or, with
-    world == 1, the single-process engine.  Rank 0 returns the produced token ids."""
+    world == 1, the single-process engine.  Rank 0 returns the produced token ids, plus the
+    logits of a whole-prompt prefill called with ``Sequence`` objects (the engine's public
+    ``prefill(seqs)`` form) for a row-level comparison across TP degrees."""
     import os
 
     import torch.distributed as dist
@@ -132,19 +134,30 @@ def serve_generate(rank: int, world: int, max_tokens: int = 8) -> dict:
 
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
             os.environ.pop(k, None)
-        eng = InferenceEngine("tiny", **kw)
+        eng = InferenceEngine(model, **kw)
     else:
         from llmctl.serve.tp import TPInferenceEngine
 
         dist.init_process_group("gloo")
-        eng = TPInferenceEngine("tiny", **kw)
+        eng = TPInferenceEngine(model, **kw)
         if eng.tp_rank != 0:
             eng.worker_loop()
             return {}
     seqs = eng.generate(PROMPTS, SamplingParams(max_tokens=max_tokens, temperature=0.0))
+    # Sequence-object prefill: two fresh prompts through the public entry point
+    from llmctl.serve.scheduler import Sequence
+
+    probe = [Sequence(prompt_ids=[11, 12, 13, 14, 15, 16], params=SamplingParams()),
+             Sequence(prompt_ids=[2, 4, 6], params=SamplingParams())]
+    for s in probe:
+        assert eng.kv.add_sequence(s.seq_id, s.num_tokens)
+    logits = eng.prefill(probe).float().cpu()
+    for s in probe:
+        eng.kv.free_sequence(s.seq_id)
     if world > 1:
         eng.stop_workers()
-    return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": eng.kv_cache.k.shape[-2]}
+    return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": eng.kv_cache.k.shape[-2],
+            "prefill_logits": logits}
 
 
 def serve_generate_gpu(rank: int, world: int, max_tokens: int = 8) -> dict:
