@@ -274,7 +274,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 
   // V bits (A/B'd by tools/gemm64_bench.py): 1 = issue the phase's DMA in the read section
   // (before the wait and the first barrier, where the wave otherwise idles at the barrier)
-  // instead of right before the MFMAs; 2 = no s_setprio around the MFMA cluster
+  // instead of right before the MFMAs; 2 = no s_setprio around the MFMA cluster; 4 = the
+  // two-phase schedule (ktile2 below)
   constexpr bool EARLY = V & 1, PRIO = !(V & 2);
   auto mfma_quadrant = [&](auto m0_c, auto n0_c) {
     constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
@@ -346,9 +347,78 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     bar();
   };
 
-  for (int t = 0; t < KT; t += 2) {
-    ktile(t, smem);
-    ktile(t + 1, smem + BUF);
+  // V & 4: TWO phases per K-tile, 32 MFMAs per segment (one 64x64 half of the wave's block x
+  // K = 64), so the barrier round trip + skew between segments (~80 cycles measured per 16-MFMA
+  // segment: 76 % MFMA-busy, profiles/gemm64_pmc_r2.txt) is paid half as often.  Per wave:
+  //   R0(t): reads A_lo frags (m 0-3) + all 4 B frags (n 0-3); issues B_h1(t+1), A_hi(t+1);
+  //          vmcnt(8) retires A_hi(t)                                  | partner group: M1(t-1)
+  //   M0(t): 32 MFMAs (m 0-3, n 0-3)                                   | partner: R0(t)
+  //   R1(t): reads A_hi frags (m 4-7); issues A_lo(t+2), B_h0(t+2) into THIS buffer's A_lo / B_h0
+  //          slots (last read in R0(t) by both groups, retired by the lgkmcnt(0) ending every R
+  //          segment, one barrier earlier); vmcnt(6) retires A_lo/B_h0/B_h1 of t+1
+  //   M1(t): 32 MFMAs (m 4-7, n 0-3), B frags reused                   | partner: R1(t)
+  // Every R segment ends with lgkmcnt(0) before its barrier (WAR for the next DMA, RAW for the
+  // MFMAs); all DMA issue stays out of the MFMA segments.
+  auto ktile2 = [&](int t, const unsigned char* buf) {
+    // R0
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_LO * HALF, ap + 16 * i, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
+    issue(K_<B_H1>{}, t + 1);
+    issue(K_<A_HI>{}, t + 1);
+    wait_vm<8>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_sched_barrier(0);
+    // M0
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[i][j] = mfma16(bfr[j][ks], af[i][ks], acc[i][j]);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    bar();
+    // R1
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_HI * HALF, ap + 16 * i, ks, lane);
+    issue(K_<A_LO>{}, t + 2);
+    issue(K_<B_H0>{}, t + 2);
+    wait_vm<6>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_sched_barrier(0);
+    // M1
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[4 + i][j] = mfma16(bfr[j][ks], af[i][ks], acc[4 + i][j]);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+
+  if constexpr (V & 4) {
+    // the prologue above left A_hi(0), A_lo(1), B_h0(1) in flight — the state R1(-1) leaves
+    for (int t = 0; t < KT; t += 2) {
+      ktile2(t, smem);
+      ktile2(t + 1, smem + BUF);
+    }
+  } else {
+    for (int t = 0; t < KT; t += 2) {
+      ktile(t, smem);
+      ktile(t + 1, smem + BUF);
+    }
   }
   if (wr == 0) bar();  // re-align the barrier count of the two groups
   wait_vm<0>();        // the clamped tail items are still landing
@@ -501,6 +571,8 @@ void launch_g(const G64Args& g, int variant) {
     case 1: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g); break;
     case 2: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 2>), grid, block, 0, stream(), g); break;
     case 3: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 3>), grid, block, 0, stream(), g); break;
+    case 4: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 4>), grid, block, 0, stream(), g); break;
+    case 6: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 6>), grid, block, 0, stream(), g); break;
     default: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 0>), grid, block, 0, stream(), g); break;
   }
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;

@@ -126,8 +126,9 @@ class Zero3Model:
         if u.full is not None:
             return
         u.full = torch.empty(u.numel, dtype=self.dtype, device=self.device)
-        u.gather_work = dist.all_gather_into_tensor(u.full, self._shard(u).clone(), group=self.group,
-                                                    async_op=True)
+        # the shard is read in place (no staging copy): every gather is waited before the
+        # optimizer rewrites the shards (forward / backward use, or finish_grad_sync)
+        u.gather_work = dist.all_gather_into_tensor(u.full, self._shard(u), group=self.group, async_op=True)
         if not async_op:
             self._wait(u)
 
@@ -223,18 +224,34 @@ class Zero3Model:
         if u.pending == 0 and u is not self.root:
             self._reduce_unit(u)
 
+    # reduce-scatters in flight per rank: enough to cover the next layer's backward, bounded so
+    # the unit-sized full-gradient buffers they keep alive stay a few layers' worth
+    MAX_INFLIGHT = 2
+
     def _reduce_unit(self, u: _Unit):
+        """Reduce-scatter the unit's full gradient into this rank's shard ASYNCHRONOUSLY: the next
+        layer's backward runs while RCCL reduces this one (the collective stream waits for the
+        gradient writes; the shard accumulation waits for the collective).  The unit's gathered
+        parameters are released right away — only its gradient buffer stays alive until the
+        collective has been waited for (``_drain``)."""
         c = u.numel // self.dp
         out = torch.empty(c, dtype=self.dtype, device=self.device)
-        dist.reduce_scatter_tensor(out, u.full_grad, group=self.group)
-        g = self.flat.grad[u.shard_start:u.shard_start + c]
-        g.add_(out)
+        work = dist.reduce_scatter_tensor(out, u.full_grad, group=self.group, async_op=True)
+        self._grad_works.append((work, out, u.full_grad, u.shard_start, c))
         for n, p, r in u.params:
             p.grad = None
         u.full_grad = None
         u.grad_done = True
         if u is not self.root:
             self._release(u)
+        self._drain(self.MAX_INFLIGHT)
+
+    def _drain(self, keep: int = 0):
+        """Wait for all but the ``keep`` newest gradient reduce-scatters and add their shards."""
+        while len(self._grad_works) > keep:
+            work, out, _full, start, c = self._grad_works.pop(0)
+            work.wait()
+            self.flat.grad[start:start + c].add_(out)
 
     # ------------------------------------------------------------------ engine API
     def begin_step(self):
@@ -267,6 +284,11 @@ class Zero3Model:
         if self.root is not None and self.root.full_grad is not None:
             self._reduce_unit(self.root)
             self._release(self.root)
+        self._drain(0)
+        for u in self.all_units:  # no gather may still read a shard the optimizer rewrites
+            if u.gather_work is not None:
+                u.gather_work.wait()
+                u.gather_work = None
 
     def attach_optimizer(self, opt):
         opt.dp_sharded = True

@@ -27,20 +27,21 @@ TOL = 1.2e-2  # bf16 output rounding is <= 2^-8 of the row max; fp32 accumulatio
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
 @pytest.mark.parametrize("acc", [False, True])
 @pytest.mark.parametrize("split", [0, 1, 2])
-def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split):
+@pytest.mark.parametrize("variant", [1, 4])
+def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split, variant):
     A = _bf(M, K, seed=71)
     B = _bf(N, K, seed=72)
     a = A.t().contiguous() if at else A
     b = B.t().contiguous() if bt else B
     c0 = _bf(M, N, seed=73)
     out = c0.clone() if acc else torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    native_lib.gemm64_ex(a, b, out, at, bt, acc, 104 + 1000 * split)
+    native_lib.gemm64_ex(a, b, out, at, bt, acc, 4 + 100 * variant + 1000 * split)
     want = A.float() @ B.float().t() + (c0.float() if acc else 0.0)
     assert torch.isfinite(out.float()).all()
     assert row_err(out, want) < TOL
 
 
-@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304, 1104, 2104, 4008, 8104])
+@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304, 404, 408, 604, 1104, 2104, 4008, 8104, 1404, 2404])
 def test_gemm64_configs(native_lib, config):
     """Every tile-order group / schedule variant / tail split computes the same product (fwd
     and wgrad); 1xxx = no split, Sxxx = S K-ranges (24 tiles < one round: all of them split)."""
