@@ -88,6 +88,19 @@ def build_interleaved_rounds(P: int, V: int, M: int):
     return rounds
 
 
+class _Once:
+    """Works of one batch_isend_irecv group, waited for at most once (a second ``wait`` on a
+    completed gloo receive blocks forever)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self) -> None:
+        for w in self.works or ():
+            w.wait()
+        self.works = None
+
+
 @torch.no_grad()
 def broadcast_tied_embedding(model, pg) -> None:
     """Copy stage 0's ``embed`` into the last stage's ``lm_head`` (tied word embeddings).
@@ -195,6 +208,19 @@ class PipelineSchedule:
             for w in works:
                 w.wait()
 
+    def _post_recv(self, buf: torch.Tensor, peer: int) -> List:
+        """Post a receive and return its works: the caller waits for them only when the data is
+        needed, so the transfer overlaps the compute in between.  Used only where every op
+        posted on that peer pair in the meantime is also a receive (warm-up activations from the
+        previous stage, cool-down gradients from the next), so the per-pair order of operations
+        — all NCCL matches point-to-point by — is exactly that of the un-prefetched schedule."""
+        return dist.batch_isend_irecv([dist.P2POp(dist.irecv, buf, peer)])
+
+    @staticmethod
+    def _wait(works: Optional[List]) -> None:
+        for w in works or ():
+            w.wait()
+
     def _drain_sends(self) -> None:
         for w, _ in self._pending_sends:
             w.wait()
@@ -278,20 +304,24 @@ class PipelineSchedule:
             bwd_i += 1
             return g
 
-        # warm-up forwards
-        for _ in range(warm):
-            x_in = None
-            if not self.is_first:
-                x_in = self._empty(B, S)
-                self._p2p(recv=(x_in, self.prev))
+        remaining = M - warm
+        # warm-up forwards: the receive of the NEXT activation is posted before this forward's
+        # compute (receive-ahead), so it lands while the stage computes
+        x_next, rw = None, None
+        if not self.is_first and M > 0:
+            x_next = self._empty(B, S)
+            rw = self._post_recv(x_next, self.prev)
+        for j in range(warm):
+            self._wait(rw)
+            x_in, rw = x_next, None
+            if not self.is_first and j + 1 < M:  # the next forward's input (warm-up or steady)
+                x_next = self._empty(B, S)
+                rw = self._post_recv(x_next, self.prev)
             out = do_forward(x_in)
             if not self.is_last:
                 self._p2p(send=(out.detach(), self.next))
-        remaining = M - warm
-        x_in = None
-        if remaining > 0 and not self.is_first:
-            x_in = self._empty(B, S)
-            self._p2p(recv=(x_in, self.prev))
+        self._wait(rw)
+        x_in = x_next if remaining > 0 else None
         for i in range(remaining):
             out = do_forward(x_in)
             grad_out = None
@@ -306,12 +336,17 @@ class PipelineSchedule:
                     self._p2p(send=(g, self.prev), recv=(x_in, self.prev))
                 else:
                     self._p2p(send=(g, self.prev))
-        # cool-down backwards
-        for _ in range(warm):
-            grad_out = None
-            if not self.is_last:
-                grad_out = self._empty(B, S)
-                self._p2p(recv=(grad_out, self.next))
+        # cool-down backwards: the next gradient's receive is posted before this backward
+        g_next, gw = None, None
+        if warm > 0 and not self.is_last:
+            g_next = self._empty(B, S)
+            gw = self._post_recv(g_next, self.next)
+        for j in range(warm):
+            self._wait(gw)
+            grad_out, gw = g_next, None
+            if not self.is_last and j + 1 < warm:
+                g_next = self._empty(B, S)
+                gw = self._post_recv(g_next, self.next)
             g = do_backward(grad_out)
             if not self.is_first:
                 self._p2p(send=(g, self.prev))
@@ -344,6 +379,12 @@ class PipelineSchedule:
         grads: dict = {}
         stash: dict = {}
         losses: List[torch.Tensor] = []
+        # a round's send/recv group is NOT waited at the end of the round: every received buffer
+        # remembers its group's works and is waited for when a later round consumes it, so the
+        # transfers overlap the next rounds' compute (the group stays one batch_isend_irecv:
+        # opposite-direction messages on one peer pair must be posted together)
+        arrive: dict = {}
+        inflight: List = []
         for acts, msgs in self._rounds:
             a = acts[s]
             out_msg: dict = {}
@@ -353,6 +394,7 @@ class PipelineSchedule:
                 if kind == "F":
                     x_in = None
                     if vs > 0:
+                        arrive.pop(("act", vs, mb)).wait()
                         x_in = inputs.pop((vs, mb))
                         x_in.requires_grad_(True)
                     ids, labels = batches[mb]
@@ -368,20 +410,28 @@ class PipelineSchedule:
                     if vs == last_vs:
                         out.backward()
                     else:
+                        arrive.pop(("grad", vs, mb)).wait()
                         torch.autograd.backward(out, grads.pop((vs, mb)))
                     if vs > 0:
                         out_msg[("grad", vs - 1, mb)] = x_in.grad
-            ops = []
+            ops, keys, sent = [], [], []
             for kind, src, dst, vs_dst, mb in msgs:
                 if src == s:
-                    ops.append(dist.P2POp(dist.isend, out_msg[(kind, vs_dst, mb)].contiguous(), self.ranks[dst]))
+                    t = out_msg[(kind, vs_dst, mb)].contiguous()
+                    sent.append(t)
+                    ops.append(dist.P2POp(dist.isend, t, self.ranks[dst]))
                 elif dst == s:
                     buf = self._empty(B, S)
                     (inputs if kind == "act" else grads)[(vs_dst, mb)] = buf
+                    keys.append((kind, vs_dst, mb))
                     ops.append(dist.P2POp(dist.irecv, buf, self.ranks[src]))
             if ops:
-                for w in dist.batch_isend_irecv(ops):
-                    w.wait()
+                works = _Once(dist.batch_isend_irecv(ops))
+                for k in keys:
+                    arrive[k] = works
+                inflight.append((works, sent))
+        for works, _ in inflight:
+            works.wait()
         self._set_sync(True)
         loss = torch.stack(losses).sum() if losses else torch.zeros((), device=self.e.device)
         self.last_loss = loss

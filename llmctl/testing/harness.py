@@ -23,6 +23,10 @@ def _entry(rank, world, port, fn, args, q):
     import torch
 
     torch.set_num_threads(1)
+    if os.environ.get("LLMCTL_HANG_DUMP"):  # debugging aid: stacks of every rank after N s
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["LLMCTL_HANG_DUMP"]), exit=False)
     try:
         out = fn(rank, world, *args)
         import io
