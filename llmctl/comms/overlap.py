@@ -49,11 +49,17 @@ class GradSyncEngine:
         self._next = 0
         self._works: List = []
         self._hooks = []
+        sink = getattr(flat, "sink", None)
         for b in flat.buckets:
             for p in b.params:
+                # GEMM-written grads (llmctl.exec.linear) signal readiness through the sink only:
+                # autograd still runs a sinked parameter's post-accumulate hook (with grad None),
+                # and counting both made a multi-parameter bucket launch before its last gradient
+                # was written (caught by the DP2 x TP2 equivalence tests)
+                if sink is not None and getattr(p, "_llmctl_grad_sink", None) is sink:
+                    continue
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
-        sink = getattr(flat, "sink", None)
-        if sink is not None:  # GEMM-written grads (llmctl.exec.linear) signal readiness here
+        if sink is not None:
             sink.callbacks.append(self._on_grad)
         self._expected = {b.index: len(b.params) for b in flat.buckets}
 

@@ -44,9 +44,11 @@ def _config(**kw):
 
 
 def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "tiny",
-                 micro_per_rank: int = 1) -> dict:
+                 micro_per_rank: int = 1, overrides: Optional[dict] = None) -> dict:
     """Run ``steps`` optimizer steps under ``layout`` (tp/pp/zero/sp/...) and return the
-    gathered full state + losses (rank 0 meaningful)."""
+    gathered full state + losses (rank 0 meaningful).  ``overrides``: extra TrainingConfig
+    fields (e.g. a larger Adam eps, so gradient elements that are zero in exact arithmetic —
+    fp32 summation-order noise — do not become +-lr updates whose sign differs per layout)."""
     from llmctl.runtime.engine import TrainingEngine
 
     if layout.get("staging"):  # host-staging patches installed (CPU tensors pass through)
@@ -62,7 +64,7 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
                   context_parallel=layout.get("cp", 1),
                   context_parallel_mode=layout.get("cp_mode", "ulysses"),
                   expert_parallel=layout.get("ep", 1),
-                  pack_sequences=layout.get("pack", False), doc_separator=PACK_SEP)
+                  pack_sequences=layout.get("pack", False), doc_separator=PACK_SEP, **(overrides or {}))
     eng = TrainingEngine(cfg)
     eng.load_full_state_dict(reference_state(model))
     vocab = eng.model_config.vocab_size
@@ -91,7 +93,7 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
 
 
 def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: int = 1,
-                    pack: bool = False) -> dict:
+                    pack: bool = False, overrides: Optional[dict] = None) -> dict:
     """Single process; the DP ranks' batches are accumulation micro-steps."""
     import os
 
@@ -99,7 +101,7 @@ def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: in
 
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         os.environ.pop(k, None)
-    cfg = _config(model_name_or_path=model, pack_sequences=pack, doc_separator=PACK_SEP)
+    cfg = _config(model_name_or_path=model, pack_sequences=pack, doc_separator=PACK_SEP, **(overrides or {}))
     eng = TrainingEngine(cfg)
     eng.load_full_state_dict(reference_state(model))
     vocab = eng.model_config.vocab_size

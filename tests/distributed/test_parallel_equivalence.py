@@ -252,3 +252,15 @@ def test_moe_dp4_ep2_zero1_matches_single():
     out = run_ranks(train_layout, 4, STEPS, {"ep": 2, "zero": 1}, "tiny-moe")
     _losses_close(out[0]["losses"], ref["losses"])
     _close(out[0]["state"], ref["state"])
+
+
+@pytest.mark.parametrize("zero", [0, 1])
+def test_dp2_tp2_multi_param_buckets_match_single(zero):
+    """DP x TP on the 8-layer model, where a DP bucket holds several GEMM-written (sinked)
+    weights (wo + wqkv): the bucket must launch only after its LAST gradient is written.
+    Regression: autograd also runs a sinked weight's post-accumulate hook (grad None), the sync
+    engine counted it twice and all-reduced the bucket before wqkv's gradient existed."""
+    ref = train_reference(STEPS, dp=2, model="tiny-deep")
+    out = run_ranks(train_layout, 4, STEPS, {"tp": 2, "zero": zero}, "tiny-deep")
+    _losses_close(out[0]["losses"], ref["losses"])
+    _close(out[0]["state"], ref["state"])
