@@ -123,6 +123,7 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
   else static_assert(N == 0, "add the immediate");
 }
 
@@ -274,8 +275,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 
   // V bits (A/B'd by tools/gemm64_bench.py): 1 = issue the phase's DMA in the read section
   // (before the wait and the first barrier, where the wave otherwise idles at the barrier)
-  // instead of right before the MFMAs; 2 = no s_setprio around the MFMA cluster; 4 = the
-  // two-phase schedule (ktile2 below)
+  // instead of right before the MFMAs; 2 = no s_setprio around the MFMA cluster.  (A two-phase
+  // schedule with 32-MFMA segments measured neutral, +-1 %: profiles/gemm_ld_probe_r3.txt.)
   constexpr bool EARLY = V & 1, PRIO = !(V & 2);
   auto mfma_quadrant = [&](auto m0_c, auto n0_c) {
     constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
@@ -347,78 +348,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     bar();
   };
 
-  // V & 4: TWO phases per K-tile, 32 MFMAs per segment (one 64x64 half of the wave's block x
-  // K = 64), so the barrier round trip + skew between segments (~80 cycles measured per 16-MFMA
-  // segment: 76 % MFMA-busy, profiles/gemm64_pmc_r2.txt) is paid half as often.  Per wave:
-  //   R0(t): reads A_lo frags (m 0-3) + all 4 B frags (n 0-3); issues B_h1(t+1), A_hi(t+1);
-  //          vmcnt(8) retires A_hi(t)                                  | partner group: M1(t-1)
-  //   M0(t): 32 MFMAs (m 0-3, n 0-3)                                   | partner: R0(t)
-  //   R1(t): reads A_hi frags (m 4-7); issues A_lo(t+2), B_h0(t+2) into THIS buffer's A_lo / B_h0
-  //          slots (last read in R0(t) by both groups, retired by the lgkmcnt(0) ending every R
-  //          segment, one barrier earlier); vmcnt(6) retires A_lo/B_h0/B_h1 of t+1
-  //   M1(t): 32 MFMAs (m 4-7, n 0-3), B frags reused                   | partner: R1(t)
-  // Every R segment ends with lgkmcnt(0) before its barrier (WAR for the next DMA, RAW for the
-  // MFMAs); all DMA issue stays out of the MFMA segments.
-  auto ktile2 = [&](int t, const unsigned char* buf) {
-    // R0
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_LO * HALF, ap + 16 * i, ks, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
-    issue(K_<B_H1>{}, t + 1);
-    issue(K_<A_HI>{}, t + 1);
-    wait_vm<8>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    __builtin_amdgcn_sched_barrier(0);
-    // M0
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) acc[i][j] = mfma16(bfr[j][ks], af[i][ks], acc[i][j]);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    bar();
-    // R1
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_HI * HALF, ap + 16 * i, ks, lane);
-    issue(K_<A_LO>{}, t + 2);
-    issue(K_<B_H0>{}, t + 2);
-    wait_vm<6>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    __builtin_amdgcn_sched_barrier(0);
-    // M1
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) acc[4 + i][j] = mfma16(bfr[j][ks], af[i][ks], acc[4 + i][j]);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    bar();
-  };
-
-  if constexpr (V & 4) {
-    // the prologue above left A_hi(0), A_lo(1), B_h0(1) in flight — the state R1(-1) leaves
-    for (int t = 0; t < KT; t += 2) {
-      ktile2(t, smem);
-      ktile2(t + 1, smem + BUF);
-    }
-  } else {
-    for (int t = 0; t < KT; t += 2) {
-      ktile(t, smem);
-      ktile(t + 1, smem + BUF);
-    }
+  for (int t = 0; t < KT; t += 2) {
+    ktile(t, smem);
+    ktile(t + 1, smem + BUF);
   }
   if (wr == 0) bar();  // re-align the barrier count of the two groups
   wait_vm<0>();        // the clamped tail items are still landing
@@ -518,6 +450,297 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   }
 }
 
+// ---- persistent variant ------------------------------------------------------------------------
+// Measured (profiles/gemm_ld_probe_r3.txt): the same kernel runs ~1450 TF at K = 4096 and
+// ~1525 TF at K = 11008-32000 — a fixed per-tile cost (workgroup launch, the prologue's pipeline
+// fill with nothing to overlap it, the epilogue's store tail) of ~5 % of a 92-us K = 4096 tile.
+// gemm64p_kernel keeps one workgroup per CU resident and walks the work items g = blockIdx.x,
+// + gridDim.x, ...: the K-tile DMA stream does not stop at a tile boundary — the items past the
+// last K-tile of tile i (which the one-shot kernel re-loads and discards) ARE the first K-tiles
+// of tile i+1, in exactly the prologue's order, so tile i+1 starts with its first operands
+// already in LDS.  The epilogue of tile i runs between the two K-loops with no barrier; as the
+// two wave groups run one barrier apart, each group's epilogue overlaps the other group's MFMA
+// segment.  Epilogue stores are inline-asm global_store (exactly EPI_OPS vector-memory ops per
+// thread, which the first wait of the next tile counts past); epilogues that load (accumulate,
+// SwiGLU backward) end with vmcnt(0) instead.
+struct Item {
+  int tm, tn, sp, u, KT;
+  unsigned kt0;
+};
+
+template <int GROUP>
+__device__ __forceinline__ Item decode_item(const G64Args& args, int bid) {
+  int wg, sp = -1, u = 0;
+  if (bid < args.n_main) {
+    const int nwg = args.n_main;
+    const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
+    wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
+  } else {
+    const int i = bid - args.n_main;
+    u = i / args.splits;
+    sp = i - u * args.splits;
+    wg = args.n_main + u;
+  }
+  const int per_group = GROUP * args.tiles_n;
+  const int grp = wg / per_group;
+  const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
+  const int inner = wg - grp * per_group;
+  Item it;
+  it.tm = grp * GROUP + inner % gsz;
+  it.tn = inner / gsz;
+  it.sp = sp;
+  it.u = u;
+  it.KT = sp < 0 ? args.K / TK : args.kt_part;
+  it.kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
+  return it;
+}
+
+constexpr int EPI_OPS = 32;  // vector-memory ops per thread of a store-only epilogue (8 x 4 tiles)
+
+__device__ __forceinline__ void st_x2(unsigned short* p, s2_t v) {
+  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_x4(float* p, f32x4_t v) {
+  asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+
+template <bool AT, bool BT, int EPI, int GROUP>
+__global__ __launch_bounds__(NTHR, 1) void gemm64p_kernel(G64Args args, int n_items) {
+  static_assert(EPI != EPI_SWIGLU_FWD, "the pairing epilogue exchanges through LDS: one-shot kernel only");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  int g = blockIdx.x;
+  if (g >= n_items) return;
+  const long lda = args.lda, ldb = args.ldb;
+  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
+  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
+  auto base_a = [&](const Item& it) {
+    return AT ? args.a + (long)it.tm * TM : args.a + (long)it.tm * TM * lda;
+  };
+  auto base_b = [&](const Item& it) {
+    return BT ? args.b + (long)it.tn * TN : args.b + (long)it.tn * TN * ldb;
+  };
+  // only what the DMA stream needs stays live through the K-loop (SGPR budget): the current and
+  // next item's operand bases and K-tile ranges; the epilogue re-decodes its item
+  Item cur = decode_item<GROUP>(args, g);
+  const unsigned short *pa = base_a(cur), *pb = base_b(cur);
+  unsigned kt0 = cur.kt0;
+  int KT = cur.KT;
+  int gn = g + (int)gridDim.x;
+  bool has_next = gn < n_items;
+  const unsigned short *pa_x = pa, *pb_x = pb;
+  unsigned kx = kt0 + (unsigned)(KT - 1);
+  int kx_step = 0;
+  if (has_next) {
+    const Item nx = decode_item<GROUP>(args, gn);
+    pa_x = base_a(nx);
+    pb_x = base_b(nx);
+    kx = nx.kt0;
+    kx_step = 1;
+  }
+
+  unsigned vo[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    vo[A_LO][i] = stage_voff<AT, A_LO>(i, tid, lda);
+    vo[A_HI][i] = stage_voff<AT, A_HI>(i, tid, lda);
+    vo[B_H0][i] = stage_voff<BT, B_H0>(i, tid, ldb);
+    vo[B_H1][i] = stage_voff<BT, B_H1>(i, tid, ldb);
+  }
+  const unsigned lds0 = lds_addr(smem) + wave * 1024;
+
+  // stream item: half-tile KIND of K-tile t of the current item; t >= KT continues into the next
+  // item's K-tiles 0, 1 (KT is even, so the LDS buffer parity carries over); with no next item the
+  // last K-tile is re-loaded into slots nobody reads again
+  // stream item: half-tile KIND of K-tile t; t >= KT continues into the next item (pa_x / pb_x /
+  // kx: the next item's bases and first K-tile, or — with no next item — the current bases and
+  // its last K-tile with step 0, i.e. a discarded re-load).  Branch-free scalar selects: a
+  // branch per issue cost ~3 s_cbranch per DMA piece in the inner loop
+  auto issue = [&](auto kind_c, int t) {
+    constexpr int kind = decltype(kind_c)::value;
+    const int over = t - KT;
+    const unsigned long m = (unsigned long)(long)(over >> 31);  // all ones while t < KT
+    const unsigned long pc = (unsigned long)(kind <= A_HI ? pa : pb), px = (unsigned long)(kind <= A_HI ? pa_x : pb_x);
+    const unsigned long base = px ^ ((pc ^ px) & m);
+    const unsigned tx = kx + (unsigned)(over * kx_step);
+    const unsigned tc = tx ^ ((tx ^ (kt0 + (unsigned)t)) & (unsigned)m);
+    const i32x4_t r = make_rsrc(reinterpret_cast<const void*>(base));
+    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
+    const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
+    bdma16(r, vo[kind][0], so, l);
+    bdma16(r, vo[kind][1], so, l + 8192);
+  };
+
+  f32x4_t acc[8][4];
+  const int ap = wr * 64, bh = (wc >> 1) * HALF, bp = (wc & 1) * 64;
+  bf16x8_t af[4][2], bfr[4][2];
+  auto mfma_quadrant = [&](auto m0_c, auto n0_c) {
+    constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[m0 + i][n0 + j] = mfma16(bfr[n0 + j][ks], af[i][ks], acc[m0 + i][n0 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // gemm64_kernel's variant-1 schedule (DMA issued in the read section); AFTER_EPI: the first
+  // K-tile after an epilogue, whose j = 1 wait also counts the EPI_OPS stores issued between
+  auto ktile = [&](int t, const unsigned char* buf, bool after_epi) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_LO * HALF, ap + 16 * i, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
+    issue(K_<B_H1>{}, t + 1);
+    bar();
+    mfma_quadrant(K_<0>{}, K_<0>{});
+    bar();
+#pragma unroll
+    for (int j = 2; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
+    issue(K_<A_HI>{}, t + 1);
+    if (after_epi) wait_vm<8 + EPI_OPS>();  // wave-uniform scalar branch
+    else wait_vm<8>();
+    bar();
+    mfma_quadrant(K_<0>{}, K_<2>{});
+    bar();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_HI * HALF, ap + 16 * i, ks, lane);
+    issue(K_<A_LO>{}, t + 2);
+    bar();
+    mfma_quadrant(K_<4>{}, K_<2>{});
+    bar();
+    issue(K_<B_H0>{}, t + 2);
+    wait_vm<6>();
+    bar();
+    mfma_quadrant(K_<4>{}, K_<0>{});
+    bar();
+  };
+
+  // prologue (first item only): the stream up to B_h0(1) in flight; A_lo/B_h0/B_h1 of K-tile 0 retired
+  issue(K_<A_LO>{}, 0);
+  issue(K_<B_H0>{}, 0);
+  issue(K_<B_H1>{}, 0);
+  issue(K_<A_HI>{}, 0);
+  issue(K_<A_LO>{}, 1);
+  issue(K_<B_H0>{}, 1);
+  wait_vm<6>();
+  bar();
+  if (wr == 1) bar();  // wave group 1 runs one barrier behind group 0 (for the whole launch)
+
+  bool first = true;
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma nounroll
+    for (int t = 0; t < KT; t += 2) {
+      ktile(t, smem, t == 0 && !first);
+      ktile(t + 1, smem + BUF, false);
+    }
+    // ---- epilogue of the current item (lane: C[m = .. + (l&15)][n = .. + 4(l>>4) + r])
+    cur = decode_item<GROUP>(args, g);
+    const int gq = lane >> 4, i16 = lane & 15;
+    if (cur.sp >= 0) {  // split item: fp32 partial tile, row-major 256 x 256
+      float* W = args.ws + ((long)cur.u * args.splits + cur.sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 64 + 4 * gq;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st_x4(W + (16 * i) * TN + 16 * j, acc[i][j]);
+    } else {
+      unsigned short* Cb =
+          args.c + (long)(cur.tm * TM + wr * 128 + i16) * args.ldc + cur.tn * TN + wc * 64 + 4 * gq;
+      if constexpr (EPI == EPI_SWIGLU_BWD) {
+        const unsigned short* Gb = args.aux + (Cb - args.c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s2_t gv[4], uv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const unsigned short* gp = Gb + (long)(16 * i) * args.ldc + 16 * j;
+            gv[j] = *reinterpret_cast<const s2_t*>(gp);
+            uv[j] = *reinterpret_cast<const s2_t*>(gp + args.N);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            unsigned short* p = Cb + (long)(16 * i) * args.ldc + 16 * j;
+            const f32x4_t v = acc[i][j];
+            const float gf[4] = {bf2f(gv[j][0] & 0xffff), bf2f(gv[j][0] >> 16), bf2f(gv[j][1] & 0xffff),
+                                 bf2f(gv[j][1] >> 16)};
+            const float uf[4] = {bf2f(uv[j][0] & 0xffff), bf2f(uv[j][0] >> 16), bf2f(uv[j][1] & 0xffff),
+                                 bf2f(uv[j][1] >> 16)};
+            float dg[4], du[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) swiglu_bwd1(v[e], gf[e], uf[e], dg[e], du[e]);
+            s2_t og, ou;
+            og[0] = (unsigned)f2bf(dg[0]) | ((unsigned)f2bf(dg[1]) << 16);
+            og[1] = (unsigned)f2bf(dg[2]) | ((unsigned)f2bf(dg[3]) << 16);
+            ou[0] = (unsigned)f2bf(du[0]) | ((unsigned)f2bf(du[1]) << 16);
+            ou[1] = (unsigned)f2bf(du[2]) | ((unsigned)f2bf(du[3]) << 16);
+            *reinterpret_cast<s2_t*>(p) = og;
+            *reinterpret_cast<s2_t*>(p + args.N) = ou;
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            unsigned short* p = Cb + (long)(16 * i) * args.ldc + 16 * j;
+            f32x4_t v = acc[i][j];
+            if constexpr (EPI == EPI_ACC) {
+              const s2_t old = *reinterpret_cast<const s2_t*>(p);
+              v[0] += bf2f(old[0] & 0xffff);
+              v[1] += bf2f(old[0] >> 16);
+              v[2] += bf2f(old[1] & 0xffff);
+              v[3] += bf2f(old[1] >> 16);
+            }
+            s2_t o;
+            o[0] = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+            o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+            st_x2(p, o);
+          }
+        if constexpr (EPI == EPI_ACC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    if (!has_next) break;
+    // advance: the next item's first K-tiles are already in flight / landed
+    g = gn;
+    pa = pa_x;
+    pb = pb_x;
+    kt0 = kx;
+    KT = g < args.n_main ? args.K / TK : args.kt_part;
+    gn += (int)gridDim.x;
+    has_next = gn < n_items;
+    kx = kt0 + (unsigned)(KT - 1);
+    kx_step = 0;
+    if (has_next) {
+      const Item nx = decode_item<GROUP>(args, gn);
+      pa_x = base_a(nx);
+      pb_x = base_b(nx);
+      kx = nx.kt0;
+      kx_step = 1;
+    }
+    first = false;
+  }
+  if (wr == 0) bar();  // re-align the barrier count of the two groups
+  wait_vm<0>();        // the clamped tail items are still landing
+}
+
 // sum of the split partials of tail tile u (grouped-order position n_main + u) + epilogue;
 // thread = 8 consecutive columns of one row
 template <int EPI, int GROUP>
@@ -567,12 +790,18 @@ template <bool AT, bool BT, int EPI, int GROUP>
 void launch_g(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
   const dim3 grid(n_items), block(NTHR);
+  if constexpr (EPI != EPI_SWIGLU_FWD) {
+    if (variant == 5) {  // persistent: one workgroup per CU walks the items
+      const dim3 pgrid(min(n_items, num_cus()));
+      hipLaunchKernelGGL((gemm64p_kernel<AT, BT, EPI, GROUP>), pgrid, block, 0, stream(), g, n_items);
+      variant = -1;
+    }
+  }
   switch (variant) {
+    case -1: break;
     case 1: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g); break;
     case 2: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 2>), grid, block, 0, stream(), g); break;
     case 3: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 3>), grid, block, 0, stream(), g); break;
-    case 4: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 4>), grid, block, 0, stream(), g); break;
-    case 6: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 6>), grid, block, 0, stream(), g); break;
     default: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 0>), grid, block, 0, stream(), g); break;
   }
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;

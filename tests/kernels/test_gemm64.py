@@ -27,7 +27,7 @@ TOL = 1.2e-2  # bf16 output rounding is <= 2^-8 of the row max; fp32 accumulatio
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
 @pytest.mark.parametrize("acc", [False, True])
 @pytest.mark.parametrize("split", [0, 1, 2])
-@pytest.mark.parametrize("variant", [1, 4])
+@pytest.mark.parametrize("variant", [1, 5])
 def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split, variant):
     A = _bf(M, K, seed=71)
     B = _bf(N, K, seed=72)
@@ -41,7 +41,7 @@ def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split, variant):
     assert row_err(out, want) < TOL
 
 
-@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304, 404, 408, 604, 1104, 2104, 4008, 8104, 1404, 2404])
+@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304, 504, 508, 1104, 2104, 4008, 8104, 1504, 2504, 8504])
 def test_gemm64_configs(native_lib, config):
     """Every tile-order group / schedule variant / tail split computes the same product (fwd
     and wgrad); 1xxx = no split, Sxxx = S K-ranges (24 tiles < one round: all of them split)."""
@@ -63,10 +63,32 @@ def test_gemm64_split_tail_multi_round(native_lib):
     A, B = _bf(K, M, seed=91), _bf(K, N, seed=92)
     c0 = _bf(M, N, seed=93)
     want = A.float().t() @ B.float()
-    for cfg in (104, 8104):
+    for cfg in (104, 8104, 504, 1504, 8504):  # x5xx: persistent (items streamed per CU)
         out = c0.clone()
         native_lib.gemm64_ex(A, B, out, True, True, True, cfg)
         assert row_err(out, want + c0.float()) < TOL, cfg
+        out = torch.full_like(c0, float("nan"))
+        native_lib.gemm64_ex(A, B, out, True, True, False, cfg)
+        assert row_err(out, want) < TOL, cfg
+
+
+@pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True)])
+def test_gemm64_persistent_many_rounds(native_lib, at, bt):
+    """Persistent kernel over ~3.4 rounds of items per CU with a split tail: every workgroup
+    streams several tiles back to back (the next tile's first K-tiles ride on the previous
+    tile's DMA stream); fwd / dgrad / wgrad layouts vs fp32."""
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    tiles = n_cu * 3 + n_cu // 3
+    M, N, K = 256 * (tiles // 4 + 1), 256 * 4, 512
+    A, B = _bf(M, K, seed=11), _bf(N, K, seed=12)
+    a = A.t().contiguous() if at else A
+    b = B.t().contiguous() if bt else B
+    want = A.float() @ B.float().t()
+    for cfg in (504, 1504):
+        out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        native_lib.gemm64_ex(a, b, out, at, bt, False, cfg)
+        assert torch.isfinite(out.float()).all(), cfg
+        assert row_err(out, want) < TOL, cfg
 
 
 def test_gemm64_strided_views(native_lib):
@@ -117,7 +139,7 @@ def test_linear_backward_on_gemm64(native_lib, monkeypatch, mode):
 
 
 @pytest.mark.parametrize("M,H,F", [(256, 256, 256), (512, 384, 768), (2304, 1024, 1280)])
-@pytest.mark.parametrize("config", [104, 1104, 2104])
+@pytest.mark.parametrize("config", [104, 1104, 2104, 504, 2504])
 def test_gemm64_swiglu_dgrad(native_lib, M, H, F, config):
     """Down-projection data gradient with the SwiGLU backward in the store epilogue (and in the
     tail-split reduction, config 2104): dgu vs fp32 swiglu_bwd(dy @ W, gu)."""
