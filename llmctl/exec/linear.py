@@ -310,6 +310,16 @@ def data_grad(dy: torch.Tensor, w: torch.nn.Parameter) -> torch.Tensor:
     return dy.matmul(w)
 
 
+def data_grad_into(dy2: torch.Tensor, w: torch.nn.Parameter, out: torch.Tensor) -> None:
+    """``out = dy2 @ w`` into a preallocated (row-slice) output: gemm64 writes it directly."""
+    if dgrad64_ok(dy2, w) and _rows_ok(out):
+        from llmctl.ops._lib import native
+
+        native().gemm64_ex(dy2, w, out, False, True, False, gemm64_config("dgrad", dy2.shape[0], w.shape[1], w.shape[0]))
+        return
+    out.copy_(data_grad(dy2, w))
+
+
 def swiglu_data_grad(dy: torch.Tensor, w: torch.nn.Parameter, gu: torch.Tensor) -> torch.Tensor:
     """``swiglu_bwd(dy @ w, gu)`` for the MLP down projection: on gemm64 the SwiGLU backward runs
     in the data-gradient GEMM's epilogue (``gemm64_swiglu_dgrad``: dgate / dup from the fp32 dAct

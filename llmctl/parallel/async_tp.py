@@ -27,7 +27,6 @@ from typing import List, Optional
 
 import torch
 import torch.distributed as dist
-import torch.nn.functional as F
 
 from llmctl.exec.linear import data_grad, weight_grad
 
@@ -50,28 +49,39 @@ def _shift(send: torch.Tensor, nxt: int, prv: int, group):
     return recv, works, send
 
 
-def _ag_matmul(x: torch.Tensor, group, mm) -> (torch.Tensor, torch.Tensor):
-    """gather(x) (token chunks in rank order) fed chunk by chunk to ``mm``; returns
-    (cat of mm outputs in rank order, gathered x)."""
+def _ag_matmul(x: torch.Tensor, group, mm, n_out: int, keep_full: bool = True):
+    """gather(x) (token chunks in rank order) fed chunk by chunk to ``mm(chunk, out_view)``,
+    which writes its product straight into the rows of one preallocated output (no torch.cat
+    pass); received chunks land directly in the rows of one preallocated gathered-input buffer
+    (returned when ``keep_full``, else None)."""
     ws, r, nxt, prv = _peers(group)
-    chunks: List[Optional[torch.Tensor]] = [None] * ws
-    outs: List[Optional[torch.Tensor]] = [None] * ws
-    cur = x.contiguous()
+    x = x.contiguous()
+    T = x.shape[0]
+    y = torch.empty(ws * T, n_out, dtype=x.dtype, device=x.device)
+    full = torch.empty(ws * T, *x.shape[1:], dtype=x.dtype, device=x.device) if keep_full or ws > 2 else None
+    cur = x
     for s in range(ws):
         c = (r - s) % ws
-        chunks[c] = cur
-        pending = _shift(cur, nxt, prv, group) if s < ws - 1 else None  # next chunk on the wire
-        outs[c] = mm(cur)
+        pending = None
+        if s < ws - 1:  # the next chunk on the wire while this one multiplies
+            cp = (c - 1) % ws
+            dst = full[cp * T:(cp + 1) * T] if full is not None else torch.empty_like(x)
+            pending = (dst, dist.batch_isend_irecv([dist.P2POp(dist.isend, cur, nxt, group),
+                                                     dist.P2POp(dist.irecv, dst, prv, group)]))
+        mm(cur, y[c * T:(c + 1) * T])
         if pending is not None:
             for w in pending[1]:
                 w.wait()
             cur = pending[0]
-    return torch.cat(outs, 0), torch.cat(chunks, 0)
+    if full is not None and keep_full:
+        full[r * T:(r + 1) * T].copy_(x)
+        return y, full
+    return y, None
 
 
 def _matmul_rs(x_full: torch.Tensor, group, mm) -> torch.Tensor:
     """reduce_scatter over token chunks of mm(x_full), chunk-wise: the partial sum of chunk
-    (r - s - 1) % ws is computed at step s, added to the one received and passed on."""
+    (r - s - 1) % ws is computed at step s, added (in place) to the one received and passed on."""
     ws, r, nxt, prv = _peers(group)
     if x_full.shape[0] % ws:
         raise ValueError(f"token dim {x_full.shape[0]} not divisible by tp={ws}")
@@ -84,32 +94,86 @@ def _matmul_rs(x_full: torch.Tensor, group, mm) -> torch.Tensor:
         if pending is not None:  # the partial of chunk c from the previous rank
             for w in pending[1]:
                 w.wait()
-            part = part + pending[0]
+            part.add_(pending[0])
         if s < ws - 1:
-            pending = _shift(part.contiguous(), nxt, prv, group)
+            pending = _shift(part, nxt, prv, group)
         else:
             acc = part
     return acc
 
 
+def _save_full() -> bool:
+    """Keep the gathered input of a column-parallel SP linear for its weight gradient (tp x the
+    shard's activation memory per QKV / up projection) instead of re-gathering it in backward."""
+    return os.environ.get("LLMCTL_ASYNC_TP_SAVE_FULL", "0") == "1"
+
+
+def _fwd_into(w, b):
+    """Chunk GEMM writing into a row slice of the preallocated output: gemm64 straight into the
+    slice where forward_linear would pick it, else forward_linear (hipBLASLt) + one copy."""
+    from llmctl.exec.linear import forward_linear
+
+    def mm(xc, out):
+        if _direct(xc, w, out):
+            _gemm_into(xc, w, b, out)
+        elif out.is_contiguous():
+            torch.mm(xc, w.t(), out=out)
+            if b is not None:
+                out += b
+        else:
+            out.copy_(forward_linear(xc, w, b))
+    return mm
+
+
+def _direct(xc, w, out) -> bool:
+    from llmctl.exec.linear import fwd64_pick, _gemm64_ok
+
+    M, K = xc.shape
+    N = w.shape[0]
+    return fwd64_pick(M, N, K) and _gemm64_ok(M, N, K, xc, w, out)
+
+
+def _gemm_into(xc, w, b, out):
+    from llmctl.exec.linear import gemm64_config
+    from llmctl.ops._lib import native
+
+    M, K = xc.shape
+    native().gemm64_ex(xc, w, out, False, False, False, gemm64_config("fwd", M, w.shape[0], K))
+    if b is not None:
+        out += b
+
+
 class _ColumnSP(torch.autograd.Function):
-    """y = gather(x_shard) @ W^T (+ b) with the gather overlapped; W column-parallel."""
+    """y = gather(x_shard) @ W^T (+ b) with the gather overlapped; W column-parallel.  Saves only
+    the local token shard: backward re-gathers it (an async all-gather running beside the
+    data-gradient ring) for the weight gradient, as Megatron does — keeping the gathered input
+    would cost tp x the shard's memory per projection, undoing SP's activation saving."""
 
     @staticmethod
     def forward(ctx, x, w, b, group):
-        y, x_full = _ag_matmul(x, group, lambda xc: F.linear(xc, w, b))
-        ctx.save_for_backward(x_full, w)
-        ctx.wparam, ctx.group, ctx.has_b = w, group, b is not None
+        keep = _save_full()
+        y, x_full = _ag_matmul(x, group, _fwd_into(w, b), w.shape[0], keep_full=keep)
+        ctx.save_for_backward(x_full if keep else x.contiguous(), w)
+        ctx.wparam, ctx.group, ctx.has_b, ctx.keep = w, group, b is not None, keep
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x_full, w = ctx.saved_tensors
+        xs, w = ctx.saved_tensors
         dy = dy.contiguous()
+        gather = None
+        if ctx.needs_input_grad[1] and not ctx.keep:
+            ws = dist.get_world_size(ctx.group)
+            x_full = torch.empty(ws * xs.shape[0], *xs.shape[1:], dtype=xs.dtype, device=xs.device)
+            gather = dist.all_gather_into_tensor(x_full, xs, group=ctx.group, async_op=True)
+        else:
+            x_full = xs
+        dx = _matmul_rs(dy, ctx.group, lambda g: data_grad(g, ctx.wparam)) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
+            if gather is not None:
+                gather.wait()
             dw = weight_grad(ctx.wparam, dy, x_full)  # through the grad sink when present
-        dx = _matmul_rs(dy, ctx.group, lambda g: data_grad(g, ctx.wparam)) if ctx.needs_input_grad[0] else None
         db = dy.sum(0) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db, None
 
@@ -119,14 +183,22 @@ class _RowSP(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, group):
+        from llmctl.exec.linear import forward_linear
+
         ctx.save_for_backward(x, w)
         ctx.wparam, ctx.group = w, group
-        return _matmul_rs(x.contiguous(), group, lambda xc: F.linear(xc, w))
+        return _matmul_rs(x.contiguous(), group, lambda xc: forward_linear(xc, w))
 
     @staticmethod
     def backward(ctx, dy):
         x_full, w = ctx.saved_tensors
-        dx, dy_full = _ag_matmul(dy.contiguous(), ctx.group, lambda g: data_grad(g, ctx.wparam))
+
+        def dgrad_into(g, out):
+            from llmctl.exec.linear import data_grad_into
+
+            data_grad_into(g, ctx.wparam, out)
+
+        dx, dy_full = _ag_matmul(dy.contiguous(), ctx.group, dgrad_into, w.shape[1])
         dw = None
         if ctx.needs_input_grad[1]:
             dw = weight_grad(ctx.wparam, dy_full, x_full.reshape(-1, x_full.shape[-1]))

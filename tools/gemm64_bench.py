@@ -50,8 +50,6 @@ def main():
     ap.add_argument("--groups", type=int, nargs="+", default=[4, 8])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--no-old", action="store_true")
-    ap.add_argument("--w4", type=int, nargs="*", default=[],
-                    help="gemm_w4_ex configs to run too (one wave per SIMD, 128x128 per wave)")
     a = ap.parse_args()
     assert _lib.load(), _lib._error
     ops = torch.ops.llmctl
@@ -84,18 +82,6 @@ def main():
             g2 = g.clone()
             ops.gemm64_ex(dy, x, g2, True, True, True, 4)
             errs["wgrad_acc"] = max_row_err(g2, (ref.float() * 2).to(torch.bfloat16))
-            for c in a.w4:
-                ops.gemm_w4_ex(dy, x, g, True, True, False, c)
-                errs[f"wgrad_w4c{c}"] = max_row_err(g, ref)
-            if a.w4:
-                ref = dy.matmul(W)
-                for c in a.w4:
-                    ops.gemm_w4_ex(dy, W, dx, False, True, False, c)
-                    errs[f"dgrad_w4c{c}"] = max_row_err(dx, ref)
-                ref = torch.nn.functional.linear(x, W)
-                for c in a.w4:
-                    ops.gemm_w4_ex(x, W, y, False, False, False, c)
-                    errs[f"fwd_w4c{c}"] = max_row_err(y, ref)
             del ref, g2
             worst = max(worst, max(errs.values()))
         cases = {
@@ -108,10 +94,6 @@ def main():
                 cases["fwd_old"] = lambda: ops.gemm_ex(x, W, y, False, False, False)
                 cases["dgrad_old"] = lambda: ops.gemm_ex(dy, W, dx, False, True, False)
                 cases["wgrad_old"] = lambda: ops.gemm_ex(dy, x, g, True, True, False)
-            for c in a.w4:
-                cases[f"fwd_w4c{c}"] = lambda c=c: ops.gemm_w4_ex(x, W, y, False, False, False, c)
-                cases[f"dgrad_w4c{c}"] = lambda c=c: ops.gemm_w4_ex(dy, W, dx, False, True, False, c)
-                cases[f"wgrad_w4c{c}"] = lambda c=c: ops.gemm_w4_ex(dy, x, g, True, True, False, c)
             for grp in a.groups:
                 cases[f"fwd_g{grp}"] = lambda grp=grp: ops.gemm64_ex(x, W, y, False, False, False, grp)
                 cases[f"dgrad_g{grp}"] = lambda grp=grp: ops.gemm64_ex(dy, W, dx, False, True, False, grp)
