@@ -20,11 +20,14 @@ and report what they applied.
 from __future__ import annotations
 
 import json
+import logging
 import os
 import re
 from collections import Counter
 from pathlib import Path
 from typing import Any, Dict, Optional
+
+log = logging.getLogger("llmctl.tuning_cache")
 
 _SHAPE = re.compile(r"(\d+)x(\d+)x(\d+)")
 
@@ -48,6 +51,7 @@ def knobs(cache: Dict[str, Dict[str, Any]]) -> Dict[str, Any]:
     out: Dict[str, Any] = {"gemm64": {}, "gemm64_shapes": {}, "skinny": {}, "bucket_mb": None, "fa_split": None,
                            "decode_splits": None}
     per_layout: Dict[str, Counter] = {}
+    scalar: Dict[str, set] = {}
     for k, cfg in cache.items():
         if k.startswith("gemm64_") and "config" in cfg:
             layout = k.split("_")[1]
@@ -60,12 +64,21 @@ def knobs(cache: Dict[str, Dict[str, Any]]) -> Dict[str, Any]:
             if m:
                 out["skinny"][tuple(int(x) for x in m.groups())] = int(cfg["config"])
         elif k.startswith("comm_") and cfg.get("bucket_mb"):
-            out["bucket_mb"] = float(cfg["bucket_mb"])
+            scalar.setdefault("bucket_mb", set()).add(float(cfg["bucket_mb"]))
         elif k.startswith("fa_split_") and "split" in cfg:
-            out["fa_split"] = int(cfg["split"])
+            scalar.setdefault("fa_split", set()).add(int(cfg["split"]))
         elif k.startswith("decode_splits_") and "splits" in cfg:
-            out["decode_splits"] = int(cfg["splits"])
+            scalar.setdefault("decode_splits", set()).add(int(cfg["splits"]))
     out["gemm64"] = {lay: c.most_common(1)[0][0] for lay, c in per_layout.items()}
+    # process-wide overrides (bucket size, attention / decode splits) only when every tuned shape
+    # agrees: a split tuned for one (N, ctx, Hkv) or (B, S, H, D) must not replace the adaptive
+    # per-grid rule for all the others
+    for name, vals in scalar.items():
+        if len(vals) == 1:
+            out[name] = next(iter(vals))
+        else:
+            log.info("tuning cache: %s differs across shapes %s; keeping the built-in per-shape rule",
+                     name, sorted(vals))
     return out
 
 
