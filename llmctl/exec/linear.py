@@ -159,6 +159,17 @@ def wgrad_into(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate:
     profiles/gemm64_variants_r2.jsonl; the 32-deep gemm_ex where K is not a multiple of 128);
     other shapes go to hipBLASLt."""
     M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
+    if g.dtype == torch.float32:  # fp32 main gradient: accumulate without a bf16 rounding
+        if (_gemm64_ok(M, N, K, dy2, x2) and g.is_cuda and g.stride(1) == 1 and g.stride(0) % 4 == 0
+                and g.data_ptr() % 16 == 0 and K * dy2.stride(0) * 2 < 2**31 and K * x2.stride(0) * 2 < 2**31):
+            from llmctl.ops._lib import native
+
+            native().gemm64_ex(dy2, x2, g, True, True, accumulate, gemm64_config("wgrad", M, N, K))
+        elif accumulate:
+            g.add_(dy2.t().matmul(x2))
+        else:
+            g.copy_(dy2.t().matmul(x2))
+        return
     if (_gemm64_ok(M, N, K, g, dy2, x2) and K * dy2.stride(0) * 2 < 2**31 and K * x2.stride(0) * 2 < 2**31):
         from llmctl.ops._lib import native
 
@@ -241,7 +252,9 @@ class GradSink:
         p._llmctl_fresh = True
 
     def write(self, p: torch.nn.Parameter, dy2: torch.Tensor, x2: torch.Tensor) -> None:
-        g = p.grad
+        g = getattr(p, "main_grad", None)
+        if g is None:
+            g = p.grad
         if g is None:
             raise RuntimeError("grad sink parameter has no flat .grad view")
         wgrad_into(g, dy2, x2, accumulate=not p._llmctl_fresh)

@@ -71,7 +71,11 @@ enum : int { A_LO = 0, A_HI = 1, B_H0 = 2, B_H1 = 3 };
 // F + [128 tn, ...) in its right half (the second B half-tile reads through its own buffer
 // resource); the up accumulators cross to the gate waves through LDS and only act = silu(g) * u
 // [M, F] is stored (C, ldc = F) — no gu tensor, no separate SwiGLU pass
-enum : int { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU_BWD = 2, EPI_SWIGLU_FWD = 3 };
+// EPI_STORE_F32 / EPI_ACC_F32 (fp32 main gradients, wgrad layout): C is fp32 (args.c reinterpreted
+// as float*, ldc in floats): the weight gradient is written / accumulated in fp32, never rounded
+// to bf16 between micro-steps
+enum : int { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU_BWD = 2, EPI_SWIGLU_FWD = 3, EPI_STORE_F32 = 4, EPI_ACC_F32 = 5 };
+constexpr bool epi_f32(int e) { return e == EPI_STORE_F32 || e == EPI_ACC_F32; }
 template <int V>
 using K_ = std::integral_constant<int, V>;
 
@@ -397,6 +401,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
       for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + 16 * j) = acc[i][j];
     return;
   }
+  if constexpr (epi_f32(EPI)) {
+    float* Cf = reinterpret_cast<float*>(args.c) + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 64 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4_t* p = reinterpret_cast<f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j);
+        if constexpr (EPI == EPI_ACC_F32) *p = *p + acc[i][j];
+        else *p = acc[i][j];
+      }
+    return;
+  }
   unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 64 + 4 * g;
   if constexpr (EPI == EPI_SWIGLU_BWD) {
     const unsigned short* Gb = args.aux + (Cb - args.c);
@@ -642,6 +658,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64p_kernel(G64Args args, int n_it
 
   bool first = true;
   for (;;) {
+    // this item's epilogue coordinates (the current item only; decoded before its K-loop)
+    const Item ep = first ? cur : decode_item<GROUP>(args, g);
+    const bool ep_split = ep.sp >= 0;
+    const long ep_off = ep_split ? ((long)ep.u * args.splits + ep.sp) * (TM * TN)
+                                 : (long)(ep.tm * TM) * args.ldc + ep.tn * TN;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -652,17 +673,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64p_kernel(G64Args args, int n_it
       ktile(t + 1, smem + BUF, false);
     }
     // ---- epilogue of the current item (lane: C[m = .. + (l&15)][n = .. + 4(l>>4) + r])
-    cur = decode_item<GROUP>(args, g);
     const int gq = lane >> 4, i16 = lane & 15;
-    if (cur.sp >= 0) {  // split item: fp32 partial tile, row-major 256 x 256
-      float* W = args.ws + ((long)cur.u * args.splits + cur.sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 64 + 4 * gq;
+    if (ep_split) {  // split item: fp32 partial tile, row-major 256 x 256
+      float* W = args.ws + ep_off + (wr * 128 + i16) * TN + wc * 64 + 4 * gq;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st_x4(W + (16 * i) * TN + 16 * j, acc[i][j]);
+    } else if constexpr (epi_f32(EPI)) {
+      float* Cf = reinterpret_cast<float*>(args.c) + ep_off + (long)(wr * 128 + i16) * args.ldc + wc * 64 + 4 * gq;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float* p = Cf + (long)(16 * i) * args.ldc + 16 * j;
+          if constexpr (EPI == EPI_ACC_F32) st_x4(p, *reinterpret_cast<const f32x4_t*>(p) + acc[i][j]);
+          else st_x4(p, acc[i][j]);
+        }
+      if constexpr (EPI == EPI_ACC_F32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-      unsigned short* Cb =
-          args.c + (long)(cur.tm * TM + wr * 128 + i16) * args.ldc + cur.tn * TN + wc * 64 + 4 * gq;
+      unsigned short* Cb = args.c + ep_off + (long)(wr * 128 + i16) * args.ldc + wc * 64 + 4 * gq;
       if constexpr (EPI == EPI_SWIGLU_BWD) {
         const unsigned short* Gb = args.aux + (Cb - args.c);
 #pragma unroll
@@ -765,6 +795,17 @@ __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
       v[4 + j] += x1[j];
     }
   }
+  if constexpr (epi_f32(EPI)) {
+    f32x4_t* pf = reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(args.c) + (long)(tm * TM + row) * args.ldc + tn * TN + col);
+    f32x4_t lo = {v[0], v[1], v[2], v[3]}, hi = {v[4], v[5], v[6], v[7]};
+    if constexpr (EPI == EPI_ACC_F32) {
+      lo += pf[0];
+      hi += pf[1];
+    }
+    pf[0] = lo;
+    pf[1] = hi;
+    return;
+  }
   unsigned short* p = args.c + (long)(tm * TM + row) * args.ldc + tn * TN + col;
   if constexpr (EPI == EPI_SWIGLU_BWD) {
     const unsigned short* gp = args.aux + (p - args.c);
@@ -797,12 +838,16 @@ void launch_g(const G64Args& g, int variant) {
       variant = -1;
     }
   }
-  switch (variant) {
-    case -1: break;
-    case 1: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g); break;
-    case 2: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 2>), grid, block, 0, stream(), g); break;
-    case 3: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 3>), grid, block, 0, stream(), g); break;
-    default: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 0>), grid, block, 0, stream(), g); break;
+  if constexpr (epi_f32(EPI)) {  // fp32 outputs: persistent or variant 1 only (fewer instantiations)
+    if (variant != -1) hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g);
+  } else {
+    switch (variant) {
+      case -1: break;
+      case 1: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g); break;
+      case 2: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 2>), grid, block, 0, stream(), g); break;
+      case 3: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 3>), grid, block, 0, stream(), g); break;
+      default: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 0>), grid, block, 0, stream(), g); break;
+    }
   }
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
   if (n_tail > 0)
@@ -866,8 +911,10 @@ bool gemm64_supported(long M, long N, long K) { return M % TM == 0 && N % TN == 
 void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool at_, bool bt_, bool accumulate,
                int64_t config) {
   LLMCTL_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm64_ex: 2-D operands");
+  const bool f32_out = out.scalar_type() == at::kFloat;
   LLMCTL_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
-                   out.scalar_type() == at::kBFloat16, "gemm64_ex: bf16 operands");
+                   (out.scalar_type() == at::kBFloat16 || (f32_out && at_ && bt_)),
+               "gemm64_ex: bf16 operands, bf16 output (fp32 output: wgrad layout only)");
   LLMCTL_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm64_ex: GPU tensors");
   LLMCTL_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1, "gemm64_ex: unit inner stride");
   const long M = at_ ? a.size(1) : a.size(0);
@@ -880,7 +927,7 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   LLMCTL_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 4 == 0 &&
                    (reinterpret_cast<uintptr_t>(a.data_ptr()) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(out.data_ptr()) & 7) == 0,
+                   (reinterpret_cast<uintptr_t>(out.data_ptr()) & (f32_out ? 15 : 7)) == 0,
                "gemm64_ex: 16-byte aligned operand rows");
   // 32-bit buffer offsets: the farthest byte any tile's DMA addresses from its tile origin
   const long a_span = at_ ? K * a.stride(0) * 2 : (long)TM * a.stride(0) * 2;
@@ -897,6 +944,12 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
     g.ws = ws.data_ptr<float>();
   }
   const int grp = (int)(config % 1000);
+  if (f32_out) {  // fp32 main gradients: the persistent or the variant-1 schedule only
+    const int c = (grp / 100) % 10 == 5 ? 500 + grp % 100 : 100 + grp % 100;
+    if (accumulate) launch<true, true, EPI_ACC_F32>(g, c);
+    else launch<true, true, EPI_STORE_F32>(g, c);
+    return;
+  }
   const int sel = (at_ ? 4 : 0) | (bt_ ? 2 : 0) | (accumulate ? 1 : 0);
   switch (sel) {
     case 0: launch<false, false, EPI_STORE>(g, grp); break;

@@ -152,7 +152,9 @@ class PipelineSchedule:
             return None
         opt = self.e.optimizer
         if opt.zero_stage == 0:
-            return p.grad
+            from llmctl.runtime.flat import grad_view
+
+            return grad_view(p)
         b = self.e.flat.param_bucket[id(p)]
         assert b.params == [p], "tied embedding copy must own its bucket"
         off, c = opt.shard_offsets[b.index]

@@ -77,6 +77,12 @@ class TrainingConfig:
     virtual_stages: int = 1  # interleaved pipeline: model chunks per pipeline rank (1 = plain 1F1B)
     tuning_cache: Optional[str] = None  # autotuner results to apply (else $LLMCTL_TUNING_CACHE)
     bucket_mb: float = 256.0
+    # gradient accumulation / reduction dtype: "fp32" keeps fp32 main gradients (GEMM epilogues
+    # accumulate in fp32, DP reductions in fp32; ~2x gradient memory and bucket bytes), "bf16"
+    # the parameter dtype; "auto" = fp32 whenever micro-batches accumulate (grad accumulation or
+    # pipeline micro-batches) with bf16 parameters, where repeated bf16 rounding of the running
+    # sum loses low-order gradient bits (Megatron's default for bf16)
+    main_grads: str = "auto"
     betas: Tuple[float, float] = (0.9, 0.95)
     eps: float = 1e-8
     device: str = "auto"
@@ -218,7 +224,9 @@ class TrainingEngine:
         self.pc = pc
         dp = pg.layout.dp
         align = 64 * max(dp, 1)
-        bucket_numel = int(c.bucket_mb * 2**20 / torch.tensor([], dtype=c.dtype).element_size())
+        grad_dtype = self._main_grad_dtype()
+        self.grad_dtype = grad_dtype
+        bucket_numel = int(c.bucket_mb * 2**20 / torch.tensor([], dtype=grad_dtype).element_size())
         self.grad_sink = None
         if c.zero_stage >= 3 and dp > 1:
             if pp > 1 and mc.tie_word_embeddings:
@@ -235,7 +243,8 @@ class TrainingEngine:
             if pg.layout.ep > 1:  # expert shards: their own flat buffer, reduced over expert-DP
                 named = [(n, p) for n, p in named if not getattr(p, "expert", False)]
             solo = ("embed", "lm_head") if (pp > 1 and mc.tie_word_embeddings) else ()
-            self.flat = FlatParameters(named, bucket_numel=bucket_numel, align=align, solo=solo)
+            self.flat = FlatParameters(named, bucket_numel=bucket_numel, align=align, solo=solo,
+                                       grad_dtype=grad_dtype)
             # GEMM-written weight gradients (no AccumulateGrad pass); tied embeddings excluded
             from llmctl.exec.linear import GradSink
 
@@ -290,6 +299,22 @@ class TrainingEngine:
         n_local = sum(p.numel() for p in self.model.parameters())
         log.info("rank %d: tp=%d pp=%d dp=%d zero=%d layers[%d:%d] local params %.3fB on %s",
                  self.rank, pg.layout.tp, pp, dp, c.zero_stage, lo, hi, n_local / 1e9, self.device)
+
+    def _main_grad_dtype(self) -> torch.dtype:
+        c = self.config
+        mode = (c.main_grads or "auto").lower()
+        if mode not in ("auto", "fp32", "bf16"):
+            raise ValueError(f"main_grads must be auto | fp32 | bf16, got {c.main_grads!r}")
+        if c.dtype == torch.float32 or mode == "bf16":
+            return c.dtype
+        accum = c.gradient_accumulation_steps > 1 or c.pipeline_parallel > 1
+        if mode == "auto" and not accum:
+            return c.dtype
+        if c.zero_stage >= 3:
+            if mode == "fp32":
+                log.warning("main_grads=fp32 is not implemented for ZeRO-3: gradients stay %s", c.dtype)
+            return c.dtype
+        return torch.float32
 
     def _install_param_gather_hooks(self) -> None:
         """ZeRO-1/2: the post-step all-gather of updated parameter shards overlaps the next

@@ -58,6 +58,21 @@ class Bucket:
         return self.region == "decay"
 
 
+def _fold_main_grad(p: nn.Parameter) -> None:
+    """Post-accumulate hook (fp32 main gradients): add the bf16 autograd gradient into the fp32
+    flat view and drop it.  Also runs, with ``p.grad`` None, for GEMM-written weights."""
+    g = p.grad
+    if g is not None:
+        p.main_grad.add_(g)
+        p.grad = None
+
+
+def grad_view(p: nn.Parameter) -> Optional[torch.Tensor]:
+    """The flat-buffer gradient of ``p``: its fp32 main gradient if it has one, else ``.grad``."""
+    g = getattr(p, "main_grad", None)
+    return g if g is not None else p.grad
+
+
 class FlatParameters:
     """Re-home ``named_params`` into flat buffers (in place: ``p.data`` becomes a view)."""
 
@@ -128,13 +143,26 @@ class FlatParameters:
         self.data = torch.zeros(self.numel, dtype=dtype, device=dev)
         self.grad = torch.zeros(self.numel, dtype=self.grad_dtype, device=dev) if allocate_grad else None
         self.params: List[nn.Parameter] = [p for _, p in named_params]
+        # fp32 main gradients (grad_dtype wider than the params): a parameter's ``.grad`` cannot
+        # be a view of a buffer of another dtype, so the flat fp32 view is ``p.main_grad``
+        # (Megatron's convention).  GEMM-written weights accumulate straight into it in fp32
+        # (llmctl.exec.linear.GradSink); autograd-produced grads (norms, embeddings) land in a
+        # transient bf16 ``p.grad`` that a post-accumulate hook folds in and drops — registered
+        # here, i.e. before the DP overlap engine's hooks, so a bucket launches after the fold.
+        self.main_grads = self.grad is not None and self.grad_dtype != dtype
         for n, p in named_params:
             off = self.offsets[id(p)]
             view = self.data[off:off + p.numel()].view_as(p)
             view.copy_(p.data)
             p.data = view
             if self.grad is not None:
-                p.grad = self.grad[off:off + p.numel()].view_as(p)
+                gv = self.grad[off:off + p.numel()].view_as(p)
+                if self.main_grads:
+                    p.main_grad = gv
+                    p.grad = None
+                    p.register_post_accumulate_grad_hook(_fold_main_grad)
+                else:
+                    p.grad = gv
 
     # ------------------------------------------------------------------ helpers
     def install_sinks(self, sink, predicate) -> int:
@@ -157,9 +185,13 @@ class FlatParameters:
             self.grad.zero_()
         for p in self.params:
             off = self.offsets[id(p)]
-            g = p.grad
-            if g is None or g.data_ptr() != self.grad[off:].data_ptr():
-                p.grad = g = self.grad[off:off + p.numel()].view_as(p)
+            if self.main_grads:
+                p.grad = None
+                g = p.main_grad
+            else:
+                g = p.grad
+                if g is None or g.data_ptr() != self.grad[off:].data_ptr():
+                    p.grad = g = self.grad[off:off + p.numel()].view_as(p)
             if sink is not None:
                 if getattr(p, "_llmctl_grad_sink", None) is sink:
                     sink.reset(p)

@@ -438,3 +438,26 @@ def train_layout_gpu(rank: int, world: int, steps: int, layout: dict, model: str
     ev = eng.evaluate([tuple(t.to(dev) for t in make_batch(vocab, cfg.seq_len, cfg.batch_size, 99, 0))])
     torch.cuda.synchronize()
     return {"losses": losses, "eval": ev, "native": bool(_lib.load()), "backend": eng.backend}
+
+
+def train_drift(rank: int, world: int, steps: int, main_grads: str, precision: str = "bf16") -> dict:
+    """DP=world x grad-accumulation 4 on the tiny model for ``steps`` steps with the given
+    parameter precision and gradient-accumulation dtype; returns the per-step mean losses and
+    the final parameters (fp32) on rank 0 — the fp32-main-gradient drift study."""
+    from llmctl.runtime.engine import TrainingEngine
+
+    cfg = _config(model_name_or_path="tiny", mixed_precision=precision, main_grads=main_grads,
+                  gradient_accumulation_steps=4, learning_rate=3e-3, scheduler="constant")
+    eng = TrainingEngine(cfg)
+    eng.load_full_state_dict(reference_state("tiny"))
+    losses = []
+    for s in range(steps):
+        out = eng.train_step([make_batch(512, cfg.seq_len, cfg.batch_size, s, eng.pg.dp_rank, i) for i in range(4)])
+        lt = out["loss"].detach().float().reshape(1).clone()
+        if eng.pg.dp_group is not None:
+            torch.distributed.all_reduce(lt, group=eng.pg.dp_group)
+            lt /= eng.pg.layout.dp
+        losses.append(float(lt))
+    state = {n: p.detach().float().clone() for n, p in eng.model.named_parameters()}
+    return {"losses": losses, "state": state if rank == 0 else None,
+            "grad_dtype": str(eng.grad_dtype), "flat_grad_dtype": str(eng.flat.grad.dtype)}

@@ -1,0 +1,79 @@
+"""fp32 main gradients (``TrainingConfig.main_grads``): GEMM-written weight gradients and the
+autograd ones accumulate across micro-steps in fp32 and are reduced over DP in fp32, instead of
+being rounded to bf16 after every micro-step (SURVEY §2.3 "Mixed precision"; the reference's
+accumulation + backward is ``llmctl/runtime/engine.py:284-289``)."""
+
+import torch
+
+from llmctl.testing.harness import run_ranks
+from llmctl.testing.workers import _config, make_batch, reference_state, train_drift
+
+STEPS = 50
+
+
+def _accumulated_grads(main_grads: str):
+    from llmctl.runtime.engine import TrainingEngine
+    from llmctl.runtime.flat import grad_view
+
+    cfg = _config(model_name_or_path="tiny", mixed_precision="bf16", main_grads=main_grads,
+                  gradient_accumulation_steps=8)
+    eng = TrainingEngine(cfg)
+    eng.load_full_state_dict(reference_state("tiny"))
+    eng.flat.zero_grad()
+    n = 8
+    for i in range(n):
+        x, y = make_batch(512, cfg.seq_len, cfg.batch_size, 0, 0, i)
+        with eng.sync.no_sync() if i < n - 1 else _Null():
+            eng.model(x, y, loss_denom=float(y.numel() * n)).backward()
+    eng.sync.finish()
+    return eng, {eng.flat.names[id(p)]: grad_view(p).detach().float().clone() for p in eng.flat.params}
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def test_fp32_main_grads_accumulate_exactly():
+    """8 micro-steps: the fp32 main gradient equals the fp32 sum of the per-micro-step bf16-model
+    gradients far more closely than the bf16 running sum does."""
+    eng32, g32 = _accumulated_grads("fp32")
+    assert eng32.flat.grad.dtype == torch.float32 and eng32.flat.main_grads
+    eng16, g16 = _accumulated_grads("bf16")
+    assert eng16.flat.grad.dtype == torch.bfloat16
+    # exact reference: the same micro-steps, each gradient taken alone (fp32 copy), summed in fp64
+    from llmctl.runtime.engine import TrainingEngine
+    from llmctl.runtime.flat import grad_view
+
+    cfg = _config(model_name_or_path="tiny", mixed_precision="bf16", main_grads="fp32", gradient_accumulation_steps=8)
+    eng = TrainingEngine(cfg)
+    eng.load_full_state_dict(reference_state("tiny"))
+    exact = {k: torch.zeros_like(v, dtype=torch.float64) for k, v in g32.items()}
+    for i in range(8):
+        eng.flat.zero_grad()
+        x, y = make_batch(512, cfg.seq_len, cfg.batch_size, 0, 0, i)
+        with eng.sync.no_sync():
+            eng.model(x, y, loss_denom=float(y.numel() * 8)).backward()
+        for p in eng.flat.params:
+            exact[eng.flat.names[id(p)]] += grad_view(p).double()
+    err32 = max(((g32[k].double() - exact[k]).abs().max() / exact[k].abs().max().clamp_min(1e-30)).item() for k in exact)
+    err16 = max(((g16[k].double() - exact[k]).abs().max() / exact[k].abs().max().clamp_min(1e-30)).item() for k in exact)
+    assert err32 < 1e-5, err32
+    assert err16 > 10 * err32, (err16, err32)
+
+
+def test_dp4_accum4_fp32_main_grads_drift():
+    """DP4 x accumulation 4, 50 steps, bf16 parameters: the loss trajectory with fp32 main
+    gradients stays at least as close to the all-fp32 run as the bf16-gradient one (bounded
+    drift); recorded in profiles/main_grads_drift_r3.txt."""
+    ref = run_ranks(train_drift, 4, STEPS, "bf16", "fp32", timeout=900)[0]
+    f32 = run_ranks(train_drift, 4, STEPS, "fp32", "bf16", timeout=900)[0]
+    b16 = run_ranks(train_drift, 4, STEPS, "bf16", "bf16", timeout=900)[0]
+    assert f32["flat_grad_dtype"] == "torch.float32" and b16["flat_grad_dtype"] == "torch.bfloat16"
+    d32 = max(abs(a - b) for a, b in zip(f32["losses"], ref["losses"]))
+    d16 = max(abs(a - b) for a, b in zip(b16["losses"], ref["losses"]))
+    assert d32 < 0.05, (d32, d16)
+    assert d32 <= d16 * 1.25 + 2e-3, (d32, d16)

@@ -172,3 +172,20 @@ def test_swiglu_down_autograd_fused_matches_unfused(native_lib):
         out.backward(dy)
         assert row_err(out, ref_out.detach()) < 2e-2
         assert row_err(gu.grad, g32.grad) < 2e-2 and row_err(w.grad, w32.grad) < 2e-2
+
+
+@pytest.mark.parametrize("cfg", [104, 504, 2104, 2504, 1504])
+def test_gemm64_wgrad_fp32_output(native_lib, cfg):
+    """fp32 main gradients: the wgrad layout stores / accumulates an fp32 C (no bf16 rounding of
+    the running sum); one-shot and persistent schedules, with and without the split tail."""
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    M, N, K = 256 * (n_cu // 8 + 1), 256 * 8, 1024
+    A, B = _bf(K, M, seed=31), _bf(K, N, seed=32)
+    want = A.float().t() @ B.float()
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.float32)
+    native_lib.gemm64_ex(A, B, out, True, True, False, cfg)
+    assert (out - want).abs().max().item() < 2e-3 * want.abs().max().item()
+    c0 = torch.randn(M, N, device=DEV)
+    out = c0.clone()
+    native_lib.gemm64_ex(A, B, out, True, True, True, cfg)
+    assert (out - (want + c0)).abs().max().item() < 2e-3 * want.abs().max().item()
