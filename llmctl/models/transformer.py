@@ -113,6 +113,105 @@ class _SwiGLUDown(torch.autograd.Function):
         return dgu, dw, None
 
 
+def _fused_fwd_enabled() -> bool:
+    """Training-forward GEMMs with fused epilogues (gemm64 ``EPI_ROPE_QKV`` / ``EPI_UP_SWIGLU``);
+    ``LLMCTL_FUSED_FWD=0`` keeps the hipBLASLt projection + separate RoPE / SwiGLU passes (A/B)."""
+    return os.environ.get("LLMCTL_FUSED_FWD", "1") != "0"
+
+
+def _gemm64_rows(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    from llmctl.exec.linear import _gemm64_enabled, _rows_ok
+    from llmctl.ops._lib import use_native
+
+    T, K = x2.shape
+    return (_gemm64_enabled() and x2.is_cuda and use_native(x2) and x2.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.is_contiguous() and T % 256 == 0 and K % 128 == 0
+            and _rows_ok(x2) and 256 * x2.stride(0) * 2 < 2**31)
+
+
+def _prep_weight_t(w: nn.Parameter, tokens: int) -> None:
+    """Start the side-stream W^T refresh now (forward) if this weight's data gradient will not
+    run on gemm64 — as ``_Linear.forward`` does."""
+    from llmctl.exec.linear import dgrad64_shape_ok
+
+    sink = getattr(w, "_llmctl_grad_sink", None)
+    if sink is not None and not dgrad64_shape_ok(tokens, w):
+        sink.weight_t(w)
+
+
+class _QKVRopeAttention(torch.autograd.Function):
+    """QKV projection + RoPE + causal flash attention with the RoPE and the head split in the
+    projection GEMM's epilogue (``gemm64_qkv_rope``: no qkv tensor, no rope_qkv_fwd pass) and,
+    in backward, the RoPE backward in the attention backward's stores (``flash_attn_bwd_qkv``
+    writes d(qkv) directly), followed by the projection's weight gradient (grad sink) and data
+    gradient.  Replaces ``linear(x, wqkv)`` + ``ops.rope_flash_attention`` — reference step
+    ``llmctl/runtime/engine.py:283-300``."""
+
+    @staticmethod
+    def forward(ctx, x, w, cos, sin, nq, nkv, B, S, positions, doc_start):
+        from llmctl.exec.linear import gemm64_config
+        from llmctl.ops._lib import native
+
+        x2 = x.reshape(-1, x.shape[-1])
+        T = x2.shape[0]
+        pos = positions.reshape(-1).int().contiguous() if positions is not None else None
+        q, k, v = native().gemm64_qkv_rope(x2, w, cos, sin, pos, nq, nkv, S,
+                                           gemm64_config("fwd", T, w.shape[0], x2.shape[1]) % 1000)
+        if ctx.needs_input_grad[0]:
+            _prep_weight_t(w, T)
+        D = 128
+        q, k, v = q.view(B, S, nq, D), k.view(B, S, nkv, D), v.view(B, S, nkv, D)
+        scale = D ** -0.5
+        o, lse = native().flash_attn_fwd(q, k, v, scale, True, doc_start)
+        ctx.save_for_backward(x2, q, k, v, o, lse, cos, sin, pos if pos is not None else torch.empty(0))
+        ctx.wparam, ctx.has_pos, ctx.S, ctx.scale, ctx.doc_start = w, pos is not None, S, scale, doc_start
+        ctx.xshape = x.shape
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        from llmctl.ops._lib import native
+
+        x2, q, k, v, o, lse, cos, sin, pos = ctx.saved_tensors
+        dqkv = native().flash_attn_bwd_qkv(do.contiguous(), q, k, v, o, lse, ctx.scale, True, ctx.doc_start, cos,
+                                           sin, pos if ctx.has_pos else None, ctx.S)
+        dw = weight_grad(ctx.wparam, dqkv, x2) if ctx.needs_input_grad[1] else None
+        dx = data_grad(dqkv, ctx.wparam).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        return dx, dw, None, None, None, None, None, None, None, None
+
+
+class _UpSwiGLUDown(torch.autograd.Function):
+    """Gate/up projection with SwiGLU in its epilogue (``gemm64_up_swiglu`` stores gu for the
+    backward and act for the down projection: no swiglu_fwd pass) + the down projection; the
+    backward is ``_SwiGLUDown``'s (SwiGLU backward in the down data-gradient epilogue) followed by
+    the up projection's weight / data gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w_up, w_down):
+        from llmctl.exec.linear import forward_linear, gemm64_config
+        from llmctl.ops._lib import native
+
+        x2 = x.reshape(-1, x.shape[-1])
+        T = x2.shape[0]
+        gu, act = native().gemm64_up_swiglu(x2, w_up, gemm64_config("fwd", T, w_up.shape[0], x2.shape[1]) % 1000)
+        out = forward_linear(act, w_down)
+        if ctx.needs_input_grad[0]:
+            _prep_weight_t(w_up, T)
+        ctx.save_for_backward(x2, gu, act)
+        ctx.w_up, ctx.w_down, ctx.xshape = w_up, w_down, x.shape
+        return out.view(*x.shape[:-1], w_down.shape[0])
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, gu, act = ctx.saved_tensors
+        dout2 = dout.reshape(-1, dout.shape[-1])
+        dw_down = weight_grad(ctx.w_down, dout2, act)
+        dgu = swiglu_data_grad(dout2, ctx.w_down, gu)
+        dw_up = weight_grad(ctx.w_up, dgu, x2) if ctx.needs_input_grad[1] else None
+        dx = data_grad(dgu, ctx.w_up).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        return dx, dw_up, dw_down
+
+
 class DecoderLayer(nn.Module):
     def __init__(self, cfg: ModelConfig, pc: ParallelContext, layer_idx: int, device=None, dtype=None):
         super().__init__()
@@ -189,7 +288,18 @@ class DecoderLayer(nn.Module):
     def _async_sp(self) -> bool:
         return self.pc.tp_size > 1 and self.pc.sequence_parallel and async_tp.enabled()
 
+    def _fused_qkv_ok(self, x, rope) -> bool:
+        if not (_fused_fwd_enabled() and rope is not None and self.bqkv is None and self.D == 128
+                and self.nq % 2 == 0 and self.nkv % 2 == 0 and self.pc.cp_size == 1 and not self._async_sp()
+                and torch.is_grad_enabled() and os.environ.get("LLMCTL_FUSED_ROPE_ATTN", "1") != "0"):
+            return False
+        return _gemm64_rows(x.reshape(-1, x.shape[-1]), self.wqkv) and rope[0].shape[-1] == 64
+
     def attention(self, xn, B, S, rope, positions=None, doc_start=None):
+        if self._fused_qkv_ok(xn, rope):
+            x = self._col_in(xn)
+            o = _QKVRopeAttention.apply(x, self.wqkv, rope[0], rope[1], self.nq, self.nkv, B, S, positions, doc_start)
+            return self._attn_out(o, B, S)
         if self._async_sp():  # SP all-gather overlapped with the QKV GEMM
             qkv = async_tp.column_parallel_sp(xn, self.wqkv, self.bqkv, self.pc.tp_group)
         else:
@@ -238,7 +348,11 @@ class DecoderLayer(nn.Module):
             out = async_tp.row_parallel_sp(h, self.w_down, g)
         else:
             x = self._col_in(xn)
-            if self.cfg.gated_mlp:
+            if (self.cfg.gated_mlp and _fused_fwd_enabled() and self.b_up is None and torch.is_grad_enabled()
+                    and self.pc.activation_checkpoint != "selective" and self.w_up.shape[0] % 256 == 0
+                    and _gemm64_rows(x.reshape(-1, x.shape[-1]), self.w_up)):
+                out = _UpSwiGLUDown.apply(x, self.w_up, self.w_down)
+            elif self.cfg.gated_mlp:
                 gu = linear(x, self.w_up, self.b_up)
                 out = _SwiGLUDown.apply(gu, self.w_down, self.pc.activation_checkpoint == "selective")
             else:

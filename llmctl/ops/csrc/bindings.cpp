@@ -68,5 +68,7 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("gemm64_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int config=4) -> ()");
   m.def("gemm64_swiglu_fwd(Tensor x, Tensor w, int config) -> Tensor");
   m.def("gemm64_swiglu_dgrad(Tensor dy, Tensor w, Tensor gu, int config=104) -> Tensor");
+  m.def("gemm64_qkv_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, Tensor? pos, int nq, int nkv, int seq, int config=104) -> (Tensor, Tensor, Tensor)");
+  m.def("gemm64_up_swiglu(Tensor x, Tensor w, int config=104) -> (Tensor, Tensor)");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
 }

@@ -74,7 +74,21 @@ enum : int { A_LO = 0, A_HI = 1, B_H0 = 2, B_H1 = 3 };
 // EPI_STORE_F32 / EPI_ACC_F32 (fp32 main gradients, wgrad layout): C is fp32 (args.c reinterpreted
 // as float*, ldc in floats): the weight gradient is written / accumulated in fp32, never rounded
 // to bf16 between micro-steps
-enum : int { EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU_BWD = 2, EPI_SWIGLU_FWD = 3, EPI_STORE_F32 = 4, EPI_ACC_F32 = 5 };
+// Fused training-forward epilogues (one-shot kernel; B fragment slots remapped so each wave owns
+// both columns of every pair it combines — no cross-wave exchange):
+// EPI_ROPE_QKV: QKV projection (D = 128: a 256-column tile = 2 heads).  Wave wc owns head
+//   (wc >> 1)'s dims (wc & 1) * 32 + [0, 32) and the same + 64, i.e. both halves of its rotation
+//   pairs; the epilogue rounds to bf16, applies RoPE to q / k heads (cos / sin tables [P][64],
+//   position = pos[t] or t % seq) and stores q [T, nq, D], k / v [T, nkv, D] separately — the
+//   rope_qkv_fwd pass and its re-read of qkv disappear.
+// EPI_UP_SWIGLU: gate/up projection with the gate rows 128 tn.. (B_h0) and the matching up rows
+//   F + 128 tn.. (B_h1, as EPI_SWIGLU_FWD) in one tile; wave wc owns gate cols wc * 32 + [0, 32)
+//   and the same up cols; stores gu [T, 2F] (kept for the backward) AND act = silu(g) * u [T, F]
+//   — the swiglu_fwd pass and its re-read of gu disappear.
+enum : int {
+  EPI_STORE = 0, EPI_ACC = 1, EPI_SWIGLU_BWD = 2, EPI_SWIGLU_FWD = 3, EPI_STORE_F32 = 4, EPI_ACC_F32 = 5,
+  EPI_ROPE_QKV = 6, EPI_UP_SWIGLU = 7
+};
 constexpr bool epi_f32(int e) { return e == EPI_STORE_F32 || e == EPI_ACC_F32; }
 template <int V>
 using K_ = std::integral_constant<int, V>;
@@ -91,6 +105,13 @@ struct G64Args {
   int kt_part;  // K-tiles per split item (even)
   float* ws;    // [n_tail][splits][256][256] fp32 partials
   const unsigned short* aux;  // EPI_SWIGLU_BWD: gu [M, 2N], leading dimension ldc
+  // fused forward epilogues
+  unsigned short* out2 = nullptr;  // EPI_ROPE_QKV: k; EPI_UP_SWIGLU: act [M, N]
+  unsigned short* out3 = nullptr;  // EPI_ROPE_QKV: v
+  const float* cosT = nullptr;     // EPI_ROPE_QKV: [P][64] tables
+  const float* sinT = nullptr;
+  const int* pos = nullptr;        // EPI_ROPE_QKV: int32 position per token (nullptr: t % seq)
+  int nq = 0, nkv = 0, seq = 1;
 };
 
 // SwiGLU backward of one element: d = dL/dact, act = silu(g) * u
@@ -216,12 +237,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 
   const long lda = args.lda, ldb = args.ldb;
   const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
-  const unsigned short* Bb = EPI == EPI_SWIGLU_FWD ? args.b + (long)tn * (TN / 2) * ldb
+  constexpr bool PAIRED_B = EPI == EPI_SWIGLU_FWD || EPI == EPI_UP_SWIGLU;  // gate + up rows per tile
+  const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
                              : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
   const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
   // EPI_SWIGLU_FWD: B_H1 image rows 128 + ip -> up row N + 128 tn + ip (N = F)
-  const i32x4_t rb_hi = EPI == EPI_SWIGLU_FWD ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb)
-                                              : rb;
+  const i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
   // byte step of one K-tile in each operand
   const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
   const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
@@ -275,6 +296,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   const int ap = wr * 64;              // this wave's first image row/col in an A half-tile
   const int bh = (wc >> 1) * HALF;     // this wave's B half-tile
   const int bp = (wc & 1) * 64;        // ... and its first position in it
+  // B fragment slot j -> (half-tile byte offset, first image position): plain 16-column blocks, or
+  // the paired maps of the fused epilogues (slot j + 2 holds the partner columns of slot j)
+  auto bhalf = [&](int j) { return EPI == EPI_UP_SWIGLU ? (j >> 1) * HALF : bh; };
+  auto bpos = [&](int j) {
+    if constexpr (EPI == EPI_ROPE_QKV) return (wc & 1) * 32 + (j & 1) * 16 + (j >> 1) * 64;
+    else if constexpr (EPI == EPI_UP_SWIGLU) return wc * 32 + (j & 1) * 16;
+    else return bp + 16 * j;
+  };
   bf16x8_t af[4][2], bfr[4][2];
 
   // V bits (A/B'd by tools/gemm64_bench.py): 1 = issue the phase's DMA in the read section
@@ -306,7 +335,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bhalf(j), bpos(j), ks, lane);
     if constexpr (EARLY) issue(K_<B_H1>{}, t + 1);
     bar();
     if constexpr (!EARLY) issue(K_<B_H1>{}, t + 1);
@@ -316,7 +345,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 #pragma unroll
     for (int j = 2; j < 4; ++j)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bhalf(j), bpos(j), ks, lane);
     if constexpr (EARLY) {
       issue(K_<A_HI>{}, t + 1);
       wait_vm<8>();
@@ -361,6 +390,92 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 
   // ---- epilogue: lane holds C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3
   const int g = lane >> 4, i16 = lane & 15;
+  if constexpr (EPI == EPI_ROPE_QKV) {
+    // slot j (j = 0, 1) holds dims d = (wc & 1) * 32 + 16 j + 4 g + r of head h, slot j + 2 dims d + 64
+    const int h = 2 * tn + (wc >> 1);
+    const int nrot = args.nq + args.nkv;  // heads [0, nrot) rotate
+    unsigned short* dst0;
+    long dst_ld;
+    if (h < args.nq) {
+      dst0 = args.c + (long)h * 128;
+      dst_ld = (long)args.nq * 128;
+    } else if (h < nrot) {
+      dst0 = args.out2 + (long)(h - args.nq) * 128;
+      dst_ld = (long)args.nkv * 128;
+    } else {
+      dst0 = args.out3 + (long)(h - nrot) * 128;
+      dst_ld = (long)args.nkv * 128;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = tm * TM + wr * 128 + 16 * i + i16;
+      unsigned short* drow = dst0 + (long)t * dst_ld;
+      const long p = args.pos ? (long)args.pos[t] : (long)(t % args.seq);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int d = (wc & 1) * 32 + 16 * j + 4 * g;
+        float o1[4], o2[4];
+        if (h < nrot) {  // as rope_fwd_kernel on the bf16-stored projection
+          const f32x4_t cs = *reinterpret_cast<const f32x4_t*>(args.cosT + p * 64 + d);
+          const f32x4_t sn = *reinterpret_cast<const f32x4_t*>(args.sinT + p * 64 + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = bf2f(f2bf(acc[i][j][e])), b = bf2f(f2bf(acc[i][j + 2][e]));
+            o1[e] = a * cs[e] - b * sn[e];
+            o2[e] = b * cs[e] + a * sn[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o1[e] = acc[i][j][e];
+            o2[e] = acc[i][j + 2][e];
+          }
+        }
+        s2_t a1, a2;
+        a1[0] = (unsigned)f2bf(o1[0]) | ((unsigned)f2bf(o1[1]) << 16);
+        a1[1] = (unsigned)f2bf(o1[2]) | ((unsigned)f2bf(o1[3]) << 16);
+        a2[0] = (unsigned)f2bf(o2[0]) | ((unsigned)f2bf(o2[1]) << 16);
+        a2[1] = (unsigned)f2bf(o2[2]) | ((unsigned)f2bf(o2[3]) << 16);
+        *reinterpret_cast<s2_t*>(drow + d) = a1;
+        *reinterpret_cast<s2_t*>(drow + 64 + d) = a2;
+      }
+    }
+    return;
+  }
+  if constexpr (EPI == EPI_UP_SWIGLU) {
+    // slot j (j = 0, 1): gate cols 128 tn + wc * 32 + 16 j + 4 g + r; slot j + 2: the same up cols
+    const long F = args.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long t = (long)tm * TM + wr * 128 + 16 * i + i16;
+      unsigned short* gurow = args.c + t * args.ldc;
+      unsigned short* arow = args.out2 + t * F;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = tn * 128 + wc * 32 + 16 * j + 4 * g;
+        float o[4];
+        s2_t pg, pu, pa;
+        unsigned short gb[4], ub[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // as swiglu_fwd_kernel on the bf16-stored g / u
+          gb[e] = f2bf(acc[i][j][e]);
+          ub[e] = f2bf(acc[i][j + 2][e]);
+          const float gg = bf2f(gb[e]), uu = bf2f(ub[e]);
+          o[e] = gg * (1.f / (1.f + __expf(-gg))) * uu;
+        }
+        pg[0] = (unsigned)gb[0] | ((unsigned)gb[1] << 16);
+        pg[1] = (unsigned)gb[2] | ((unsigned)gb[3] << 16);
+        pu[0] = (unsigned)ub[0] | ((unsigned)ub[1] << 16);
+        pu[1] = (unsigned)ub[2] | ((unsigned)ub[3] << 16);
+        pa[0] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+        pa[1] = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+        *reinterpret_cast<s2_t*>(gurow + col) = pg;
+        *reinterpret_cast<s2_t*>(gurow + F + col) = pu;
+        *reinterpret_cast<s2_t*>(arow + col) = pa;
+      }
+    }
+    return;
+  }
   if constexpr (EPI == EPI_SWIGLU_FWD) {
     // up waves (wc 2, 3) hand their tiles to the gate waves (wc 0, 1) with the same (wr, i, j, lane)
     // through the now idle 128-KB LDS image: [wr][wc & 1][i][j][lane] f32x4
@@ -516,13 +631,17 @@ constexpr int EPI_OPS = 32;  // vector-memory ops per thread of a store-only epi
 __device__ __forceinline__ void st_x2(unsigned short* p, s2_t v) {
   asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
+// a store of more than 64 bits of data needs wait states before a VALU write of its data VGPRs
+// (hipcc pads only its own stores): the trailing s_nop covers the accumulator re-zeroing that
+// follows the epilogue
 __device__ __forceinline__ void st_x4(float* p, f32x4_t v) {
-  asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 template <bool AT, bool BT, int EPI, int GROUP>
 __global__ __launch_bounds__(NTHR, 1) void gemm64p_kernel(G64Args args, int n_items) {
-  static_assert(EPI != EPI_SWIGLU_FWD, "the pairing epilogue exchanges through LDS: one-shot kernel only");
+  static_assert(EPI != EPI_SWIGLU_FWD && EPI != EPI_ROPE_QKV && EPI != EPI_UP_SWIGLU,
+                "paired-column epilogues: one-shot kernel only");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -831,14 +950,16 @@ template <bool AT, bool BT, int EPI, int GROUP>
 void launch_g(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
   const dim3 grid(n_items), block(NTHR);
-  if constexpr (EPI != EPI_SWIGLU_FWD) {
+  constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
+  if constexpr (!fused_fwd) {
     if (variant == 5) {  // persistent: one workgroup per CU walks the items
       const dim3 pgrid(min(n_items, num_cus()));
       hipLaunchKernelGGL((gemm64p_kernel<AT, BT, EPI, GROUP>), pgrid, block, 0, stream(), g, n_items);
       variant = -1;
     }
   }
-  if constexpr (epi_f32(EPI)) {  // fp32 outputs: persistent or variant 1 only (fewer instantiations)
+  if constexpr (epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU) {
+    // fp32 outputs / fused training epilogues: variant 1 (or persistent) only (fewer instantiations)
     if (variant != -1) hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g);
   } else {
     switch (variant) {
@@ -1025,7 +1146,80 @@ at::Tensor gemm64_swiglu_fwd(const at::Tensor& x, const at::Tensor& w, int64_t c
   return act;
 }
 
+// QKV projection with RoPE + head split in the epilogue (training forward): x [T, K] (T % 256),
+// w [(nq + 2 nkv) * 128, K], cos / sin [P][64] fp32, pos int32 [T] or empty (t % seq).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm64_qkv_rope(const at::Tensor& x, const at::Tensor& w,
+                                                               const at::Tensor& cosT, const at::Tensor& sinT,
+                                                               const c10::optional<at::Tensor>& pos, int64_t nq,
+                                                               int64_t nkv, int64_t seq, int64_t config) {
+  LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                   x.is_cuda() && w.is_cuda() && x.stride(1) == 1 && w.is_contiguous(),
+               "gemm64_qkv_rope: bf16 GPU x [T, K] (unit inner stride), contiguous W [(nq+2nkv)*128, K]");
+  const long T = x.size(0), K = x.size(1), N = w.size(0);
+  LLMCTL_CHECK(w.size(1) == K && N == (nq + 2 * nkv) * 128 && nq % 2 == 0 && nkv % 2 == 0,
+               "gemm64_qkv_rope: head_dim 128, even head counts, W [(nq+2nkv)*128, K]");
+  LLMCTL_CHECK(T % TM == 0 && K % (2 * TK) == 0 && K > 0, "gemm64_qkv_rope: T % 256, K % 128 (got ", T, "x", K, ")");
+  LLMCTL_CHECK(cosT.scalar_type() == at::kFloat && sinT.scalar_type() == at::kFloat && cosT.is_contiguous() &&
+                   sinT.is_contiguous() && cosT.dim() == 2 && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes(),
+               "gemm64_qkv_rope: fp32 cos/sin tables [P][64]");
+  LLMCTL_CHECK(x.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+                   (long)TM * x.stride(0) * 2 < (1L << 31) && (long)TN * K * 2 < (1L << 31),
+               "gemm64_qkv_rope: 16-byte aligned rows / 32-bit offsets");
+  const bool has_pos = pos.has_value() && pos->defined() && pos->numel() > 0;
+  if (has_pos) {
+    LLMCTL_CHECK(pos->scalar_type() == at::kInt && pos->is_contiguous() && pos->numel() == T,
+                 "gemm64_qkv_rope: int32 positions [T]");
+  } else {
+    LLMCTL_CHECK(cosT.size(0) >= seq, "gemm64_qkv_rope: tables shorter than seq");
+  }
+  const c10::DeviceGuard dg(x.device());
+  auto q = at::empty({T, nq, 128}, x.options());
+  auto k = at::empty({T, nkv, 128}, x.options());
+  auto v = at::empty({T, nkv, 128}, x.options());
+  G64Args g{reinterpret_cast<const unsigned short*>(x.data_ptr()), reinterpret_cast<const unsigned short*>(w.data_ptr()),
+            reinterpret_cast<unsigned short*>(q.data_ptr()), x.stride(0), K, 0,
+            (int)T, (int)N, (int)K, (int)(T / TM), (int)(N / TN), 0, 1, 0, nullptr, nullptr};
+  g.out2 = reinterpret_cast<unsigned short*>(k.data_ptr());
+  g.out3 = reinterpret_cast<unsigned short*>(v.data_ptr());
+  g.cosT = cosT.data_ptr<float>();
+  g.sinT = sinT.data_ptr<float>();
+  g.pos = has_pos ? pos->data_ptr<int>() : nullptr;
+  g.nq = (int)nq;
+  g.nkv = (int)nkv;
+  g.seq = (int)std::max<int64_t>(seq, 1);
+  plan_split(g, 1);  // whole tiles (the epilogue needs the full K sum)
+  launch<false, false, EPI_ROPE_QKV>(g, (int)(config % 1000));
+  return {q, k, v};
+}
+
+// Gate/up projection storing gu [T, 2F] and act = silu(g) * u [T, F] (training forward).
+std::tuple<at::Tensor, at::Tensor> gemm64_up_swiglu(const at::Tensor& x, const at::Tensor& w, int64_t config) {
+  LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                   x.is_cuda() && w.is_cuda() && x.stride(1) == 1 && w.is_contiguous(),
+               "gemm64_up_swiglu: bf16 GPU x [T, K] (unit inner stride), contiguous W_up [2F, K]");
+  const long T = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  LLMCTL_CHECK(w.size(1) == K && w.size(0) == 2 * F, "gemm64_up_swiglu: W_up must be [2F, K]");
+  LLMCTL_CHECK(T % TM == 0 && F % (TN / 2) == 0 && K % (2 * TK) == 0 && K > 0,
+               "gemm64_up_swiglu: T % 256, F % 128, K % 128 (got ", T, "x", F, "x", K, ")");
+  LLMCTL_CHECK(x.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+                   (long)TM * x.stride(0) * 2 < (1L << 31) && (long)TN * K * 2 < (1L << 31) &&
+                   (2 * F) * K * 2 < (1L << 31),
+               "gemm64_up_swiglu: 16-byte aligned rows / 32-bit offsets");
+  const c10::DeviceGuard dg(x.device());
+  auto gu = at::empty({T, 2 * F}, x.options());
+  auto act = at::empty({T, F}, x.options());
+  G64Args g{reinterpret_cast<const unsigned short*>(x.data_ptr()), reinterpret_cast<const unsigned short*>(w.data_ptr()),
+            reinterpret_cast<unsigned short*>(gu.data_ptr()), x.stride(0), K, 2 * F,
+            (int)T, (int)F, (int)K, (int)(T / TM), (int)(F / (TN / 2)), 0, 1, 0, nullptr, nullptr};
+  g.out2 = reinterpret_cast<unsigned short*>(act.data_ptr());
+  plan_split(g, 1);
+  launch<false, false, EPI_UP_SWIGLU>(g, (int)(config % 1000));
+  return {gu, act};
+}
+
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("gemm64_qkv_rope", &gemm64_qkv_rope);
+  m.impl("gemm64_up_swiglu", &gemm64_up_swiglu);
   m.impl("gemm64_swiglu_fwd", &gemm64_swiglu_fwd);
   m.impl("gemm64_ex", &gemm64_ex);
   m.impl("gemm64_swiglu_dgrad", &gemm64_swiglu_dgrad);
