@@ -69,6 +69,13 @@ class CustomAllReduce:
         self.ops.car_allreduce(x, out, self.data_ptrs, self.sig_ptrs, self.rank, self.world, self.max_bytes)
         return out
 
+    def all_reduce_add_rmsnorm(self, part: torch.Tensor, bias: Optional[torch.Tensor], res: torch.Tensor,
+                               norm_w: torch.Tensor, eps: float):
+        """(rmsnorm(res + sum(part) + bias) * norm_w, res + sum(part) + bias) in one kernel: the TP
+        decode layer's row-parallel reduction fused with the next norm (``part`` [M, N] bf16)."""
+        return self.ops.car_allreduce_add_rmsnorm(part, bias, res.contiguous(), norm_w, float(eps), self.data_ptrs,
+                                                  self.sig_ptrs, self.rank, self.world, self.max_bytes)
+
     def check(self) -> None:
         if self.ops.car_error(self._sig):
             raise RuntimeError("custom all-reduce: a peer did not signal (timeout)")

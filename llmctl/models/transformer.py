@@ -114,9 +114,12 @@ class _SwiGLUDown(torch.autograd.Function):
 
 
 def _fused_fwd_enabled() -> bool:
-    """Training-forward GEMMs with fused epilogues (gemm64 ``EPI_ROPE_QKV`` / ``EPI_UP_SWIGLU``);
-    ``LLMCTL_FUSED_FWD=0`` keeps the hipBLASLt projection + separate RoPE / SwiGLU passes (A/B)."""
-    return os.environ.get("LLMCTL_FUSED_FWD", "1") != "0"
+    """Training-forward GEMMs with fused epilogues (gemm64 ``EPI_ROPE_QKV`` / ``EPI_UP_SWIGLU``)
+    when ``LLMCTL_FUSED_FWD=1``.  Off by default: on the GPT-7B step the saved RoPE / SwiGLU passes
+    (~0.45 ms per layer) are outweighed by gemm64's forward running 4-7 % below hipBLASLt's tuned
+    forward kernels (1474-1477 vs 1543-1588 TF on the QKV / gate-up shapes): 842 / 845 ms per step
+    fused vs 837 / 839 ms unfused, same box (profiles/fused_fwd_ab_r3.txt)."""
+    return os.environ.get("LLMCTL_FUSED_FWD", "0") == "1"
 
 
 def _gemm64_rows(x2: torch.Tensor, w: torch.Tensor) -> bool:

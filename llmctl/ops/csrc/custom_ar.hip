@@ -39,21 +39,8 @@ struct CarArgs {
   long half_elems;  // elements per epoch-parity half of a data buffer
 };
 
-__global__ __launch_bounds__(256) void car_oneshot_kernel(CarArgs a) {
-  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
-  unsigned* my_sig = reinterpret_cast<unsigned*>(a.sig[a.rank]);
-  __shared__ unsigned s_epoch;
-  if (tid == 0) s_epoch = __hip_atomic_load(my_sig + CAR_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  __syncthreads();
-  const unsigned epoch = s_epoch;
-  const long par = (long)(epoch & 1) * a.half_elems;
-  // 1. input slice -> own buffer
-  uint4* mine = reinterpret_cast<uint4*>(reinterpret_cast<unsigned short*>(a.data[a.rank]) + par);
-  const uint4* in = reinterpret_cast<const uint4*>(a.inp);
-  for (long i = (long)b * 256 + tid; i < a.n8; i += (long)nb * 256) mine[i] = in[i];
-  __threadfence_system();
-  __syncthreads();
-  // 2. signal every peer, then wait for every peer's signal for this block
+// steps 2 (signal + bounded wait for this block's flags) shared by both kernels
+__device__ __forceinline__ void car_signal_wait(const CarArgs& a, unsigned* my_sig, int b, int tid, unsigned epoch) {
   if (tid < a.world) {
     unsigned* peer = reinterpret_cast<unsigned*>(a.sig[tid]);
     __hip_atomic_store(peer + b * CAR_MAX_RANKS + a.rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -68,6 +55,40 @@ __global__ __launch_bounds__(256) void car_oneshot_kernel(CarArgs a) {
     }
   }
   __syncthreads();
+}
+
+// step 4: the last block to finish advances the epoch (device-side: graph replays stay correct)
+__device__ __forceinline__ void car_finish(unsigned* my_sig, int nb, int tid, unsigned epoch) {
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned d = __hip_atomic_fetch_add(my_sig + CAR_DONE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (unsigned)nb - 1) {
+      __hip_atomic_store(my_sig + CAR_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(my_sig + CAR_EPOCH, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned car_epoch(unsigned* my_sig, int tid) {
+  __shared__ unsigned s_epoch;
+  if (tid == 0) s_epoch = __hip_atomic_load(my_sig + CAR_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  return s_epoch;
+}
+
+__global__ __launch_bounds__(256) void car_oneshot_kernel(CarArgs a) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  unsigned* my_sig = reinterpret_cast<unsigned*>(a.sig[a.rank]);
+  const unsigned epoch = car_epoch(my_sig, tid);
+  const long par = (long)(epoch & 1) * a.half_elems;
+  // 1. input slice -> own buffer
+  uint4* mine = reinterpret_cast<uint4*>(reinterpret_cast<unsigned short*>(a.data[a.rank]) + par);
+  const uint4* in = reinterpret_cast<const uint4*>(a.inp);
+  for (long i = (long)b * 256 + tid; i < a.n8; i += (long)nb * 256) mine[i] = in[i];
+  __threadfence_system();
+  __syncthreads();
+  // 2. signal every peer, then wait for every peer's signal for this block
+  car_signal_wait(a, my_sig, b, tid, epoch);
   // 3. reduce this block's slice over all ranks
   for (long i = (long)b * 256 + tid; i < a.n8; i += (long)nb * 256) {
     float acc[8];
@@ -83,15 +104,85 @@ __global__ __launch_bounds__(256) void car_oneshot_kernel(CarArgs a) {
     }
     store8(a.out + i * 8, acc);
   }
-  // 4. last block to finish advances the epoch (device-side: graph replays stay correct)
+  car_finish(my_sig, nb, tid, epoch);
+}
+
+// Row-parallel projection partials -> all-reduce + bias + residual add + RMSNorm in ONE kernel
+// (TP decode: the o / down projections' partial sums are reduced and the next sub-layer's input
+// norm applied without the RCCL / one-shot all-reduce output round-tripping through HBM and a
+// separate add+norm launch).  Block b owns rows b, b + nb, ...: it stages them in its own
+// buffer, exchanges one flag per peer (the same rows on every rank), then for each row
+//   o = bf16(sum_r part_r + bias); s = bf16(o + res) -> res_out; y = bf16(s * rsqrt(mean(s^2) + eps) * w)
+// exactly as the unfused all-reduce -> add_rmsnorm (and decode_fin_add_rmsnorm) round.
+struct CarNormArgs {
+  const unsigned short* bias;  // [N] or nullptr
+  const unsigned short* res;   // [M, N]
+  const unsigned short* nw;    // [N]
+  unsigned short* res_out;     // [M, N]
+  int M, N;
+  float eps;
+};
+
+__global__ __launch_bounds__(256) void car_add_rmsnorm_kernel(CarArgs a, CarNormArgs c) {
+  extern __shared__ __attribute__((aligned(16))) float srow[];
+  __shared__ float red[4];
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  unsigned* my_sig = reinterpret_cast<unsigned*>(a.sig[a.rank]);
+  const unsigned epoch = car_epoch(my_sig, tid);
+  const long par = (long)(epoch & 1) * a.half_elems;
+  const int N = c.N, n8 = N / 8;
+  unsigned short* mine = reinterpret_cast<unsigned short*>(a.data[a.rank]) + par;
+  for (int m = b; m < c.M; m += nb)
+    for (int i = tid; i < n8; i += 256)
+      reinterpret_cast<uint4*>(mine + (long)m * N)[i] = reinterpret_cast<const uint4*>(a.inp + (long)m * N)[i];
+  __threadfence_system();
   __syncthreads();
-  if (tid == 0) {
-    const unsigned d = __hip_atomic_fetch_add(my_sig + CAR_DONE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (unsigned)nb - 1) {
-      __hip_atomic_store(my_sig + CAR_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(my_sig + CAR_EPOCH, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  car_signal_wait(a, my_sig, b, tid, epoch);
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+  for (int m = b; m < c.M; m += nb) {
+    const long base = (long)m * N;
+    float ss = 0.f;
+    for (int i = tid; i < n8; i += 256) {
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      for (int r = 0; r < a.world; ++r) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned short*>(a.data[r]) + par + base);
+        const u32x4 v = __builtin_nontemporal_load(src + i);
+        const unsigned short* h = reinterpret_cast<const unsigned short*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(h[j]);
+      }
+      float rv[8], bv[8];
+      load8(c.res + base + i * 8, rv);
+      if (c.bias) load8(c.bias + i * 8, bv);
+      float sv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float o = bf2f(f2bf(acc[j]));
+        if (c.bias) o = bf2f(f2bf(o + bv[j]));
+        sv[j] = bf2f(f2bf(o + rv[j]));
+        srow[i * 8 + j] = sv[j];
+        ss += sv[j] * sv[j];
+      }
+      store8(c.res_out + base + i * 8, sv);
     }
+    // block sum of ss (4 waves)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + c.eps);
+    for (int i = tid; i < n8; i += 256) {
+      float wv[8], yv[8];
+      load8(c.nw + i * 8, wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) yv[j] = srow[i * 8 + j] * rs * wv[j];
+      store8(a.out + base + i * 8, yv);
+    }
+    __syncthreads();  // srow / red reused by the block's next row
   }
+  car_finish(my_sig, nb, tid, epoch);
 }
 
 }  // namespace
@@ -160,7 +251,52 @@ void car_allreduce(const at::Tensor& inp, at::Tensor& out, const at::Tensor& dat
   hipLaunchKernelGGL(car_oneshot_kernel, dim3(nb), dim3(256), 0, stream(), a);
 }
 
-TORCH_LIBRARY_IMPL(llmctl, CUDA, m) { m.impl("car_allreduce", &car_allreduce); }
+// partial [M, N] (this rank's row-parallel projection output) -> (y = rmsnorm(res + sum + bias) * w, res_out)
+std::tuple<at::Tensor, at::Tensor> car_allreduce_add_rmsnorm(const at::Tensor& partial, const c10::optional<at::Tensor>& bias,
+                                                             const at::Tensor& res, const at::Tensor& nw, double eps,
+                                                             const at::Tensor& data_ptrs, const at::Tensor& sig_ptrs,
+                                                             int64_t rank, int64_t world, int64_t half_bytes) {
+  LLMCTL_CHECK(partial.is_cuda() && partial.is_contiguous() && partial.scalar_type() == at::kBFloat16 &&
+                   partial.dim() == 2 && res.sizes() == partial.sizes() && res.is_contiguous() &&
+                   res.scalar_type() == at::kBFloat16,
+               "car_allreduce_add_rmsnorm: contiguous bf16 partial / residual [M, N]");
+  const long M = partial.size(0), N = partial.size(1);
+  LLMCTL_CHECK(nw.is_contiguous() && nw.numel() == N && nw.scalar_type() == at::kBFloat16,
+               "car_allreduce_add_rmsnorm: norm weight bf16 [N]");
+  const bool has_b = bias.has_value() && bias->defined();
+  if (has_b) {
+    LLMCTL_CHECK(bias->is_contiguous() && bias->numel() == N && bias->scalar_type() == at::kBFloat16,
+                 "car_allreduce_add_rmsnorm: bias bf16 [N]");
+  }
+  LLMCTL_CHECK(N % 8 == 0 && N <= 16384 && M * N * 2 <= half_bytes, "car_allreduce_add_rmsnorm: N % 8, N <= 16384, fits");
+  LLMCTL_CHECK(world >= 1 && world <= CAR_MAX_RANKS && rank >= 0 && rank < world, "car_allreduce_add_rmsnorm: world <= 8");
+  LLMCTL_CHECK(data_ptrs.device().is_cpu() && sig_ptrs.device().is_cpu() && data_ptrs.numel() == world &&
+                   sig_ptrs.numel() == world && data_ptrs.scalar_type() == at::kLong,
+               "car_allreduce_add_rmsnorm: CPU int64 pointer tables");
+  const c10::DeviceGuard g(partial.device());
+  auto y = at::empty_like(partial);
+  auto res_out = at::empty_like(partial);
+  CarArgs a{};
+  a.inp = bf_ptr(partial);
+  a.out = bf_mut(y);
+  for (int r = 0; r < world; ++r) {
+    a.data[r] = (unsigned long long)data_ptrs.data_ptr<int64_t>()[r];
+    a.sig[r] = (unsigned long long)sig_ptrs.data_ptr<int64_t>()[r];
+  }
+  a.rank = (int)rank;
+  a.world = (int)world;
+  a.n8 = M * N / 8;
+  a.half_elems = half_bytes / 2;
+  CarNormArgs c{has_b ? bf_ptr(*bias) : nullptr, bf_ptr(res), bf_ptr(nw), bf_mut(res_out), (int)M, (int)N, (float)eps};
+  const int nb = (int)std::max<long>(1, std::min<long>(CAR_MAX_BLOCKS, M));
+  hipLaunchKernelGGL(car_add_rmsnorm_kernel, dim3(nb), dim3(256), (size_t)N * 4, stream(), a, c);
+  return {y, res_out};
+}
+
+TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("car_allreduce", &car_allreduce);
+  m.impl("car_allreduce_add_rmsnorm", &car_allreduce_add_rmsnorm);
+}
 // the tensor-less buffer/IPC helpers are registered as catch-all kernels in bindings.cpp
 
 }  // namespace llmctl

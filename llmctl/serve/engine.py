@@ -120,6 +120,15 @@ class InferenceEngine:
     def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
         return logits
 
+    def _fused_reduce_ok(self) -> bool:
+        """TP > 1: can the row-parallel reductions fuse the bias / residual / RMSNorm (TP engine)."""
+        return False
+
+    def _reduce_add_rmsnorm(self, part, bias, res, norm_w, eps):
+        """(rmsnorm(res + reduce(part) + bias) * norm_w, new residual) — TP=1: no reduction."""
+        y = part if bias is None else part + bias
+        return ops.add_rmsnorm(y, res, norm_w, eps)
+
     # ------------------------------------------------------------------ model pieces
     def _embed(self, ids: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
         m = self.model
@@ -257,11 +266,13 @@ class InferenceEngine:
     def _fused_decode(self) -> bool:
         """Decode layers on the fused-epilogue projections (``ops.decode_qkv_rope_cache`` /
         ``decode_up_swiglu`` / ``decode_linear_add_rmsnorm``): 10 kernels per layer instead of 13
-        (the RoPE/cache-write, SwiGLU and add+RMSNorm passes ride on the projections' finalize).  Needs the GPU path, TP=1
-        (the row-parallel all-reduce sits between a projection and the next norm), RMSNorm,
-        RoPE and a gated MLP; ``LLMCTL_DECODE_FUSED=0`` keeps the unfused layer (A/B)."""
+        (the RoPE/cache-write, SwiGLU and add+RMSNorm passes ride on the projections' finalize).  Needs the GPU path,
+        RMSNorm, RoPE and a gated MLP; at TP > 1 the row-parallel projections' all-reduce, bias,
+        residual add and next RMSNorm are one custom-all-reduce kernel
+        (``_reduce_add_rmsnorm``); ``LLMCTL_DECODE_FUSED=0`` keeps the unfused layer (A/B)."""
         cfg, m = self.cfg, self.model
-        return (self.device.type == "cuda" and self.tp == 1 and self.rope is not None and cfg.gated_mlp
+        return (self.device.type == "cuda" and (self.tp == 1 or self._fused_reduce_ok()) and self.rope is not None
+                and cfg.gated_mlp
                 and not cfg.is_moe and m.final_norm_b is None
                 and all(l.attn_norm_b is None and l.mlp_norm_b is None for l in m.layers)
                 and os.environ.get("LLMCTL_DECODE_FUSED", "1") != "0")
@@ -290,14 +301,22 @@ class InferenceEngine:
         kc, vc = self.kv_cache.k, self.kv_cache.v
         x = self._embed(ids, positions)
         xn, res = ops.rmsnorm(x, layers[0].attn_norm_w, eps), x
+        tp = self.tp > 1
         for li, layer in enumerate(layers):
             o = ops.decode_attention_qkv(xn, layer.wqkv, layer.bqkv, self.rope[0], self.rope[1], layer.nq,
                                          layer.nkv, positions, kc[li], vc[li], slots, block_tables, ctx_lens)
-            xn, res = ops.decode_linear_add_rmsnorm(o.view(o.shape[0], -1), layer.wo, layer.bo, res,
-                                                    layer.mlp_norm_w, eps)
-            act = ops.decode_up_swiglu(xn, layer.w_up, layer.b_up)
+            if tp:  # row-parallel o-proj partial -> one kernel: all-reduce + bias + residual + RMSNorm
+                xn, res = self._reduce_add_rmsnorm(ops.decode_linear(o.view(o.shape[0], -1), layer.wo), layer.bo,
+                                                   res, layer.mlp_norm_w, eps)
+            else:
+                xn, res = ops.decode_linear_add_rmsnorm(o.view(o.shape[0], -1), layer.wo, layer.bo, res,
+                                                        layer.mlp_norm_w, eps)
+            act = ops.decode_up_swiglu(xn, layer.w_up, layer.b_up)  # the local F shard
             nw = layers[li + 1].attn_norm_w if li + 1 < len(layers) else m.final_norm_w
-            xn, res = ops.decode_linear_add_rmsnorm(act, layer.w_down, layer.b_down, res, nw, eps)
+            if tp:
+                xn, res = self._reduce_add_rmsnorm(ops.decode_linear(act, layer.w_down), layer.b_down, res, nw, eps)
+            else:
+                xn, res = ops.decode_linear_add_rmsnorm(act, layer.w_down, layer.b_down, res, nw, eps)
         return self._gather_vocab(ops.decode_linear(xn, m.head_weight()))
 
     def _bucket(self, n: int) -> int:

@@ -91,6 +91,23 @@ class TPInferenceEngine(InferenceEngine):
         dist.all_reduce(x, group=self.tp_group)
         return x
 
+    def _fused_reduce_ok(self) -> bool:
+        return self.car is not None and os.environ.get("LLMCTL_TP_FUSED_DECODE", "1") != "0"
+
+    def _reduce_add_rmsnorm(self, part, bias, res, norm_w, eps):
+        """One kernel (``car_allreduce_add_rmsnorm``): the row-parallel partials' all-reduce, the
+        bias, the residual add and the next sub-layer's RMSNorm; RCCL + add_rmsnorm when the
+        message does not fit the one-shot buffer (or under gloo on CPU)."""
+        if (self.car is not None and self.car.eligible(part) and part.dim() == 2 and part.shape[1] <= 16384
+                and part.numel() * 2 <= self.car.max_bytes):
+            return self.car.all_reduce_add_rmsnorm(part, bias, res, norm_w, eps)
+        y = self._reduce(part)
+        if bias is not None:
+            y = y + bias
+        from llmctl import ops
+
+        return ops.add_rmsnorm(y, res, norm_w, eps)
+
     def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
         n, vl = logits.shape
         if self.car is not None and logits.dtype == torch.bfloat16 and self.tp_size * n * vl * 2 <= self.car.max_bytes:

@@ -58,7 +58,7 @@ def test_gemm64_up_swiglu_matches_fp32(native_lib, T, K, F):
 
 
 def _layer_grads(fused: bool, monkeypatch, sink: bool):
-    monkeypatch.setenv("LLMCTL_FUSED_FWD", "1" if fused else "0")
+    monkeypatch.setenv("LLMCTL_FUSED_FWD", "1" if fused else "0")  # default off: A/B both
     from llmctl.exec.linear import GradSink
     from llmctl.models import ParallelContext, get_model_config
     from llmctl.models.transformer import DecoderLayer
