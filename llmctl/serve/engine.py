@@ -262,6 +262,70 @@ class InferenceEngine:
         last = torch.tensor(plan["last"], device=d)
         return self._final(x.index_select(0, last), res.index_select(0, last))
 
+    # ------------------------------------------------------------------ mixed prefill + decode
+    def mixed_plan(self, chunks: List[PrefillChunk], seqs: List[Sequence]) -> Dict:
+        """One step's prefill chunks AND decode tokens as one token batch (decode rows last)."""
+        p, d = self.prefill_plan(chunks), self.decode_plan(seqs)
+        return {"op": "mixed", "prefill": p, "decode": d}
+
+    @torch.inference_mode()
+    def mixed(self, chunks: List[PrefillChunk], seqs: List[Sequence]) -> torch.Tensor:
+        return self.mixed_exec(self.mixed_plan(chunks, seqs))
+
+    @torch.inference_mode()
+    def mixed_exec(self, plan: Dict) -> torch.Tensor:
+        """Mixed step (continuous batching's fused step): the decode tokens of the running batch
+        ride in the prefill chunks' forward — every projection / MLP GEMM streams its weights
+        once for both kinds of rows — and only attention splits by row kind: prefill rows through
+        the (paged or fresh-prompt flash) prefill attention, decode rows through the paged decode
+        kernel.  Returns logits [n_final_chunks + n_decode, V]: the final chunks' rows first, in
+        chunk order, then the decode rows (eager: the graph-captured decode step is for
+        decode-only steps).  Reference batching: ``llmctl/serve/server.py:89-125, 372-386``."""
+        d = self.device
+        pp, dp = plan["prefill"], plan["decode"]
+        Tp, Td = len(pp["ids"]), len(dp["ids"])
+        ids = torch.cat([torch.from_numpy(pp["ids"]), torch.tensor(dp["ids"], dtype=torch.long)]).to(d, non_blocking=True)
+        pos = torch.cat([torch.from_numpy(pp["pos"]), torch.tensor(dp["positions"], dtype=torch.int32)]).to(d, non_blocking=True)
+        slots = torch.cat([torch.from_numpy(pp["slots"]), torch.tensor(dp["slots"], dtype=torch.long)]).to(d, non_blocking=True)
+        bt = torch.from_numpy(pp["bt"]).to(d, non_blocking=True)
+        cu = torch.tensor(pp["cu"], dtype=torch.int32).to(d, non_blocking=True)
+        ctx = torch.tensor(pp["ctx"], dtype=torch.int32).to(d, non_blocking=True)
+        work = torch.tensor(pp["work"], dtype=torch.int32).to(d, non_blocking=True)
+        bt_d = torch.from_numpy(dp["bt"]).to(d, non_blocking=True)
+        ctx_d = torch.tensor(dp["ctx"], dtype=torch.int32).to(d, non_blocking=True)
+        fa = pp.get("doc") is not None and d.type == "cuda" and os.environ.get("LLMCTL_PREFILL_FA", "1") != "0"
+        doc = torch.from_numpy(pp["doc"]).to(d, non_blocking=True).view(1, Tp) if fa and len(pp["cu"]) > 2 else None
+        x = self._embed(ids, pos.long())
+        res = None
+        kc, vc = self.kv_cache.k, self.kv_cache.v
+        for li, layer in enumerate(self.model.layers):
+            xn, res = self._norm(layer, x, res, "attn")
+            q, k, v = self._qkv(layer, xn, pos, self.max_model_len, kc[li], vc[li], slots)
+            if fa:
+                op = ops.flash_attention(q[:Tp].reshape(1, Tp, layer.nq, layer.D),
+                                         k[:Tp].reshape(1, Tp, layer.nkv, layer.D),
+                                         v[:Tp].reshape(1, Tp, layer.nkv, layer.D), causal=True, doc_start=doc)
+            else:
+                op = ops.paged_prefill_attention(q[:Tp].reshape(Tp, layer.nq, layer.D), kc[li], vc[li], bt, cu, ctx,
+                                                 work=work)
+            od = ops.paged_attention_decode(q[Tp:].reshape(Td, layer.nq, layer.D).contiguous(), kc[li], vc[li], bt_d,
+                                            ctx_d)
+            o = torch.cat([op.reshape(Tp, -1), od.reshape(Td, -1)])
+            a = self._reduce(ops.decode_linear(o, layer.wo))
+            if layer.bo is not None:
+                a = a + layer.bo
+            xn, res = self._norm(layer, a, res, "mlp")
+            x = self._mlp(layer, xn)
+        self.stats["prefill_tokens"] += Tp
+        self.stats["decode_tokens"] += Td
+        self.stats["mixed_steps"] = self.stats.get("mixed_steps", 0) + 1
+        rows = torch.tensor(list(pp["last"]) + list(range(Tp, Tp + Td)), device=d)
+        return self._final(x.index_select(0, rows), res.index_select(0, rows))
+
+    def _mixed_ok(self) -> bool:
+        """``LLMCTL_MIXED_STEPS=0`` runs a step's decode and prefill as two forwards (A/B)."""
+        return os.environ.get("LLMCTL_MIXED_STEPS", "1") != "0"
+
     # ------------------------------------------------------------------ decode
     def _fused_decode(self) -> bool:
         """Decode layers on the fused-epilogue projections (``ops.decode_qkv_rope_cache`` /
@@ -455,6 +519,21 @@ class InferenceEngine:
         """One scheduling iteration; returns the number of tokens produced."""
         out = self.scheduler.schedule()
         produced = 0
+        if out.decode and out.prefill and self._mixed_ok():
+            logits = self.mixed(out.prefill, out.decode)
+            final = [c.seq for c in out.prefill if c.final]
+            toks = self.sample(logits, final + list(out.decode))
+            for c in out.prefill:
+                self.scheduler.computed(c.seq, c.count)
+                self.stats["prefix_hit_tokens"] = self.stats.get("prefix_hit_tokens", 0) + (
+                    c.seq.cached_tokens if c.start == c.seq.cached_tokens else 0)
+            for seq in out.decode:
+                self.scheduler.computed(seq, 1)
+            for seq, tok in zip(final + list(out.decode), toks):
+                self._append(seq, tok)
+                produced += 1
+            self.stats["steps"] += 1
+            return produced
         if out.decode:
             logits = self.decode(out.decode)
             for seq, tok in zip(out.decode, self.sample(logits, out.decode)):

@@ -137,6 +137,10 @@ class TPInferenceEngine(InferenceEngine):
     def decode(self, seqs: List[Sequence]) -> torch.Tensor:
         return self.decode_exec(self._bcast(self.decode_plan(seqs)))
 
+    @torch.inference_mode()
+    def mixed(self, chunks, seqs: List[Sequence]) -> torch.Tensor:
+        return self.mixed_exec(self._bcast(self.mixed_plan(chunks, seqs)))
+
     def stop_workers(self) -> None:
         if self.tp_rank == 0:
             self._bcast({"op": "stop"})
@@ -155,6 +159,8 @@ class TPInferenceEngine(InferenceEngine):
                 self.prefill_exec(plan)
             elif op == "decode":
                 self.decode_exec(plan)
+            elif op == "mixed":
+                self.mixed_exec(plan)
             else:
                 raise RuntimeError(f"unknown TP plan op {op!r}")
 

@@ -176,6 +176,7 @@ def serve_generate_gpu(rank: int, world: int, max_tokens: int = 8) -> dict:
     torch.cuda.set_device(0)
     kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=64, block_size=16, max_model_len=256,
               max_batch_tokens=512, seed=0, use_graphs=True)
+    kw.update(engine_kw or {})
     prompts = PROMPTS + [[(5 * i) % 500 + 1 for i in range(40)]]
     if world == 1:
         from llmctl.serve.engine import InferenceEngine
@@ -461,3 +462,69 @@ def train_drift(rank: int, world: int, steps: int, main_grads: str, precision: s
     state = {n: p.detach().float().clone() for n, p in eng.model.named_parameters()}
     return {"losses": losses, "state": state if rank == 0 else None,
             "grad_dtype": str(eng.grad_dtype), "flat_grad_dtype": str(eng.flat.grad.dtype)}
+
+
+def serve_forced_gpu(rank: int, world: int, max_tokens: int = 8, model: str = "tiny", forced=None,
+                     env: Optional[dict] = None, engine_kw: Optional[dict] = None) -> dict:
+    """GPU serving (TP = world ranks sharing cuda:0 over gloo + the custom IPC all-reduce, decode
+    steps in hipGraphs) with every sampled token replaced by ``forced[seq][step]`` (teacher
+    forcing; None: greedy) and the full-vocabulary logits of every step recorded on rank 0 — so
+    two configurations can be compared row by row over the same token stream."""
+    import os
+
+    import torch.distributed as dist
+
+    from llmctl.serve.scheduler import SamplingParams
+
+    for k, v in (env or {}).items():
+        os.environ[k] = v
+    torch.cuda.set_device(0)
+    kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=64, block_size=16, max_model_len=256,
+              max_batch_tokens=512, seed=0, use_graphs=True)
+    kw.update(engine_kw or {})
+    prompts = PROMPTS + [[(5 * i) % 500 + 1 for i in range(40)]]
+    if world == 1:
+        from llmctl.serve.engine import InferenceEngine
+
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            os.environ.pop(k, None)
+        eng = InferenceEngine(model, **kw)
+    else:
+        from llmctl.serve.tp import TPInferenceEngine
+
+        dist.init_process_group("gloo")
+        eng = TPInferenceEngine(model, **kw)
+        assert eng.car is not None, "custom all-reduce not active"
+        if eng.tp_rank != 0:
+            eng.worker_loop()
+            eng.release_graphs()
+            dist.barrier()
+            eng.car.close()
+            return {}
+    seqs = [eng.add_request(p, SamplingParams(max_tokens=max_tokens, temperature=0.0)) for p in prompts]
+    idx = {s.seq_id: i for i, s in enumerate(seqs)}
+    rec: Dict[int, List[torch.Tensor]] = {}
+    greedy = eng.sample
+
+    def sample(logits, batch):
+        toks = greedy(logits, batch)
+        out = []
+        for row, s, t in zip(logits.float().cpu(), batch, toks):
+            i = idx[s.seq_id]
+            rec.setdefault(i, []).append(row)
+            out.append(forced[i][len(s.output_ids)] if forced is not None else t)
+        return out
+
+    eng.sample = sample
+    while any(s.status != "finished" for s in seqs):
+        eng.step()
+    res = {"tokens": [s.output_ids for s in seqs], "graph_replays": eng.stats["graph_replays"],
+           "fused_decode": bool(eng._fused_decode()), "mixed_steps": eng.stats.get("mixed_steps", 0),
+           "logits": torch.stack([torch.stack(rec[i]) for i in range(len(seqs))])}
+    if world > 1:
+        eng.stop_workers()
+        eng.release_graphs()
+        eng.car.check()
+        dist.barrier()
+        eng.car.close()
+    return res

@@ -354,3 +354,22 @@ def test_preemption_resume_reuses_cached_blocks():
     assert seq.cached_tokens == 24 and e.stats["prefill_tokens"] - before == 1  # 25 known, 24 re-attached
     ref = InferenceEngine("tiny", prefix_caching=False, **kw)
     assert seq.output_ids == _greedy(ref, [prompt], 10)[0]
+
+
+@pytest.mark.parametrize("prefix", [False, True])
+def test_mixed_prefill_decode_steps_match_separate(monkeypatch, prefix):
+    """A step with both decode tokens and prefill chunks runs ONE forward (decode rows appended to
+    the chunk batch, attention split by row kind): greedy outputs equal the two-forward steps."""
+    prompts = [[1, 2, 3, 4, 5] * 6, [9] * 37, [7, 7, 3], [3, 1, 4, 1, 5, 9, 2, 6] * 5]
+    kw = dict(device="cpu", max_batch_size=4, num_kv_blocks=64, block_size=8, max_model_len=256,
+              max_batch_tokens=48, prefix_caching=prefix)
+    p = SamplingParams(max_tokens=9, temperature=0.0)
+    monkeypatch.setenv("LLMCTL_MIXED_STEPS", "1")
+    e = InferenceEngine("tiny", **kw)
+    a = [s.output_ids for s in e.generate(prompts, p)]
+    assert e.stats.get("mixed_steps", 0) > 0
+    monkeypatch.setenv("LLMCTL_MIXED_STEPS", "0")
+    e2 = InferenceEngine("tiny", **kw)
+    b = [s.output_ids for s in e2.generate(prompts, p)]
+    assert e2.stats.get("mixed_steps", 0) == 0
+    assert a == b
