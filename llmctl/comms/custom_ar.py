@@ -21,7 +21,14 @@ from llmctl.ops._lib import native
 
 
 class CustomAllReduce:
-    def __init__(self, group=None, max_bytes: int = 2 << 20, device: Optional[torch.device] = None):
+    """``max_bytes``: largest message of the one-shot kernel (decode); ``twoshot_bytes``: largest
+    message of the two-shot kernel (prefill-sized: reduce-scatter + all-gather through the peer
+    buffers, 2 (w-1)/w x n bytes read per rank instead of (w-1) x n), used above
+    ``twoshot_min_bytes`` when world > 2.  The data buffer's two epoch-parity halves are sized for
+    the larger of the two (input copy + reduced slice)."""
+
+    def __init__(self, group=None, max_bytes: int = 2 << 20, device: Optional[torch.device] = None,
+                 twoshot_bytes: int = 0, twoshot_min_bytes: int = 1 << 20):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -29,9 +36,12 @@ class CustomAllReduce:
             raise ValueError("custom all-reduce supports up to 8 ranks (one node)")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.max_bytes = max_bytes
+        self.twoshot_bytes = twoshot_bytes if self.world > 2 else 0
+        self.twoshot_min_bytes = twoshot_min_bytes
+        self.half_bytes = max(max_bytes, self.twoshot_bytes + self.twoshot_bytes // max(self.world, 1))
         ops = native()
         self.ops = ops
-        self._data = ops.car_malloc(2 * max_bytes)  # two epoch-parity halves
+        self._data = ops.car_malloc(2 * self.half_bytes)  # two epoch-parity halves
         self._sig = ops.car_malloc(4 * ops.car_sig_words())
         mine = (bytes(ops.car_ipc_handle(self._data).numpy()), bytes(ops.car_ipc_handle(self._sig).numpy()))
         handles: List = [None] * self.world
@@ -56,9 +66,19 @@ class CustomAllReduce:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
                 and x.numel() * 2 <= self.max_bytes)
 
+    def twoshot_eligible(self, x: torch.Tensor) -> bool:
+        n = x.numel() * 2
+        return (self.twoshot_bytes > 0 and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
+                and x.numel() % (8 * self.world) == 0 and self.twoshot_min_bytes <= n <= self.twoshot_bytes)
+
     def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Sum of ``x`` over the group (in place unless ``out`` is given); RCCL beyond the
         buffer size or for other dtypes."""
+        if self.twoshot_eligible(x) and (not self.eligible(x) or x.numel() * 2 >= self.twoshot_min_bytes):
+            out = x if out is None else out
+            self.ops.car_allreduce_twoshot(x, out, self.data_ptrs, self.sig_ptrs, self.rank, self.world,
+                                           self.half_bytes)
+            return out
         if not self.eligible(x):
             dist.all_reduce(x, group=self.group)
             if out is not None:
@@ -66,7 +86,7 @@ class CustomAllReduce:
                 return out
             return x
         out = x if out is None else out
-        self.ops.car_allreduce(x, out, self.data_ptrs, self.sig_ptrs, self.rank, self.world, self.max_bytes)
+        self.ops.car_allreduce(x, out, self.data_ptrs, self.sig_ptrs, self.rank, self.world, self.half_bytes)
         return out
 
     def all_reduce_add_rmsnorm(self, part: torch.Tensor, bias: Optional[torch.Tensor], res: torch.Tensor,
@@ -74,7 +94,7 @@ class CustomAllReduce:
         """(rmsnorm(res + sum(part) + bias) * norm_w, res + sum(part) + bias) in one kernel: the TP
         decode layer's row-parallel reduction fused with the next norm (``part`` [M, N] bf16)."""
         return self.ops.car_allreduce_add_rmsnorm(part, bias, res.contiguous(), norm_w, float(eps), self.data_ptrs,
-                                                  self.sig_ptrs, self.rank, self.world, self.max_bytes)
+                                                  self.sig_ptrs, self.rank, self.world, self.half_bytes)
 
     def check(self) -> None:
         if self.ops.car_error(self._sig):

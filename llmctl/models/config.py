@@ -236,7 +236,7 @@ MODEL_TEMPLATES: Dict[str, Dict[str, Dict[str, Any]]] = {
             "rope": {"base": 10000, "scaling": "linear"},
         },
         "wide": {  # 8 query / 8 KV heads: enough heads for TP=8 (BASELINE config #5's degree)
-            "name": "tiny-wide", "arch": "decoder-only", "layers": 2, "hidden": 256, "ffn": 768,
+            "name": "tiny-wide", "arch": "decoder-only", "layers": 2, "hidden": 512, "ffn": 1024,
             "heads": 8, "kv_heads": 8, "vocab_size": 512, "max_position_embeddings": 512,
             "rope": {"base": 10000, "scaling": "linear"},
         },

@@ -56,6 +56,7 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("gemm_bf16(Tensor a, Tensor b) -> Tensor");
   // custom all-reduce over xGMI peer memory (custom_ar.hip)
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, Tensor data_ptrs, Tensor sig_ptrs, int rank, int world, int half_bytes) -> ()");
+  m.def("car_allreduce_twoshot(Tensor inp, Tensor(a!) out, Tensor data_ptrs, Tensor sig_ptrs, int rank, int world, int half_bytes) -> ()");
   m.def("car_allreduce_add_rmsnorm(Tensor partial, Tensor? bias, Tensor res, Tensor nw, float eps, Tensor data_ptrs, Tensor sig_ptrs, int rank, int world, int half_bytes) -> (Tensor, Tensor)");
   m.def("car_malloc(int bytes) -> int", &llmctl::car_malloc);
   m.def("car_free(int ptr) -> ()", &llmctl::car_free);

@@ -23,8 +23,10 @@ namespace {
 
 constexpr int CAR_MAX_RANKS = 8;
 constexpr int CAR_MAX_BLOCKS = 64;
-// signal buffer layout (uint32): flags[CAR_MAX_BLOCKS][CAR_MAX_RANKS], then epoch, done, error
-constexpr int CAR_EPOCH = CAR_MAX_BLOCKS * CAR_MAX_RANKS;
+// signal buffer layout (uint32): flags[CAR_MAX_BLOCKS][CAR_MAX_RANKS] (one-shot, and the two-shot
+// kernel's first round), flags2[...] (the two-shot kernel's second round), then epoch, done, error
+constexpr int CAR_FLAGS2 = CAR_MAX_BLOCKS * CAR_MAX_RANKS;
+constexpr int CAR_EPOCH = 2 * CAR_MAX_BLOCKS * CAR_MAX_RANKS;
 constexpr int CAR_DONE = CAR_EPOCH + 1;
 constexpr int CAR_ERROR = CAR_EPOCH + 2;
 constexpr int CAR_SIG_WORDS = CAR_EPOCH + 16;
@@ -39,12 +41,14 @@ struct CarArgs {
   long half_elems;  // elements per epoch-parity half of a data buffer
 };
 
-// steps 2 (signal + bounded wait for this block's flags) shared by both kernels
-__device__ __forceinline__ void car_signal_wait(const CarArgs& a, unsigned* my_sig, int b, int tid, unsigned epoch) {
+// step 2 (signal + bounded wait for this block's flags, in flag array `round`) shared by the kernels
+__device__ __forceinline__ void car_signal_wait(const CarArgs& a, unsigned* my_sig, int b, int tid, unsigned epoch,
+                                                int round = 0) {
   if (tid < a.world) {
+    const int fo = round * CAR_FLAGS2;
     unsigned* peer = reinterpret_cast<unsigned*>(a.sig[tid]);
-    __hip_atomic_store(peer + b * CAR_MAX_RANKS + a.rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    unsigned* f = my_sig + b * CAR_MAX_RANKS + tid;
+    __hip_atomic_store(peer + fo + b * CAR_MAX_RANKS + a.rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* f = my_sig + fo + b * CAR_MAX_RANKS + tid;
     long spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       __builtin_amdgcn_s_sleep(2);
@@ -103,6 +107,60 @@ __global__ __launch_bounds__(256) void car_oneshot_kernel(CarArgs a) {
       for (int j = 0; j < 8; ++j) acc[j] += bf2f(h[j]);
     }
     store8(a.out + i * 8, acc);
+  }
+  car_finish(my_sig, nb, tid, epoch);
+}
+
+// Two-shot all-reduce for prefill-sized messages (MBs): the one-shot kernel reads (world - 1) x n
+// bytes from peers per rank; here rank r first reduces only its 1/world slice (reading (world-1)/
+// world x n), publishes it, and then gathers the other ranks' reduced slices (another (world-1)/
+// world x n) — 2 (world-1)/world x n per rank, the ring's byte count, in two flag rounds.  Slice s
+// is cut into nb sub-ranges; block b owns sub-range b of every slice on every rank, so the per-
+// block flags of round 0 (everyone's copy of sub-range b landed) and round 1 (everyone's reduced
+// sub-range b landed) need no grid barrier.  Buffer half = [input copy | reduced slice], per epoch
+// parity.  n8 (16-B vectors) must split evenly: n8 % world == 0.
+__global__ __launch_bounds__(256) void car_twoshot_kernel(CarArgs a) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  unsigned* my_sig = reinterpret_cast<unsigned*>(a.sig[a.rank]);
+  const unsigned epoch = car_epoch(my_sig, tid);
+  const long par = (long)(epoch & 1) * a.half_elems;
+  const long slice8 = a.n8 / a.world;                       // vectors per slice
+  const long sub = (slice8 + nb - 1) / nb;                  // per block
+  const long lo = (long)b * sub, hi = min(slice8, lo + sub);  // this block's sub-range of a slice
+  const long res_off = a.n8 * 8;                            // reduced-slice region (elements)
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+  // 1. every slice's sub-range b of the input -> own buffer
+  uint4* mine = reinterpret_cast<uint4*>(reinterpret_cast<unsigned short*>(a.data[a.rank]) + par);
+  const uint4* in = reinterpret_cast<const uint4*>(a.inp);
+  for (int sl = 0; sl < a.world; ++sl)
+    for (long i = lo + tid; i < hi; i += 256) mine[sl * slice8 + i] = in[sl * slice8 + i];
+  __threadfence_system();
+  __syncthreads();
+  car_signal_wait(a, my_sig, b, tid, epoch, 0);
+  // 2. reduce this rank's slice, sub-range b, over all ranks -> own reduced region
+  unsigned short* red = reinterpret_cast<unsigned short*>(a.data[a.rank]) + par + res_off;
+  for (long i = lo + tid; i < hi; i += 256) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int r = 0; r < a.world; ++r) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned short*>(a.data[r]) + par);
+      const u32x4 v = __builtin_nontemporal_load(src + (long)a.rank * slice8 + i);
+      const unsigned short* h = reinterpret_cast<const unsigned short*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(h[j]);
+    }
+    store8(red + i * 8, acc);
+  }
+  __threadfence_system();
+  __syncthreads();
+  car_signal_wait(a, my_sig, b, tid, epoch, 1);
+  // 3. gather every rank's reduced slice, sub-range b
+  for (int sl = 0; sl < a.world; ++sl) {
+    const u32x4* src =
+        reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned short*>(a.data[sl]) + par + res_off);
+    u32x4* dst = reinterpret_cast<u32x4*>(a.out) + (long)sl * slice8;
+    for (long i = lo + tid; i < hi; i += 256) dst[i] = __builtin_nontemporal_load(src + i);
   }
   car_finish(my_sig, nb, tid, epoch);
 }
@@ -251,6 +309,35 @@ void car_allreduce(const at::Tensor& inp, at::Tensor& out, const at::Tensor& dat
   hipLaunchKernelGGL(car_oneshot_kernel, dim3(nb), dim3(256), 0, stream(), a);
 }
 
+// two-shot variant: the buffer half must hold the input copy AND the reduced slice
+void car_allreduce_twoshot(const at::Tensor& inp, at::Tensor& out, const at::Tensor& data_ptrs,
+                           const at::Tensor& sig_ptrs, int64_t rank, int64_t world, int64_t half_bytes) {
+  LLMCTL_CHECK(inp.is_cuda() && inp.is_contiguous() && out.is_contiguous() && inp.scalar_type() == at::kBFloat16 &&
+                   out.scalar_type() == at::kBFloat16 && out.numel() == inp.numel(),
+               "car_allreduce_twoshot: contiguous bf16 in/out of equal size");
+  LLMCTL_CHECK(world >= 1 && world <= CAR_MAX_RANKS && rank >= 0 && rank < world, "car_allreduce_twoshot: world <= 8");
+  LLMCTL_CHECK(inp.numel() % (8 * world) == 0 && inp.numel() * 2 + inp.numel() * 2 / world <= half_bytes,
+               "car_allreduce_twoshot: numel % (8 world) and input + slice <= buffer half");
+  LLMCTL_CHECK(data_ptrs.device().is_cpu() && sig_ptrs.device().is_cpu() && data_ptrs.numel() == world &&
+                   sig_ptrs.numel() == world && data_ptrs.scalar_type() == at::kLong,
+               "car_allreduce_twoshot: CPU int64 pointer tables");
+  const c10::DeviceGuard g(inp.device());
+  CarArgs a{};
+  a.inp = bf_ptr(inp);
+  a.out = bf_mut(out);
+  for (int r = 0; r < world; ++r) {
+    a.data[r] = (unsigned long long)data_ptrs.data_ptr<int64_t>()[r];
+    a.sig[r] = (unsigned long long)sig_ptrs.data_ptr<int64_t>()[r];
+  }
+  a.rank = (int)rank;
+  a.world = (int)world;
+  a.n8 = inp.numel() / 8;
+  a.half_elems = half_bytes / 2;
+  const long slice8 = a.n8 / world;
+  const int nb = (int)std::max<long>(1, std::min<long>(CAR_MAX_BLOCKS, (slice8 + 255) / 256));
+  hipLaunchKernelGGL(car_twoshot_kernel, dim3(nb), dim3(256), 0, stream(), a);
+}
+
 // partial [M, N] (this rank's row-parallel projection output) -> (y = rmsnorm(res + sum + bias) * w, res_out)
 std::tuple<at::Tensor, at::Tensor> car_allreduce_add_rmsnorm(const at::Tensor& partial, const c10::optional<at::Tensor>& bias,
                                                              const at::Tensor& res, const at::Tensor& nw, double eps,
@@ -295,6 +382,7 @@ std::tuple<at::Tensor, at::Tensor> car_allreduce_add_rmsnorm(const at::Tensor& p
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("car_allreduce", &car_allreduce);
+  m.impl("car_allreduce_twoshot", &car_allreduce_twoshot);
   m.impl("car_allreduce_add_rmsnorm", &car_allreduce_add_rmsnorm);
 }
 // the tensor-less buffer/IPC helpers are registered as catch-all kernels in bindings.cpp

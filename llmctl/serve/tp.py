@@ -55,7 +55,8 @@ class TPInferenceEngine(InferenceEngine):
                 and os.environ.get("LLMCTL_CUSTOM_AR", "1") != "0"):
             from llmctl.comms.custom_ar import CustomAllReduce
 
-            self.car = CustomAllReduce(self.tp_group, max_bytes=4 << 20, device=self.device)
+            # one-shot up to 4 MB (decode), two-shot up to 32 MB (2k-token prefill chunks at d = 8192)
+            self.car = CustomAllReduce(self.tp_group, max_bytes=4 << 20, device=self.device, twoshot_bytes=32 << 20)
 
     # ------------------------------------------------------------------ TP hooks
     def _load(self, model_path: str, dtype, seed: int):
@@ -86,7 +87,7 @@ class TPInferenceEngine(InferenceEngine):
         return int(t.item())
 
     def _reduce(self, x: torch.Tensor) -> torch.Tensor:
-        if self.car is not None and self.car.eligible(x):
+        if self.car is not None and (self.car.eligible(x) or self.car.twoshot_eligible(x)):
             return self.car.all_reduce(x)
         dist.all_reduce(x, group=self.tp_group)
         return x

@@ -207,7 +207,8 @@ def serve_generate_gpu(rank: int, world: int, max_tokens: int = 8) -> dict:
     return out
 
 
-def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters: int = 20) -> dict:
+def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters: int = 20,
+                    twoshot_bytes: int = 0) -> dict:
     """Two+ processes sharing one GPU: the IPC one-shot all-reduce must equal the sum of the
     inputs (exact fp32 sum, bf16 output) over many calls (epoch parity) and under hipGraph
     replay.  The process group is gloo (RCCL cannot put two ranks on one device)."""
@@ -218,7 +219,8 @@ def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters
 
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
-    car = CustomAllReduce(max_bytes=2 << 20, device=torch.device("cuda", 0))
+    car = CustomAllReduce(max_bytes=2 << 20, device=torch.device("cuda", 0), twoshot_bytes=twoshot_bytes,
+                          twoshot_min_bytes=64 << 10)
     worst = 0.0
     try:
         g = torch.Generator().manual_seed(1234 + rank)
@@ -261,7 +263,7 @@ def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters
     finally:
         dist.barrier()
         car.close()
-    return {"worst_rel_err": worst}
+    return {"worst_rel_err": worst, "twoshot": car.twoshot_bytes > 0}
 
 
 def _layout_config(layout: dict, model: str = "tiny"):
