@@ -518,8 +518,13 @@ def serve_forced_gpu(rank: int, world: int, max_tokens: int = 8, model: str = "t
         return out
 
     eng.sample = sample
+    progress = os.environ.get("LLMCTL_TEST_PROGRESS")  # heartbeat lines for long multi-rank GPU runs
+    n = 0
     while any(s.status != "finished" for s in seqs):
         eng.step()
+        n += 1
+        if progress and n % 4 == 0:
+            print(f"[serve_forced_gpu rank {rank}/{world}] step {n}", flush=True)
     res = {"tokens": [s.output_ids for s in seqs], "graph_replays": eng.stats["graph_replays"],
            "fused_decode": bool(eng._fused_decode()), "mixed_steps": eng.stats.get("mixed_steps", 0),
            "logits": torch.stack([torch.stack(rec[i]) for i in range(len(seqs))])}

@@ -168,7 +168,7 @@ def _logit_rows(out):
     return lg.reshape(-1, lg.shape[-1])
 
 
-def _forced_match(world: int, model: str, tol: float):
+def _forced_match(world: int, model: str, tol: float, env=None):
     """TP=world serving (world processes sharing cuda:0, custom IPC all-reduces and the vocab gather
     inside captured decode graphs; at TP > 1 the fused decode layer with the all-reduce + residual
     + RMSNorm kernel) fed the TP=1 engine's greedy tokens: every prefill / decode step's logits
@@ -178,7 +178,7 @@ def _forced_match(world: int, model: str, tol: float):
     from llmctl.testing.workers import serve_forced_gpu
 
     ref = serve_forced_gpu(0, 1, 8, model)
-    out = run_ranks(serve_forced_gpu, world, 8, model, ref["tokens"], timeout=420)
+    out = run_ranks(serve_forced_gpu, world, 8, model, ref["tokens"], env, timeout=300)
     assert out[0]["graph_replays"] > 0 and out[0]["fused_decode"]
     assert out[0]["logits"].shape == ref["logits"].shape
     err = row_err(_logit_rows(out[0]), _logit_rows(ref))
@@ -191,8 +191,12 @@ def test_tp2_serving_two_processes_custom_ar_graphs(native_lib):
 
 def test_tp8_serving_eight_processes_custom_ar_graphs(native_lib):
     """BASELINE config #5's degree (TP=8), eight processes on one GPU: one query and one KV head
-    per rank (tiny-wide), 8-way custom all-reduces."""
-    _forced_match(8, "tiny-wide", 3e-2)
+    per rank (tiny-wide), 8-way custom all-reduces.  One hardware queue per rank: the custom
+    all-reduce kernels of all eight processes must be resident together (each spins on its
+    peers' flags), and eight processes at HIP's default of 4 queues each oversubscribe the
+    hardware queue slots, so the scheduler time-slices them and every all-reduce stalls until a
+    peer's queue is mapped again (the default-queue run made no progress in 180 s)."""
+    _forced_match(8, "tiny-wide", 3e-2, {"GPU_MAX_HW_QUEUES": "1"})
 
 
 def test_mixed_prefill_decode_steps_match_separate(native_lib):
