@@ -29,6 +29,8 @@
 //   once, in bf16.
 // delta = rowsum(dO * O) is computed by the dQ kernel (its dO rows are in registers) and read by
 // the dK/dV kernel launched after it.
+#include <cstdlib>
+
 #include "attn_common.h"
 
 namespace llmctl {
@@ -80,6 +82,8 @@ struct BwdArgs {
   // dS = p dP', no per-element subtract or LSE scaling)
   float* rck_w;
   long rc_n;
+  // diagnostic timeline (fa_bwd_ablate abl 6 only): per workgroup 8 x u64, see the pipelined kernel
+  unsigned long long* stamps = nullptr;
 };
 
 // dK^T / dV^T accumulation pinned to AGPRs: through the builtin, hipcc kept these 128 registers
@@ -451,6 +455,721 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_kernel(BwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// dK / dV, software-pipelined (round 3).  Same work decomposition, LDS ring and register-resident
+// K / V as fa_bwd_dkv_kernel, but the per-tile program is reordered so the matrix pipe is never
+// idle behind the softmax VALU of the same wave.  PMC of the kernel above (B12 S2048 H32 D128,
+// profiles/attn_pmc_r3.txt): MFMA busy 28 %, the wave stalled on issue 46 % and on waits 21 % of
+// its cycles — one wave per SIMD, every phase (fragment reads -> S/dP MFMAs -> softmax ->
+// dV/dK MFMAs) serialised behind the previous one.  Here, per 64-row tile (halves 0 / 1):
+//     R0  S0/dP0 (16 MFMA)  R1  X: S1/dP1 (16 MFMA) || softmax(half 0)
+//     T0  Y: dV/dK(half 0) (16 MFMA) || softmax(half 1)   T1  dV/dK(half 1) (16 MFMA)
+// where R = Q / dO fragment + row-constant reads, T = transposed fragment reads.  X and Y are
+// inline-asm statements of two MFMAs plus the softmax of two scores (p = exp2(c s'),
+// ds = p dp', bf16 pairs): asm volatile keeps their order, so each MFMA's 32 issue cycles hide
+// ~8 VALU instructions of the other half instead of the VALU waiting for the pipe to drain.
+// Hazards (hipcc pads none inside asm): the exp results are read two instructions after their
+// v_exp (trans -> VALU), the S/dP results are read by VALU >= 2 MFMAs after the last MFMA that
+// wrote them, and the packed P / dS words are read by MFMAs >= 3 statements after their cvt.
+using s2_t = __attribute__((ext_vector_type(2))) unsigned int;
+
+__device__ __forceinline__ bf16x8_t words8(unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
+  using u4 = __attribute__((ext_vector_type(4))) unsigned;
+  return __builtin_bit_cast(bf16x8_t, u4{w0, w1, w2, w3});
+}
+
+__device__ __forceinline__ void mfma_v(f32x16& acc, bf16x8_t a, bf16x8_t b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b) : "memory");
+}
+
+// X: acc_s += a_s b_s, acc_d += a_d b_d (VGPR accumulators; b_s / b_d = the wave's K / V
+// fragments, AGPR-resident) || softmax of (s0, s1) with dp (d0, d1).  The "memory" clobber pins the
+// fragment reads placed between the statements (the next phase's operands stream in under these
+// MFMAs instead of being hoisted into one burst).
+__device__ __forceinline__ void x_step(f32x16& acc_s, f32x16& acc_d, bf16x8_t a_s, bf16x8_t b_s, bf16x8_t a_d,
+                                       bf16x8_t b_d, float s0, float s1, float d0, float d1, float c, unsigned& pw,
+                                       unsigned& dw) {
+  float t0, t1, p0, p1;
+  asm volatile(
+      "v_mul_f32 %[t0], %[c], %[s0]\n\t"
+      "v_mul_f32 %[t1], %[c], %[s1]\n\t"
+      "v_mfma_f32_32x32x16_bf16 %[as], %[xs], %[ys], %[as]\n\t"
+      "v_exp_f32 %[p0], %[t0]\n\t"
+      "v_exp_f32 %[p1], %[t1]\n\t"
+      "v_mfma_f32_32x32x16_bf16 %[ad], %[xd], %[yd], %[ad]\n\t"
+      "v_mul_f32 %[t0], %[p0], %[d0]\n\t"
+      "v_mul_f32 %[t1], %[p1], %[d1]\n\t"
+      "v_cvt_pk_bf16_f32 %[pw], %[p0], %[p1]\n\t"
+      "v_cvt_pk_bf16_f32 %[dw], %[t0], %[t1]"
+      : [as] "+v"(acc_s), [ad] "+v"(acc_d), [t0] "=&v"(t0), [t1] "=&v"(t1), [p0] "=&v"(p0), [p1] "=&v"(p1),
+        [pw] "=&v"(pw), [dw] "=&v"(dw)
+      : [xs] "v"(a_s), [ys] "a"(b_s), [xd] "v"(a_d), [yd] "a"(b_d), [s0] "v"(s0), [s1] "v"(s1), [d0] "v"(d0),
+        [d1] "v"(d1), [c] "s"(c)
+      : "memory");
+}
+
+// Y: dv += da p, dk += qa ds (AGPR accumulators) || softmax of (s0, s1) with dp (d0, d1)
+__device__ __forceinline__ void y_step(f32x16& dv, f32x16& dk, bf16x8_t da, bf16x8_t qa, bf16x8_t p, bf16x8_t ds,
+                                       float s0, float s1, float d0, float d1, float c, unsigned& pw, unsigned& dw) {
+  float t0, t1, p0, p1;
+  asm volatile(
+      "v_mul_f32 %[t0], %[c], %[s0]\n\t"
+      "v_mul_f32 %[t1], %[c], %[s1]\n\t"
+      "v_mfma_f32_32x32x16_bf16 %[dv], %[da], %[p], %[dv]\n\t"
+      "v_exp_f32 %[p0], %[t0]\n\t"
+      "v_exp_f32 %[p1], %[t1]\n\t"
+      "v_mfma_f32_32x32x16_bf16 %[dk], %[qa], %[ds], %[dk]\n\t"
+      "v_mul_f32 %[t0], %[p0], %[d0]\n\t"
+      "v_mul_f32 %[t1], %[p1], %[d1]\n\t"
+      "v_cvt_pk_bf16_f32 %[pw], %[p0], %[p1]\n\t"
+      "v_cvt_pk_bf16_f32 %[dw], %[t0], %[t1]"
+      : [dv] "+a"(dv), [dk] "+a"(dk), [t0] "=&v"(t0), [t1] "=&v"(t1), [p0] "=&v"(p0), [p1] "=&v"(p1),
+        [pw] "=&v"(pw), [dw] "=&v"(dw)
+      : [da] "v"(da), [qa] "v"(qa), [p] "v"(p), [ds] "v"(ds), [s0] "v"(s0), [s1] "v"(s1), [d0] "v"(d0),
+        [d1] "v"(d1), [c] "s"(c)
+      : "memory");
+}
+
+// AGPR accumulator tuple -> VGPR copy for an epilogue, and in-place zeroing through the matrix pipe
+// (0 * 0 + 0): the compiler never writes the dK / dV AGPRs itself (a C++ write made hipcc keep them
+// in VGPRs and copy them around every asm use)
+__device__ __forceinline__ f32x16 acc_copy(const f32x16& acc) {
+  // plain reads (v_accvgpr_read); the asm statement only orders them and keeps the stores after it
+  f32x16 out = acc;
+  asm volatile("" : "+v"(out)::"memory");
+  return out;
+}
+__device__ __forceinline__ void acc_zero(f32x16& acc) {  // in place ("+a": no second register set)
+  const bf16x8_t z = {};  // MFMA A / B take no inline constants, C does
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "+a"(acc) : "v"(z));
+}
+
+// dV / dK of one 16-row step with no softmax work beside it (the previous tile's second half)
+__device__ __forceinline__ void z_step(f32x16& dv, f32x16& dk, bf16x8_t da, bf16x8_t qa, bf16x8_t p, bf16x8_t ds) {
+  asm volatile(
+      "v_mfma_f32_32x32x16_bf16 %[dv], %[da], %[p], %[dv]\n\t"
+      "v_mfma_f32_32x32x16_bf16 %[dk], %[qa], %[ds], %[dk]"
+      : [dv] "+a"(dv), [dk] "+a"(dk)
+      : [da] "v"(da), [qa] "v"(qa), [p] "v"(p), [ds] "v"(ds)
+      : "memory");
+}
+
+template <int HD, bool CAUSAL, bool DOC, bool STAMP = false>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkv_pipe_kernel(BwdArgs a) {
+  static_assert(HD == 128 && CAUSAL, "pipelined dK/dV kernel: causal, head_dim 128");
+  constexpr int NKS = HD / 16;
+  constexpr int NDB = HD / 32;
+  constexpr int ROWB = HD * 2;
+  constexpr int TILE_B = KV_QT * ROWB;
+  constexpr int NP = TILE_B / 1024 / 4;
+  constexpr int RC_B = KV_QT * 4;
+  constexpr int BUF_B = 2 * TILE_B + 4 * RC_B;  // Q | dO | lse | delta | doc | (pad)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF_B];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  // STAMP: [0] entry, [1] HW_ID | XCC_ID << 32, [2] prologue done, [3] tile loop done, [4] epilogue
+  // stores retired, [5] tiles (constant-rate s_memrealtime, 100 MHz; workgroup's thread 0)
+  auto stamp = [&](int i) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      if (tid == 0) a.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  stamp(0);
+  if constexpr (STAMP) {
+    if (tid == 0)
+      a.stamps[blockIdx.x * 8 + 1] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(63492) |
+                                     ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(63508) << 32);
+  }
+  const int nkb = (a.S + KV_KB - 1) / KV_KB;
+  const int BH = a.B * a.Hkv;
+  int bh, kblk;
+  if (BH % 8) {
+    bh = blockIdx.x % BH;
+    kblk = blockIdx.x / BH;
+  } else {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    bh = x * (BH >> 3) + j / nkb;
+    kblk = j % nkb;
+  }
+  const int b = bh / a.Hkv, hk = bh % a.Hkv;
+  const int group = a.Hq / a.Hkv;
+  const int k0 = kblk * KV_KB;
+  const int wkey0 = k0 + wave * 32;
+  const int my_key = wkey0 + r;
+
+  if (a.S % KV_QT) {  // partial tiles: rows past S stay unwritten by the DMA and must read finite
+#pragma unroll
+    for (int i = 0; i < 2 * BUF_B / 4096; ++i)
+      *reinterpret_cast<uint4*>(smem + i * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
+    if (tid < (2 * BUF_B % 4096) / 16)
+      *reinterpret_cast<uint4*>(smem + (2 * BUF_B / 4096) * 4096 + tid * 16) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+  }
+
+  const unsigned lds0 = lds_addr(smem);
+
+  f32x16 dk[NDB], dv[NDB];
+#pragma unroll
+  for (int d = 0; d < NDB; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[d][i] = dv[d][i] = 0.f;
+
+  const int q_start = CAUSAL ? k0 : 0;
+  int q_end = a.S;
+  if constexpr (DOC) {
+    const int* ds = a.doc + (long)b * a.S;
+    int lo = min(k0 + KV_KB, a.S), hi = a.S;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ds[mid] > k0 + KV_KB - 1) hi = mid;
+      else lo = mid + 1;
+    }
+    q_end = __builtin_amdgcn_readfirstlane(lo);
+  }
+  const int nq = q_end > q_start ? (q_end - q_start + KV_QT - 1) / KV_QT : 0;
+  const int ntiles = group * nq;
+  unsigned vq[NP], vd[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int byte = (i * 4 + wave) * 1024 + lane * 16;
+    const int row = byte / ROWB;
+    const int lch = ((byte % ROWB) >> 4) ^ swz_tr<HD>(row);
+    vq[i] = (unsigned)((row * a.q_ss + lch * 8) * 2);
+    vd[i] = (unsigned)((row * a.do_ss + lch * 8) * 2);
+  }
+  const float* rc_src = a.rck_w + (wave == 1 ? a.rc_n : 0);
+  const unsigned rc_off =
+      (DOC && wave == 2) ? lane * 4
+                         : (unsigned)((32 * (lane >> 5) + 8 * ((lane >> 2) & 3) + 4 * ((lane >> 4) & 1) + (lane & 3)) * 4);
+  int iq0 = q_start;
+  const unsigned short* qh = a.q + b * a.q_sb + (long)(hk * group) * a.q_sh;
+  const unsigned short* dh = a.dout + b * a.do_sb + (long)(hk * group) * a.do_sh;
+  const float* rh = rc_src + ((long)b * a.Hq + hk * group) * a.S;
+  const unsigned short* qc = qh + (long)q_start * a.q_ss;
+  const unsigned short* dc = dh + (long)q_start * a.do_ss;
+  const long q_step = (long)KV_QT * a.q_ss, d_step = (long)KV_QT * a.do_ss;
+  auto issue = [&](auto slot_c) __attribute__((always_inline)) {
+    constexpr int SLC = decltype(slot_c)::value;
+    const int nr = min(KV_QT, a.S - iq0);
+    i32x4_t rq = buf_rsrc(qc, (unsigned)(((nr - 1) * a.q_ss + HD) * 2));
+    i32x4_t rd = buf_rsrc(dc, (unsigned)(((nr - 1) * a.do_ss + HD) * 2));
+    i32x4_t rr = (DOC && wave == 2) ? buf_rsrc(a.doc + (long)b * a.S + iq0, (unsigned)(nr * 4))
+                                    : buf_rsrc(rh + iq0, (unsigned)(nr * 4));
+    asm volatile("s_nop 4" : "+s"(rq), "+s"(rd), "+s"(rr));
+    const unsigned slot = lds0 + (unsigned)(SLC * BUF_B);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      buf_dma16(rq, vq[i], slot + (i * 4 + wave) * 1024);
+      buf_dma16(rd, vd[i], slot + TILE_B + (i * 4 + wave) * 1024);
+    }
+    buf_dma4(rr, rc_off, slot + 2 * TILE_B + wave * RC_B);
+    iq0 += KV_QT;
+    qc += q_step;
+    dc += d_step;
+    if (iq0 >= q_end) {
+      iq0 = q_start;
+      qh += a.q_sh;
+      dh += a.do_sh;
+      rh += a.S;
+      qc = qh + (long)q_start * a.q_ss;
+      dc = dh + (long)q_start * a.do_ss;
+    }
+  };
+
+  const float c = a.scale_log2;
+  // masked scores of half h (rows 32h..32h+31 of the tile starting at q0): -inf where invisible
+  auto apply_mask = [&](f32x16& s, int h, int q0, const int* doc_s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int row0 = 32 * h + 8 * gq + 4 * hh;
+      int sv[4] = {0, 0, 0, 0};
+      if constexpr (DOC) {
+        const int4 s4 = *reinterpret_cast<const int4*>(doc_s + row0);
+        sv[0] = s4.x; sv[1] = s4.y; sv[2] = s4.z; sv[3] = s4.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int qq = q0 + row0 + j;
+        bool ok = qq < a.S && my_key < a.S;
+        if constexpr (CAUSAL) ok = ok && my_key <= qq;
+        if constexpr (DOC) ok = ok && my_key >= sv[j];
+        s[4 * gq + j] = ok ? s[4 * gq + j] : -INFINITY;
+      }
+    }
+  };
+
+  // prologue: tile 0's DMA first, the K / V fragments under it (both latencies overlap), one wait
+  if (ntiles > 0) issue(std::integral_constant<int, 0>{});
+  // the wave's K / V fragments, loaded straight into AGPRs (every use is an MFMA B operand with an
+  // "a" constraint, so they never occupy VGPRs and need no per-use copy)
+  bf16x8_t kf[NKS], vf[NKS];
+  {
+    const int kc = min(my_key, a.S - 1);
+    const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh + (long)kc * a.k_ss + 8 * hh;
+    const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh + (long)kc * a.v_ss + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(kf[ks]) : "v"(Kp + 16 * ks) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(vf[ks]) : "v"(Vp + 16 * ks) : "memory");
+    }
+  }
+  vm_wait_n<0>();
+  __builtin_amdgcn_s_barrier();
+  stamp(2);
+  if (ntiles > 1) issue(std::integral_constant<int, 1>{});
+  int qi = 0;
+  auto tile = [&](auto slot_c, int t) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot_c)::value;
+    const int q0 = q_start + qi * KV_QT;
+    if (++qi == nq) qi = 0;
+    const bool live = !(CAUSAL && wkey0 > q0 + KV_QT - 1);
+    const unsigned char* Qs = smem + SL * BUF_B;
+    const unsigned char* Ds = Qs + TILE_B;
+    const float* lse_s = reinterpret_cast<const float*>(Ds + TILE_B);
+    const float* del_s = lse_s + KV_QT;
+    const int* doc_s = reinterpret_cast<const int*>(del_s + KV_QT);
+    if (!live) return;
+    // ---- R0: row constants first (the first MFMA's accumulators), then the fragments
+    f32x16 s0 = *reinterpret_cast<const f32x16*>(lse_s + 16 * hh);
+    f32x16 p0 = *reinterpret_cast<const f32x16*>(del_s + 16 * hh);
+    bf16x8_t qa[NKS], da[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      qa[ks] = lds_read_b128(Qs, tr_off<HD>(r, 2 * ks + hh));
+      da[ks] = lds_read_b128(Ds, tr_off<HD>(r, 2 * ks + hh));
+    }
+    const bool need_mask = DOC || (CAUSAL && wkey0 + 31 > q0) || (q0 + KV_QT > a.S) || (wkey0 + 31 >= a.S);
+    // ---- S0 / dP0
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      mfma_v(s0, qa[ks], kf[ks]);
+      mfma_v(p0, da[ks], vf[ks]);
+    }
+    // ---- R1, then X: S1 / dP1 || softmax of half 0, with the half-0 transposed fragments (T0)
+    //      read two per statement
+    f32x16 s1 = *reinterpret_cast<const f32x16*>(lse_s + 32 + 16 * hh);
+    f32x16 p1 = *reinterpret_cast<const f32x16*>(del_s + 32 + 16 * hh);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      qa[ks] = lds_read_b128(Qs, tr_off<HD>(32 + r, 2 * ks + hh));
+      da[ks] = lds_read_b128(Ds, tr_off<HD>(32 + r, 2 * ks + hh));
+    }
+    if (need_mask) apply_mask(s0, 0, q0, doc_s);
+    unsigned pw0[8], dw0[8];
+    bf16x8_t td[2][NDB], tq[2][NDB];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      x_step(s1, p1, qa[ks], kf[ks], da[ks], vf[ks], s0[2 * ks], s0[2 * ks + 1], p0[2 * ks], p0[2 * ks + 1], c, pw0[ks],
+             dw0[ks]);
+      const int st = ks >> 2, d = ks & 3;
+      td[st][d] = tr_frag<HD>(Ds, 16 * st, d * 32, lane);
+      tq[st][d] = tr_frag<HD>(Qs, 16 * st, d * 32, lane);
+    }
+    // ---- Y: dV / dK (half 0) || softmax of half 1, with the half-1 transposed fragments (T1)
+    if (need_mask) apply_mask(s1, 1, q0, doc_s);
+    unsigned pw1[8], dw1[8];
+    bf16x8_t cd[2][NDB], cq[2][NDB];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8_t pb = words8(pw0[4 * st], pw0[4 * st + 1], pw0[4 * st + 2], pw0[4 * st + 3]);
+      const bf16x8_t sb = words8(dw0[4 * st], dw0[4 * st + 1], dw0[4 * st + 2], dw0[4 * st + 3]);
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) {
+        const int i = 4 * st + d;
+        y_step(dv[d], dk[d], td[st][d], tq[st][d], pb, sb, s1[2 * i], s1[2 * i + 1], p1[2 * i], p1[2 * i + 1], c,
+               pw1[i], dw1[i]);
+        cd[st][d] = tr_frag<HD>(Ds, 32 + 16 * st, d * 32, lane);
+        cq[st][d] = tr_frag<HD>(Qs, 32 + 16 * st, d * 32, lane);
+      }
+    }
+    // ---- dV / dK (half 1): MFMAs only; the pipe drains into the barrier
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8_t pb = words8(pw1[4 * st], pw1[4 * st + 1], pw1[4 * st + 2], pw1[4 * st + 3]);
+      const bf16x8_t sb = words8(dw1[4 * st], dw1[4 * st + 1], dw1[4 * st + 2], dw1[4 * st + 3]);
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) z_step(dv[d], dk[d], cd[st][d], cq[st][d], pb, sb);
+    }
+  };
+  // after each tile: every wave's reads of its slot retired and tile t+1's DMA landed ->
+  // barrier, then the slot takes tile t+2
+  auto advance = [&](auto slot_c, int t) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    vm_wait_n<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < ntiles) issue(std::integral_constant<int, SL>{});
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    advance(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) {
+      tile(std::integral_constant<int, 1>{}, t + 1);
+      advance(std::integral_constant<int, 1>{}, t + 1);
+    }
+  }
+  stamp(3);
+#pragma unroll
+  for (int d = 0; d < NDB; ++d) asm volatile("s_nop 7\n\ts_nop 7" : "+a"(dk[d]), "+a"(dv[d]));
+  if (my_key < a.S) {
+    const long tok = (long)b * a.S + my_key;
+    unsigned short* dkp = a.dk + tok * a.dk_st + (long)hk * HD;
+    unsigned short* dvp = a.dv + tok * a.dv_st + (long)hk * HD;
+    const float *cr = nullptr, *sr = nullptr;
+    if (a.cos_t != nullptr) {
+      const long p = a.rope_pos ? (long)a.rope_pos[tok] : tok % a.rope_S;
+      cr = a.cos_t + p * (HD / 2);
+      sr = a.sin_t + p * (HD / 2);
+    }
+    store_row<HD>(dkp, dk, a.scale, hh, cr, sr);
+    store_row<HD>(dvp, dv, 1.f, hh, nullptr, nullptr);
+  }
+  if constexpr (STAMP) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stamp(4);
+    if (tid == 0) a.stamps[blockIdx.x * 8 + 5] = (unsigned long long)ntiles;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dK / dV, persistent (round 3).  A timeline of fa_bwd_dkv_pipe_kernel (s_memrealtime stamps,
+// tools/dkv_timeline.py, profiles/attn_dkv_r3.txt) at B12 S2048 H32: per workgroup 4.9 us of
+// prologue (K / V + first tile), 4.6 us of epilogue and a 6.1 us gap before the CU's next
+// workgroup starts, against 2.2 us per 64-row tile and 17 tiles per workgroup on average: ~30 %
+// of the kernel outside the tile loop.  Here one workgroup per CU stays resident and takes
+// (batch * kv-head, key-block) items from a per-XCD work queue (one atomic per item; queue x =
+// blockIdx % 8 holds its heads' items head-major, heaviest key block first, so the ~32 concurrent
+// items of an XCD share two or three heads' Q / dO in its L2 while the dynamic order balances the
+// causal costs).  The Q / dO DMA stream runs on across items (the next item's first tiles land
+// under the current item's last ones), the next item's K / V fragments load under the last tile's
+// products, and the barrier sits before the second-half dV / dK MFMAs so the next tile's first
+// fragment reads land under them.  Scope: causal, head_dim 128, S % 128 == 0, no packed documents
+// (every item then has >= 2 tiles, which bounds the issue cursor's lead to two items).
+// wq: int32[8] per-XCD item counters, zeroed by the host before every launch.
+template <bool STAMP>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, int* __restrict__ wq) {
+  constexpr int HD = 128;
+  constexpr int NKS = HD / 16;
+  constexpr int NDB = HD / 32;
+  constexpr int ROWB = HD * 2;
+  constexpr int TILE_B = KV_QT * ROWB;
+  constexpr int NP = TILE_B / 1024 / 4;
+  constexpr int RC_B = KV_QT * 4;
+  constexpr int BUF_B = 2 * TILE_B + 4 * RC_B;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF_B + 64];
+  // item ids handed from thread 0 to the workgroup: [0] the lookahead popped after a cursor switch
+  // (written after a barrier, read after the next one; switches are >= 2 barriers apart), [1] [2]
+  // the first two items
+  int* item_w = reinterpret_cast<int*>(smem + 2 * BUF_B);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int nkb = a.S / KV_KB;
+  const int BH = a.B * a.Hkv;
+  const bool per_xcd = BH % 8 == 0;
+  const int xq = per_xcd ? (int)(blockIdx.x & 7) : 0;
+  const int n_items = (per_xcd ? BH / 8 : BH) * nkb;
+  const int bh_base = per_xcd ? xq * (BH / 8) : 0;
+  const int group = a.Hq / a.Hkv;
+  auto pop = [&]() __attribute__((always_inline)) -> int {  // thread 0
+    const int j = __hip_atomic_fetch_add(wq + xq, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return j < n_items ? j : -1;
+  };
+  if (tid == 0) {
+    const int i0 = pop();
+    item_w[1] = i0;
+    item_w[2] = i0 >= 0 ? pop() : -1;
+  }
+  __syncthreads();
+  int cur = __builtin_amdgcn_readfirstlane(item_w[1]);
+  int nxt = __builtin_amdgcn_readfirstlane(item_w[2]);
+  if (cur < 0) return;
+
+  const unsigned lds0 = lds_addr(smem);
+  unsigned vq[NP], vd[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int byte = (i * 4 + wave) * 1024 + lane * 16;
+    const int row = byte / ROWB;
+    const int lch = ((byte % ROWB) >> 4) ^ swz_tr<HD>(row);
+    vq[i] = (unsigned)((row * a.q_ss + lch * 8) * 2);
+    vd[i] = (unsigned)((row * a.do_ss + lch * 8) * 2);
+  }
+  const float* rc_src = a.rck_w + (wave == 1 ? a.rc_n : 0);
+  const unsigned rc_off =
+      (unsigned)((32 * (lane >> 5) + 8 * ((lane >> 2) & 3) + 4 * ((lane >> 4) & 1) + (lane & 3)) * 4);
+
+  // ---- issue cursor: the Q / dO / row-constant DMA stream over (item, q-head of the GQA group, tile)
+  int iss = cur, iq0 = 0, iq_start = 0, ig = 0;
+  const unsigned short *qh = nullptr, *dh = nullptr;
+  const float* rh = nullptr;
+  bool look_pending = false;
+  int pend_item = -1;  // the item the cursor entered while compute is still on the previous one
+  auto iss_begin = [&](int item) __attribute__((always_inline)) {
+    const int bh = bh_base + item / nkb, kb = item % nkb;
+    const int bb = bh / a.Hkv, hkk = bh % a.Hkv;
+    iq_start = kb * KV_KB;
+    iq0 = iq_start;
+    ig = 0;
+    qh = a.q + bb * a.q_sb + (long)(hkk * group) * a.q_sh;
+    dh = a.dout + bb * a.do_sb + (long)(hkk * group) * a.do_sh;
+    rh = rc_src + ((long)bb * a.Hq + hkk * group) * a.S;
+  };
+  iss_begin(cur);
+  auto issue = [&](auto slot_c) __attribute__((always_inline)) {
+    constexpr int SLC = decltype(slot_c)::value;
+    i32x4_t rq = buf_rsrc(qh + (long)iq0 * a.q_ss, (unsigned)(((KV_QT - 1) * a.q_ss + HD) * 2));
+    i32x4_t rd = buf_rsrc(dh + (long)iq0 * a.do_ss, (unsigned)(((KV_QT - 1) * a.do_ss + HD) * 2));
+    i32x4_t rr = buf_rsrc(rh + iq0, (unsigned)(KV_QT * 4));
+    asm volatile("s_nop 4" : "+s"(rq), "+s"(rd), "+s"(rr));
+    const unsigned slot = lds0 + (unsigned)(SLC * BUF_B);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      buf_dma16(rq, vq[i], slot + (i * 4 + wave) * 1024);
+      buf_dma16(rd, vd[i], slot + TILE_B + (i * 4 + wave) * 1024);
+    }
+    buf_dma4(rr, rc_off, slot + 2 * TILE_B + wave * RC_B);
+    iq0 += KV_QT;
+    if (iq0 >= a.S) {
+      if (++ig < group) {  // next q-head of the GQA group
+        iq0 = iq_start;
+        qh += a.q_sh;
+        dh += a.do_sh;
+        rh += a.S;
+      } else {  // next item: it becomes the compute side's next item, thread 0 pops a lookahead
+        iss = nxt;
+        if (iss >= 0) {
+          iss_begin(iss);
+          if (tid == 0) item_w[0] = pop();
+          look_pending = true;
+        }
+        pend_item = iss;
+      }
+    }
+  };
+
+  bf16x8_t kf[NKS], vf[NKS];
+  auto load_kv = [&](int item) __attribute__((always_inline)) {
+    const int bh = bh_base + item / nkb, kb = item % nkb;
+    const int bb = bh / a.Hkv, hkk = bh % a.Hkv;
+    const int key = kb * KV_KB + wave * 32 + r;
+    const unsigned short* Kp = a.k + bb * a.k_sb + hkk * a.k_sh + (long)key * a.k_ss + 8 * hh;
+    const unsigned short* Vp = a.v + bb * a.v_sb + hkk * a.v_sh + (long)key * a.v_ss + 8 * hh;
+    // "+a": the new fragments overwrite the old ones in place (no second register set)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      asm volatile("global_load_dwordx4 %0, %1, off" : "+a"(kf[ks]) : "v"(Kp + 16 * ks) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off" : "+a"(vf[ks]) : "v"(Vp + 16 * ks) : "memory");
+    }
+  };
+
+  // prologue: tile 0's DMA with the K / V fragments under it, one wait, then tile 1's DMA
+  issue(std::integral_constant<int, 0>{});
+  load_kv(cur);
+  vm_wait_n<0>();
+  __builtin_amdgcn_s_barrier();
+  issue(std::integral_constant<int, 1>{});
+  f32x16 dk[NDB], dv[NDB];
+#pragma unroll
+  for (int d = 0; d < NDB; ++d) {
+    const bf16x8_t z = {};
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(dk[d]) : "v"(z));
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(dv[d]) : "v"(z));
+  }
+  const float c = a.scale_log2;
+
+  int n_done = 0;  // STAMP: items finished by this workgroup
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      if (tid == 0 && n_done < 64)
+        a.stamps[(blockIdx.x * 64 + n_done) * 4 + k] = k == 3 ? (unsigned long long)cur : __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  for (;;) {  // ---- items
+    stamp(0);
+    stamp(3);
+    const int bh = bh_base + cur / nkb, kb = cur % nkb;
+    const int b = bh / a.Hkv, hk = bh % a.Hkv;
+    const int k0 = kb * KV_KB;
+    const int wkey0 = k0 + wave * 32;
+    const int my_key = wkey0 + r;
+    const int ntiles = group * ((a.S - k0) / KV_QT);  // even
+    int q0 = k0;
+    auto apply_mask = [&](f32x16& s, int h) __attribute__((always_inline)) {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int row0 = q0 + 32 * h + 8 * gq + 4 * hh;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[4 * gq + j] = my_key <= row0 + j ? s[4 * gq + j] : -INFINITY;
+      }
+    };
+    // one tile in ring slot SL (as fa_bwd_dkv_pipe_kernel)
+    auto tile = [&](auto slot_c) __attribute__((always_inline)) {
+      constexpr int SL = decltype(slot_c)::value;
+      const bool live = !(wkey0 > q0 + KV_QT - 1);
+      if (!live) return;
+      const unsigned char* Qs = smem + SL * BUF_B;
+      const unsigned char* Ds = Qs + TILE_B;
+      const float* lse_s = reinterpret_cast<const float*>(Ds + TILE_B);
+      const float* del_s = lse_s + KV_QT;
+      const bool need_mask = wkey0 + 31 > q0;
+      f32x16 s0 = *reinterpret_cast<const f32x16*>(lse_s + 16 * hh);
+      f32x16 p0 = *reinterpret_cast<const f32x16*>(del_s + 16 * hh);
+      bf16x8_t qa[NKS], da[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        qa[ks] = lds_read_b128(Qs, tr_off<HD>(r, 2 * ks + hh));
+        da[ks] = lds_read_b128(Ds, tr_off<HD>(r, 2 * ks + hh));
+      }
+      f32x16 s1 = *reinterpret_cast<const f32x16*>(lse_s + 32 + 16 * hh);
+      f32x16 p1 = *reinterpret_cast<const f32x16*>(del_s + 32 + 16 * hh);
+      bf16x8_t qb[NKS], db[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {  // S0 / dP0 with the second half's fragment reads
+        mfma_v(s0, qa[ks], kf[ks]);
+        qb[ks] = lds_read_b128(Qs, tr_off<HD>(32 + r, 2 * ks + hh));
+        mfma_v(p0, da[ks], vf[ks]);
+        db[ks] = lds_read_b128(Ds, tr_off<HD>(32 + r, 2 * ks + hh));
+      }
+      if (need_mask) apply_mask(s0, 0);
+      unsigned pw0[8], dw0[8];
+      bf16x8_t td[2][NDB], tq[2][NDB];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {  // X: S1 / dP1 || softmax(half 0), T0 reads
+        x_step(s1, p1, qb[ks], kf[ks], db[ks], vf[ks], s0[2 * ks], s0[2 * ks + 1], p0[2 * ks], p0[2 * ks + 1], c,
+               pw0[ks], dw0[ks]);
+        const int st = ks >> 2, d = ks & 3;
+        td[st][d] = tr_frag<HD>(Ds, 16 * st, d * 32, lane);
+        tq[st][d] = tr_frag<HD>(Qs, 16 * st, d * 32, lane);
+      }
+      if (need_mask) apply_mask(s1, 1);
+      unsigned pw1[8], dw1[8];
+      bf16x8_t cd[2][NDB], cq[2][NDB];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {  // Y: dV / dK(half 0) || softmax(half 1), T1 reads
+        const bf16x8_t pb = words8(pw0[4 * st], pw0[4 * st + 1], pw0[4 * st + 2], pw0[4 * st + 3]);
+        const bf16x8_t sb = words8(dw0[4 * st], dw0[4 * st + 1], dw0[4 * st + 2], dw0[4 * st + 3]);
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) {
+          const int i = 4 * st + d;
+          y_step(dv[d], dk[d], td[st][d], tq[st][d], pb, sb, s1[2 * i], s1[2 * i + 1], p1[2 * i], p1[2 * i + 1], c,
+                 pw1[i], dw1[i]);
+          cd[st][d] = tr_frag<HD>(Ds, 32 + 16 * st, d * 32, lane);
+          cq[st][d] = tr_frag<HD>(Qs, 32 + 16 * st, d * 32, lane);
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {  // dV / dK (half 1)
+        const bf16x8_t pb = words8(pw1[4 * st], pw1[4 * st + 1], pw1[4 * st + 2], pw1[4 * st + 3]);
+        const bf16x8_t sb = words8(dw1[4 * st], dw1[4 * st + 1], dw1[4 * st + 2], dw1[4 * st + 3]);
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) z_step(dv[d], dk[d], cd[st][d], cq[st][d], pb, sb);
+      }
+    };
+    // after each tile: reads of its slot retired, the next tile's DMA landed -> barrier; the slot
+    // takes the stream's tile two ahead (maybe the next item's)
+    auto advance = [&](auto slot_c) __attribute__((always_inline)) {
+      constexpr int SL = decltype(slot_c)::value;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      vm_wait_n<0>();
+      __builtin_amdgcn_s_barrier();
+      if (look_pending) {
+        nxt = __builtin_amdgcn_readfirstlane(item_w[0]);
+        look_pending = false;
+      }
+      if (iss >= 0) issue(std::integral_constant<int, SL>{});
+      q0 += KV_QT;
+      if (q0 >= a.S) q0 = k0;  // next q-head of the GQA group
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(std::integral_constant<int, 0>{});
+      advance(std::integral_constant<int, 0>{});
+      tile(std::integral_constant<int, 1>{});
+      advance(std::integral_constant<int, 1>{});
+    }
+    stamp(1);
+    // ---- item end: the next item's K / V fragments load under this item's epilogue (dK scaled with
+    //      the RoPE backward fused, dV).  Its memory operations are inline asm with a fixed count
+    //      per wave, so counted waits separate them: vmcnt(16) = the RoPE tables landed (the 16 K / V
+    //      loads after them may fly), vmcnt(32) after the 32 stores = the K / V fragments landed.
+    {
+      const long tok = (long)b * a.S + my_key;
+      unsigned short* dkp = a.dk + tok * a.dk_st + (long)hk * HD;
+      unsigned short* dvp = a.dv + tok * a.dv_st + (long)hk * HD;
+      const bool rope = a.cos_t != nullptr;
+      f32x4 cs[NDB / 2][4], sn[NDB / 2][4];
+      if (rope) {
+        const long p = a.rope_pos ? (long)a.rope_pos[tok] : tok % a.rope_S;
+        const float* cr = a.cos_t + p * (HD / 2);
+        const float* sr = a.sin_t + p * (HD / 2);
+#pragma unroll
+        for (int d = 0; d < NDB / 2; ++d)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int col = d * 32 + 8 * g + 4 * hh;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(cs[d][g]) : "v"(cr + col) : "memory");
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(sn[d][g]) : "v"(sr + col) : "memory");
+          }
+      }
+      load_kv(pend_item >= 0 ? pend_item : cur);  // one code path (no next item: a harmless re-load)
+      if (rope) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      // the last MFMAs' results -> the AGPR reads below: 8-pass XDL write, 12+ wait states; the "+a"
+      // operands order every read after the padding
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) asm volatile("s_nop 7\n\ts_nop 7" : "+a"(dk[d]), "+a"(dv[d]));
+      auto st8 = [&](unsigned short* p, const float* x, float mul) __attribute__((always_inline)) {
+        s2_t w;
+        w[0] = (unsigned)f2bf(x[0] * mul) | ((unsigned)f2bf(x[1] * mul) << 16);
+        w[1] = (unsigned)f2bf(x[2] * mul) | ((unsigned)f2bf(x[3] * mul) << 16);
+        asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(w) : "memory");
+      };
+#pragma unroll
+      for (int d = 0; d < NDB / 2; ++d) {
+        const f32x16 x1 = acc_copy(dk[d]), x2 = acc_copy(dk[d + NDB / 2]);
+        acc_zero(dk[d]);
+        acc_zero(dk[d + NDB / 2]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = d * 32 + 8 * g + 4 * hh;  // < HD / 2
+          float lo[4], hi[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float c1 = rope ? cs[d][g][j] : 1.f, s1 = rope ? sn[d][g][j] : 0.f;
+            lo[j] = x1[4 * g + j] * c1 + x2[4 * g + j] * s1;
+            hi[j] = x2[4 * g + j] * c1 - x1[4 * g + j] * s1;
+          }
+          st8(dkp + col, lo, a.scale);
+          st8(dkp + col + HD / 2, hi, a.scale);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) {
+        const f32x16 x = acc_copy(dv[d]);
+        acc_zero(dv[d]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float y[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) y[j] = x[4 * g + j];
+          st8(dvp + d * 32 + 8 * g + 4 * hh, y, 1.f);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    }
+    stamp(2);
+    ++n_done;
+    if (pend_item < 0) break;  // the stream ended with this item
+    cur = pend_item;
+    pend_item = -1;
+  }
+}
+
 // =============================================================================================
 // dQ
 // =============================================================================================
@@ -653,30 +1372,73 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   }
 }
 
+// dK/dV kernel (A/B knob LLMCTL_DKV): 0 = unpipelined, 1 (default) = software-pipelined, 2 =
+// persistent where it applies (causal, head_dim 128, S % 128, no documents), else pipelined
+int dkv_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("LLMCTL_DKV");
+    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
+  }();
+  return m;
+}
+
+// the persistent dK/dV kernel's per-XCD item counters (one buffer per device, zeroed before every
+// launch on the launch's stream)
+int* dkv_queue() {
+  static int* q[64] = {nullptr};
+  int dev = 0;
+  LLMCTL_HIP_CHECK(hipGetDevice(&dev));
+  if (q[dev] == nullptr) LLMCTL_HIP_CHECK(hipMalloc(&q[dev], 64 * sizeof(int)));
+  return q[dev];
+}
+
+// dkv_impl: -1 = default (LLMCTL_DKV_PIPE), 0 = unpipelined kernel, 1 = pipelined where built
 template <int HD, bool CAUSAL, bool DOC>
-void launch_bwd(const BwdArgs& a, hipStream_t s, bool do_dq, bool do_dkv) {
+void launch_bwd(const BwdArgs& a, hipStream_t s, bool do_dq, bool do_dkv, int dkv_impl) {
   if (do_dq) {
     const int nqb = (a.S + DQ_QB - 1) / DQ_QB;
     hipLaunchKernelGGL((fa_bwd_dq_kernel<HD, CAUSAL, DOC>), dim3((unsigned)(a.B * a.Hq * nqb)), dim3(256), 0, s, a);
   }
   if (do_dkv) {
     const int nkb = (a.S + KV_KB - 1) / KV_KB;
-    hipLaunchKernelGGL((fa_bwd_dkv_kernel<HD, CAUSAL, DOC>), dim3((unsigned)(a.B * a.Hkv * nkb)), dim3(256), 0, s,
-                       a);
+    const dim3 grid((unsigned)(a.B * a.Hkv * nkb));
+    if constexpr (HD == 128 && CAUSAL) {  // the full-attention build spills (not the training path)
+      if (dkv_impl == 2 && a.stamps != nullptr) {
+        hipLaunchKernelGGL((fa_bwd_dkv_pipe_kernel<HD, CAUSAL, DOC, true>), grid, dim3(256), 0, s, a);
+        return;
+      }
+      if constexpr (!DOC) {  // persistent form: S % 128 (>= 2 tiles per item)
+        if (a.S % KV_KB == 0 && (dkv_impl == 3 || dkv_impl == 4 || (dkv_impl < 0 && dkv_mode() == 2))) {
+          int* wq = dkv_queue();
+          LLMCTL_HIP_CHECK(hipMemsetAsync(wq, 0, 8 * sizeof(int), s));
+          const int nwg = std::min<long>((long)num_cus(), (long)a.B * a.Hkv * nkb);
+          if (a.stamps != nullptr)
+            hipLaunchKernelGGL(fa_bwd_dkv_persist_kernel<true>, dim3((unsigned)nwg), dim3(256), 0, s, a, wq);
+          else
+            hipLaunchKernelGGL(fa_bwd_dkv_persist_kernel<false>, dim3((unsigned)nwg), dim3(256), 0, s, a, wq);
+          return;
+        }
+      }
+      if (dkv_impl == 1 || dkv_impl == 3 || (dkv_impl < 0 && dkv_mode() >= 1)) {
+        hipLaunchKernelGGL((fa_bwd_dkv_pipe_kernel<HD, CAUSAL, DOC>), grid, dim3(256), 0, s, a);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((fa_bwd_dkv_kernel<HD, CAUSAL, DOC>), grid, dim3(256), 0, s, a);
   }
 }
 
 void dispatch_bwd(const BwdArgs& a, int D, bool causal, bool doc, hipStream_t s, bool do_dq = true,
-                  bool do_dkv = true) {
+                  bool do_dkv = true, int dkv_impl = -1) {
   if (doc) {
-    if (D == 128) launch_bwd<128, true, true>(a, s, do_dq, do_dkv);
-    else launch_bwd<64, true, true>(a, s, do_dq, do_dkv);
+    if (D == 128) launch_bwd<128, true, true>(a, s, do_dq, do_dkv, dkv_impl);
+    else launch_bwd<64, true, true>(a, s, do_dq, do_dkv, dkv_impl);
   } else if (D == 128) {
-    if (causal) launch_bwd<128, true, false>(a, s, do_dq, do_dkv);
-    else launch_bwd<128, false, false>(a, s, do_dq, do_dkv);
+    if (causal) launch_bwd<128, true, false>(a, s, do_dq, do_dkv, dkv_impl);
+    else launch_bwd<128, false, false>(a, s, do_dq, do_dkv, dkv_impl);
   } else {
-    if (causal) launch_bwd<64, true, false>(a, s, do_dq, do_dkv);
-    else launch_bwd<64, false, false>(a, s, do_dq, do_dkv);
+    if (causal) launch_bwd<64, true, false>(a, s, do_dq, do_dkv, dkv_impl);
+    else launch_bwd<64, false, false>(a, s, do_dq, do_dkv, dkv_impl);
   }
 }
 
@@ -815,8 +1577,12 @@ at::Tensor flash_attn_bwd_qkv(const at::Tensor& dout, const at::Tensor& q, const
   return dqkv;
 }
 
-// timing-only entry for tools/attn_ablate.py (causal, no documents): abl 0 = both kernels,
-// 1 = dK/dV kernel only (its row constants prepared by two small torch ops), 2 = dQ kernel only.
+// timing / A-B entry for tools/attn_ablate.py and the GPU tests (causal, no documents): abl 0 = both
+// kernels, 1 = dK/dV kernel only (its row constants prepared by two small torch ops), 2 = dQ kernel
+// only, 3 / 4 = dK/dV only through the unpipelined / pipelined kernel, 5 = the pipelined kernel's
+// diagnostic timeline build: 8 u64 per workgroup written over dq's storage (see the kernel's STAMP),
+// 6 = dK/dV only through the persistent kernel, 7 = its timeline build (4 u64 per item, 64 items per
+// workgroup, over dq's storage).
 // ``delta`` is taken as given.
 void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                    const at::Tensor& delta, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
@@ -829,12 +1595,17 @@ void fa_bwd_ablate(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
   const c10::DeviceGuard g(q.device());
   const double scale = 1.0 / std::sqrt((double)D);
   BwdArgs a = make_args(dout, q, k, v, lse, delta, dq, dk, dv, scale);
+  if (abl == 5 || abl == 7) {
+    LLMCTL_CHECK(dq.numel() * 2 >= (long)q.size(0) * k.size(2) * ((q.size(1) + KV_KB - 1) / KV_KB) * 64,
+                 "fa_bwd_ablate: dq too small for the timeline");
+    a.stamps = reinterpret_cast<unsigned long long*>(dq.data_ptr());
+  }
   auto rck = row_consts(a, lse);
-  if (abl == 1) {  // no dQ kernel to write them
+  if (abl == 1 || abl >= 3) {  // no dQ kernel to write them
     rck.narrow(0, 0, lse.numel()).copy_(lse.reshape(-1) * (-1.0 / scale));
     rck.narrow(0, lse.numel(), lse.numel()).copy_(-delta.reshape(-1));
   }
-  dispatch_bwd(a, D, true, false, stream(), abl != 1, abl != 2);
+  dispatch_bwd(a, D, true, false, stream(), abl == 0 || abl == 2, abl != 2, abl >= 3 ? (int)abl - 3 : -1);
 }
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {

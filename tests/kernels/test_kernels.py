@@ -232,6 +232,27 @@ def test_flash_attn_forced_rescale(native_lib):
     assert _row_err(o, orf) < 2e-2, _row_err(o, orf)
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 512, 4, 4), (2, 320, 8, 2), (1, 200, 4, 1), (1, 2048, 2, 2),
+                                        (2, 512, 8, 2), (2, 1024, 16, 8), (3, 256, 24, 8)])
+def test_dkv_pipelined_matches_unpipelined(native_lib, B, S, Hq, Hkv):
+    """The software-pipelined and the persistent dK/dV kernels reorder instructions, not arithmetic:
+    bitwise equal to the unpipelined kernel (partial tiles, GQA groups, the causal diagonal, the
+    persistent kernel's per-XCD and single work queues, items spanning head groups)."""
+    D = 128
+    q, k, v, do = (_bf(B, S, h, D, seed=s) for h, s in ((Hq, 61), (Hkv, 62), (Hkv, 63), (Hq, 64)))
+    o, lse = native_lib.flash_attn_fwd(q, k, v, D ** -0.5, True)
+    delta = (do.float() * o.float()).sum(-1).transpose(1, 2).contiguous()
+    outs = []
+    for impl in (3, 4, 6, 6):  # unpipelined, pipelined, persistent (twice: the queue resets per launch)
+        dq, dk, dv = torch.zeros_like(q), torch.zeros_like(k), torch.zeros_like(v)
+        native_lib.fa_bwd_ablate(do, q, k, v, delta, lse, dq, dk, dv, impl)
+        outs.append((dk, dv))
+    torch.cuda.synchronize()
+    for dk, dv in outs[1:]:
+        assert torch.equal(outs[0][0], dk) and torch.equal(outs[0][1], dv)
+    assert outs[0][0].abs().sum() > 0
+
+
 def test_functional_autograd_matches_ref(native_lib):
     """Whole-model forward/backward through the HIP path vs the fp32 oracle path."""
     import os

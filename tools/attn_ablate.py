@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Timing of the flash-attention backward kernels (B8 S2048 H32 D128 causal, random data):
-abl 0 = dQ + dK/dV kernels, 1 = dK/dV kernel only, 2 = dQ kernel only; plus the whole
+abl 0 = dQ + dK/dV kernels, 1 = dK/dV kernel only, 2 = dQ kernel only, 3 / 4 / 6 = dK/dV through the
+unpipelined / software-pipelined / persistent kernel; plus the whole
 ``flash_attn_bwd`` op (delta pre-kernel included) and the forward for reference."""
 import json
 import sys
@@ -37,7 +38,9 @@ def timeit(f):
 
 
 res = {"shape": [B, S, H, D]}
-for abl, name in [(0, "dq+dkv"), (1, "dkv"), (2, "dq"), (1, "dkv_again")]:
+for abl, name in [(0, "dq+dkv"), (1, "dkv"), (2, "dq"), (3, "dkv_unpipelined"), (4, "dkv_pipelined"),
+                  (6, "dkv_persistent"), (3, "dkv_unpipelined_again"), (4, "dkv_pipelined_again"),
+                  (6, "dkv_persistent_again")]:
     ms = timeit(lambda: ops.fa_bwd_ablate(do, q, k, v, delta, lse, dq, dk, dv, abl))
     res[name] = {"ms": round(ms, 3), "tflops_equiv_5prod": round(fl / ms / 1e9, 1)}
     print(name, res[name], flush=True)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run ONE flash-attention kernel repeatedly (for rocprofv3 --pmc passes):
-    attn_one.py {fwd|dkv|dq} [iters] [B S H D]"""
+    attn_one.py {fwd|dkv|dq|dkv_old|dkv_pipe} [iters] [B S H D]"""
 import sys
 
 import torch
@@ -22,6 +22,6 @@ for _ in range(iters):
     if kind == "fwd":
         ops.flash_attn_fwd(q, k, v, scale, True)
     else:
-        ops.fa_bwd_ablate(do, q, k, v, delta, lse, dq, dk, dv, 1 if kind == "dkv" else 2)
+        ops.fa_bwd_ablate(do, q, k, v, delta, lse, dq, dk, dv, {"dkv": 1, "dq": 2, "dkv_old": 3, "dkv_pipe": 4}[kind])
 torch.cuda.synchronize()
 print("ok", kind)
