@@ -184,6 +184,55 @@ def wgrad_into(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate:
         torch.mm(dy2.t(), x2, out=g)
 
 
+def side_chunks(M: int, N: int, K: int, T: int, F: int) -> int:
+    """Chunks of 1024 elements per K-tile that ``gemm64_wgrad_swiglu``'s side job needs to cover
+    ``T * F`` elements over the K-tiles of an ``[M, N] x K`` weight gradient (0: unsupported) —
+    as ``side_chunks`` in gemm64.hip."""
+    ktiles = (M // 256) * (N // 256) * (K // 64)
+    E = T * F
+    if E * 4 >= 2**31 or F % 2:
+        return 0
+    for ch in (1, 2):
+        if ktiles * 1024 * ch >= E and ktiles * 1024 * ch < 2**32 and F >= 1024 * ch:
+            return ch
+    return 0
+
+
+def swiglu_side_mode() -> str:
+    """Where the MLP's SwiGLU backward runs (``LLMCTL_SWIGLU_BWD``): ``side`` (default) = as a side
+    job of the down projection's weight-gradient GEMM (``gemm64_wgrad_swiglu``), the data
+    gradient a plain GEMM; ``epilogue`` = in the data-gradient GEMM's store epilogue
+    (``gemm64_swiglu_dgrad``, round 2); ``0`` = separate elementwise kernel."""
+    return os.environ.get("LLMCTL_SWIGLU_BWD", "side")
+
+
+def wgrad_swiglu_ok(w: torch.nn.Parameter, tokens: int, F: int) -> bool:
+    """Can ``w``'s (down projection, [H, F]) weight gradient over ``tokens`` rows carry the SwiGLU
+    backward as a side job?  Needs the grad sink (the GEMM writes the flat gradient view)."""
+    if swiglu_side_mode() != "side" or getattr(w, "_llmctl_grad_sink", None) is None or not w.is_cuda:
+        return False
+    H = w.shape[0]
+    return (_gemm64_enabled() and w.dtype == torch.bfloat16 and H % 256 == 0 and F % 256 == 0
+            and tokens % 128 == 0 and tokens > 0 and side_chunks(H, F, tokens, tokens, F) > 0)
+
+
+def wgrad_swiglu_into(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate: bool,
+                      dact: torch.Tensor, gu: torch.Tensor) -> Optional[torch.Tensor]:
+    """``g (+)= dy2^T x2`` with ``dgu = swiglu_bwd(dact, gu)`` computed by the same kernel
+    (returned); None when the operands do not fit (the caller falls back)."""
+    M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
+    if not (_gemm64_ok(M, N, K, dy2, x2) and g.is_cuda and g.dtype in (torch.bfloat16, torch.float32)
+            and g.stride(1) == 1 and g.stride(0) % 8 == 0 and g.data_ptr() % 16 == 0
+            and K * dy2.stride(0) * 2 < 2**31 and K * x2.stride(0) * 2 < 2**31
+            and dact.is_contiguous() and gu.is_contiguous() and dact.shape == (K, N) and gu.shape == (K, 2 * N)
+            and dact.dtype == torch.bfloat16 and gu.dtype == torch.bfloat16
+            and side_chunks(M, N, K, K, N) > 0):
+        return None
+    from llmctl.ops._lib import native
+
+    return native().gemm64_wgrad_swiglu(dy2, x2, g, accumulate, dact, gu, gemm64_config("wgrad", M, N, K))
+
+
 class GradSink:
     def __init__(self, transpose_dgrad: Optional[bool] = None):
         self.callbacks: List[Callable[[torch.nn.Parameter], None]] = []
@@ -251,16 +300,32 @@ class GradSink:
     def reset(self, p: torch.nn.Parameter) -> None:
         p._llmctl_fresh = True
 
-    def write(self, p: torch.nn.Parameter, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+    @staticmethod
+    def _target(p: torch.nn.Parameter) -> torch.Tensor:
         g = getattr(p, "main_grad", None)
         if g is None:
             g = p.grad
         if g is None:
             raise RuntimeError("grad sink parameter has no flat .grad view")
-        wgrad_into(g, dy2, x2, accumulate=not p._llmctl_fresh)
+        return g
+
+    def _written(self, p: torch.nn.Parameter) -> None:
         p._llmctl_fresh = False
         for cb in self.callbacks:
             cb(p)
+
+    def write(self, p: torch.nn.Parameter, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+        wgrad_into(self._target(p), dy2, x2, accumulate=not p._llmctl_fresh)
+        self._written(p)
+
+    def write_swiglu(self, p: torch.nn.Parameter, dy2: torch.Tensor, x2: torch.Tensor, dact: torch.Tensor,
+                     gu: torch.Tensor) -> Optional[torch.Tensor]:
+        """``write`` with the SwiGLU backward riding on the weight-gradient GEMM: returns
+        ``dgu = swiglu_bwd(dact, gu)``, or None (nothing written) if the kernel cannot take it."""
+        dgu = wgrad_swiglu_into(self._target(p), dy2, x2, not p._llmctl_fresh, dact, gu)
+        if dgu is not None:
+            self._written(p)
+        return dgu
 
 
 class _Linear(torch.autograd.Function):

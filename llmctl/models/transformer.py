@@ -84,11 +84,16 @@ class _SwiGLUDown(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, gu, w_down, recompute=False):
+        from llmctl.exec.linear import wgrad_swiglu_ok
         from llmctl.ops._lib import native, use_native
         from llmctl.ops import ref
 
         act = native().swiglu_fwd(gu) if use_native(gu) else ref.swiglu_fwd(gu)
         out = F.linear(act, w_down)
+        T = gu.numel() // gu.shape[-1]
+        ctx.side = gu.requires_grad and wgrad_swiglu_ok(w_down, T, w_down.shape[1])
+        if ctx.side:
+            _prep_weight_t(w_down, T)  # the plain data gradient reads W^T (hipBLASLt forward layout)
         ctx.recompute = recompute
         if recompute:
             ctx.save_for_backward(gu, w_down)
@@ -108,7 +113,19 @@ class _SwiGLUDown(torch.autograd.Function):
         else:
             gu, w_down, act = ctx.saved_tensors
         dout2 = dout.reshape(-1, dout.shape[-1])
-        dw = weight_grad(ctx.wparam, dout2, act.reshape(-1, act.shape[-1]))
+        act2 = act.reshape(-1, act.shape[-1])
+        if ctx.side:
+            # plain data gradient, then the weight gradient computing dgu on the side (gemm64.hip
+            # "side job"): the HBM-bound SwiGLU backward streams under the wgrad's MFMAs
+            dact = data_grad(dout2, ctx.wparam)
+            dgu = ctx.wparam._llmctl_grad_sink.write_swiglu(ctx.wparam, dout2, act2, dact, gu.reshape(-1, gu.shape[-1]))
+            if dgu is not None:
+                return dgu.view(gu.shape), None, None
+            from llmctl.ops._lib import native, use_native
+
+            dw = weight_grad(ctx.wparam, dout2, act2)
+            return (native().swiglu_bwd(dact, gu) if use_native(gu) else ref.swiglu_bwd(dact, gu)), dw, None
+        dw = weight_grad(ctx.wparam, dout2, act2)
         dgu = swiglu_data_grad(dout, ctx.wparam, gu)
         return dgu, dw, None
 

@@ -72,5 +72,6 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("gemm64_swiglu_dgrad(Tensor dy, Tensor w, Tensor gu, int config=104) -> Tensor");
   m.def("gemm64_qkv_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, Tensor? pos, int nq, int nkv, int seq, int config=104) -> (Tensor, Tensor, Tensor)");
   m.def("gemm64_up_swiglu(Tensor x, Tensor w, int config=104) -> (Tensor, Tensor)");
+  m.def("gemm64_wgrad_swiglu(Tensor dy, Tensor act, Tensor(a!) gw, bool accumulate, Tensor dact, Tensor gu, int config=104) -> Tensor");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
 }

@@ -112,11 +112,26 @@ struct G64Args {
   const float* sinT = nullptr;
   const int* pos = nullptr;        // EPI_ROPE_QKV: int32 position per token (nullptr: t % seq)
   int nq = 0, nkv = 0, seq = 1;
+  // side job (SIDE > 0, wgrad of the down projection): dgu = swiglu_bwd(dact, gu), dact [T, F],
+  // gu / dgu [T, 2F], E = T * F elements spread over the K-tiles of the whole grid
+  const unsigned short* s_dact = nullptr;
+  const unsigned short* s_gu = nullptr;
+  unsigned short* s_dgu = nullptr;
+  unsigned s_E = 0;
+  int s_F = 0;
 };
 
 // SwiGLU backward of one element: d = dL/dact, act = silu(g) * u
 __device__ __forceinline__ void swiglu_bwd1(float d, float g, float u, float& dg, float& du) {
   const float sg = 1.f / (1.f + __expf(-g));
+  dg = d * u * (sg * (1.f + g * (1.f - sg)));
+  du = d * (g * sg);
+}
+
+// the same with a hardware reciprocal (1 ulp) instead of an IEEE division: the side job's VALU
+// runs beside MFMAs, where a 10-instruction division per element would show
+__device__ __forceinline__ void swiglu_bwd1_fast(float d, float g, float u, float& dg, float& du) {
+  const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-g));
   dg = d * u * (sg * (1.f + g * (1.f - sg)));
   du = d * (g * sg);
 }
@@ -134,6 +149,12 @@ __device__ __forceinline__ i32x4_t make_rsrc(const void* base) {
   r[3] = 0x00020000;  // raw buffer, 32-bit data format
   return r;
 }
+// range-checked raw buffer: loads at byte offsets >= bytes return 0, stores there are dropped
+__device__ __forceinline__ i32x4_t make_rsrc_n(const void* base, unsigned bytes) {
+  i32x4_t r = make_rsrc(base);
+  r[2] = (int)bytes;
+  return r;
+}
 // one LDS-DMA piece: 64 lanes x 16 B -> LDS [lds_byte, +1024), lane-linear
 __device__ __forceinline__ void bdma16(i32x4_t rsrc, unsigned voff, unsigned soff, unsigned lds_byte) {
   asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
@@ -149,7 +170,7 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-  else static_assert(N == 0, "add the immediate");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // ---- half-tile images -----------------------------------------------------------------------
@@ -275,8 +296,38 @@ __device__ __forceinline__ void epi_acc_bf16(const f32x4_t (&acc)[8][4], unsigne
     }
 }
 
-template <bool AT, bool BT, int EPI, int GROUP, int V>
+// ---- side job: an HBM-bound elementwise pass riding on a compute-bound GEMM -------------------
+// The down projection's data gradient used to carry the SwiGLU backward in its epilogue
+// (EPI_SWIGLU_BWD).  Every CU reaches that epilogue at the same moment (uniform tiles), so the
+// chip alternated between MFMA-bound main loops with idle HBM and HBM-bound epilogues (256 KB
+// read + 256 KB written per tile) with idle matrix cores: the fused dgrad ran ~560 us (35 %)
+// over the plain one at GPT-7B.  Now the dgrad stores plain dAct and the down projection's
+// weight-gradient GEMM (independent of dgu) computes dgu = swiglu_bwd(dact, gu) on the side:
+// every K-tile of every work item handles SIDE chunks of 1024 consecutive elements (2 per
+// thread: one dword of dact / gate / up loaded, one dword of dgate / dup stored), so the
+// elementwise traffic streams evenly under the MFMAs.  Element ranges follow the global K-tile
+// order (item base + t); range-checked buffer resources turn the elements past E (and the
+// prologue's dummy ops) into zero loads and dropped stores, with no branch in the loop.
+// Pipelining (variant-1 schedule; P = t & 1 selects one of two register slots), all in phase
+// j = 3, the one without LDS fragment reads (its wave group's read section has the most slack
+// under the other group's MFMA segment; in phase 0, beside 24 ds_read_b64_tr_b16, the same VALU
+// cost ~3x as much wall time):
+//   tile t, j = 1:  ... A_hi(t+1), vmcnt(8 + 5 SIDE)
+//   tile t, j = 3:  ... B_h0(t+2), W(t-2) [SwiGLU backward of slot P, 2 SIDE dword stores],
+//                   L(t) [3 SIDE dword loads into slot P], vmcnt(6 + 5 SIDE)
+// The waits retire exactly the half-tiles they did before (the side ops between are counted);
+// L(t) is retired by the j = 3 wait of tile t+1 (one K-tile of latency cover) and consumed at
+// j = 3 of tile t+2.  The prologue issues out-of-range dummies for W(-3) / L(-1) (same counts);
+// L(KT-2) / L(KT-1) are stored after the loop.
+constexpr unsigned SIDE_OOB = 0x80000000u;  // byte offset past every side buffer (E*4 < 2^31)
+#ifndef SIDE_NT
+#define SIDE_NT " nt"  // streamed once: non-temporal, do not displace the GEMM's operand lines
+#endif
+//  // byte offset past every side buffer (E*4 < 2^31)
+
+template <bool AT, bool BT, int EPI, int GROUP, int V, int SIDE = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
+  static_assert(SIDE == 0 || (V & 1), "side job: variant-1 schedule only");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -344,6 +395,75 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     }
   };
 
+  // ---- side job state (see above): per chunk the element index / column / gu row offset of this
+  // thread's next pair, per slot the loaded dwords and the gu byte offsets they came from
+  constexpr int SC = SIDE > 0 ? SIDE : 1;
+  constexpr unsigned SCH = 1024u * SC;  // elements per K-tile per work item
+  unsigned s_e[SC], s_f[SC], s_row[SC], s_og[2][SC], s_ou[2][SC], s_d[2][SC][3];
+  i32x4_t rs_dact, rs_gu, rs_dgu;
+  const unsigned sF = (unsigned)args.s_F;
+  if constexpr (SIDE > 0) {
+    rs_dact = make_rsrc_n(args.s_dact, args.s_E * 2u);
+    rs_gu = make_rsrc_n(args.s_gu, args.s_E * 4u);
+    rs_dgu = make_rsrc_n(args.s_dgu, args.s_E * 4u);
+    const unsigned ktf = (unsigned)(args.K / TK);
+    const unsigned gk0 = bid < args.n_main ? (unsigned)bid * ktf
+                                           : (unsigned)args.n_main * ktf + (unsigned)(bid - args.n_main) * (unsigned)args.kt_part;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) {
+      const unsigned e = gk0 * SCH + 1024u * c + 2u * tid;
+      const unsigned t = e / sF;
+      s_e[c] = e;
+      s_f[c] = e - t * sF;
+      s_row[c] = t * 4u * sF;
+      s_og[0][c] = s_ou[0][c] = s_og[1][c] = s_ou[1][c] = SIDE_OOB;
+    }
+  }
+  // L: SIDE x (dact, gate, up) dword loads into slot S (DUMMY: out-of-range, no advance)
+  auto side_load = [&](auto slot_c, auto dummy_c) {
+    constexpr int S = decltype(slot_c)::value;
+    constexpr bool DUMMY = decltype(dummy_c)::value;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) {
+      const bool ok = !DUMMY && s_e[c] < args.s_E;
+      const unsigned oa = ok ? 2u * s_e[c] : SIDE_OOB;
+      const unsigned og = ok ? s_row[c] + 2u * s_f[c] : SIDE_OOB;
+      const unsigned ou = ok ? og + 2u * sF : SIDE_OOB;
+      const i32x4_t ra_ = rs_dact, rg_ = rs_gu;
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" SIDE_NT : "=v"(s_d[S][c][0]) : "v"(oa), "s"(ra_) : "memory");
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" SIDE_NT : "=v"(s_d[S][c][1]) : "v"(og), "s"(rg_) : "memory");
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" SIDE_NT : "=v"(s_d[S][c][2]) : "v"(ou), "s"(rg_) : "memory");
+      s_og[S][c] = og;
+      s_ou[S][c] = ou;
+      if constexpr (!DUMMY) {
+        s_e[c] += SCH;
+        s_f[c] += SCH;
+        const bool wrap = s_f[c] >= sF;
+        s_f[c] -= wrap ? sF : 0u;
+        s_row[c] += wrap ? 4u * sF : 0u;
+      }
+    }
+  };
+  // W: SwiGLU backward of slot S's pairs, 2 x SIDE dword stores into dgu
+  auto side_store = [&](auto slot_c) {
+    constexpr int S = decltype(slot_c)::value;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) {
+      // the loads were retired by an explicit vmcnt wait; keep every use of their registers after it
+      asm volatile("" : "+v"(s_d[S][c][0]), "+v"(s_d[S][c][1]), "+v"(s_d[S][c][2]));
+      const unsigned d = s_d[S][c][0], gg = s_d[S][c][1], uu = s_d[S][c][2];
+      float dg0, du0, dg1, du1;
+      swiglu_bwd1_fast(bf2f(d & 0xffff), bf2f(gg & 0xffff), bf2f(uu & 0xffff), dg0, du0);
+      swiglu_bwd1_fast(bf2f(d >> 16), bf2f(gg >> 16), bf2f(uu >> 16), dg1, du1);
+      const unsigned pg = (unsigned)f2bf(dg0) | ((unsigned)f2bf(dg1) << 16);
+      const unsigned pu = (unsigned)f2bf(du0) | ((unsigned)f2bf(du1) << 16);
+      const unsigned og = s_og[S][c], ou = s_ou[S][c];
+      const i32x4_t r = rs_dgu;
+      asm volatile("buffer_store_dword %0, %1, %2, 0 offen" SIDE_NT ::"v"(pg), "v"(og), "s"(r) : "memory");
+      asm volatile("buffer_store_dword %0, %1, %2, 0 offen" SIDE_NT ::"v"(pu), "v"(ou), "s"(r) : "memory");
+    }
+  };
+
   f32x4_t acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -357,7 +477,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   issue(K_<A_HI>{}, 0);
   issue(K_<A_LO>{}, 1);
   issue(K_<B_H0>{}, 1);
-  wait_vm<6>();
+  if constexpr (SIDE > 0) {  // W(-3), L(-1): out-of-range dummies that keep the loop's counts
+    side_store(K_<1>{});
+    side_load(K_<1>{}, std::true_type{});
+  }
+  wait_vm<6 + 5 * SIDE>();
   bar();
   if (wr == 1) bar();  // wave group 1 runs one barrier behind group 0
 
@@ -394,7 +518,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   };
 
   // EARLY moves each issue ahead of its phase's wait: the waits then count 2 more pieces
-  auto ktile = [&](int t, const unsigned char* buf) {
+  auto ktile = [&](int t, const unsigned char* buf, auto slot_c) {
     // j = 0
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -416,7 +540,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
       for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bhalf(j), bpos(j), ks, lane);
     if constexpr (EARLY) {
       issue(K_<A_HI>{}, t + 1);
-      wait_vm<8>();
+      wait_vm<8 + 5 * SIDE>();
       bar();
     } else {
       wait_vm<6>();
@@ -438,7 +562,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     // j = 3
     if constexpr (EARLY) {
       issue(K_<B_H0>{}, t + 2);
-      wait_vm<6>();
+      if constexpr (SIDE > 0) {
+        side_store(slot_c);                     // W(t-2)
+        side_load(slot_c, std::false_type{});  // L(t)
+      }
+      wait_vm<6 + 5 * SIDE>();
       bar();
     } else {
       wait_vm<4>();
@@ -450,11 +578,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   };
 
   for (int t = 0; t < KT; t += 2) {
-    ktile(t, smem);
-    ktile(t + 1, smem + BUF);
+    ktile(t, smem, K_<0>{});
+    ktile(t + 1, smem + BUF, K_<1>{});
   }
   if (wr == 0) bar();  // re-align the barrier count of the two groups
   wait_vm<0>();        // the clamped tail items are still landing
+  if constexpr (SIDE > 0) {  // W(KT-2), W(KT-1)
+    side_store(K_<0>{});
+    side_store(K_<1>{});
+  }
 
   // ---- epilogue: lane holds C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3
   const int g = lane >> 4, i16 = lane & 15;
@@ -1138,6 +1270,92 @@ at::Tensor gemm64_swiglu_dgrad(const at::Tensor& dy, const at::Tensor& w, const 
   return dgu;
 }
 
+template <int EPI, int SIDE>
+void launch_side(const G64Args& g) {
+  const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
+  hipLaunchKernelGGL((gemm64_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NTHR), 0, stream(), g);
+  const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
+  if (n_tail > 0)
+    hipLaunchKernelGGL((gemm64_split_reduce<EPI, 4>), dim3(n_tail * (TM * TN / 8 / 256)), dim3(256), 0, stream(), g);
+}
+
+template <int EPI>
+void launch_side_ch(const G64Args& g, int ch) {
+  if (ch == 1) launch_side<EPI, 1>(g);
+  else launch_side<EPI, 2>(g);
+}
+
+// chunks of 1024 elements per K-tile the side job needs for E = T * F elements over the K-tiles
+// of an [M, N] x K wgrad (0: more than 2, or offsets past 32 bits — not supported)
+int side_chunks(long M, long N, long K, long T, long F) {
+  const long ktiles = (M / TM) * (N / TN) * (K / TK), E = T * F;
+  if (E * 4 >= (1L << 31) || F % 2) return 0;
+  for (int ch = 1; ch <= 2; ++ch)
+    if (ktiles * 1024 * ch >= E && ktiles * 1024 * ch < (1L << 32) && F >= 1024L * ch) return ch;
+  return 0;
+}
+
+// Down-projection weight gradient with the SwiGLU backward as a side job (see "side job" above):
+//   gw (+)= dy^T act               dy [T, H], act [T, F]  (wgrad layout; gw [H, F] bf16 or fp32)
+//   dgu = swiglu_bwd(dact, gu)     dact [T, F], gu [T, 2F] -> returned [T, 2F]
+at::Tensor gemm64_wgrad_swiglu(const at::Tensor& dy, const at::Tensor& act, at::Tensor& gw, bool accumulate,
+                               const at::Tensor& dact, const at::Tensor& gu, int64_t config) {
+  LLMCTL_CHECK(dy.dim() == 2 && act.dim() == 2 && gw.dim() == 2 && dact.dim() == 2 && gu.dim() == 2,
+               "gemm64_wgrad_swiglu: 2-D operands");
+  const bool f32_out = gw.scalar_type() == at::kFloat;
+  LLMCTL_CHECK(dy.scalar_type() == at::kBFloat16 && act.scalar_type() == at::kBFloat16 &&
+                   dact.scalar_type() == at::kBFloat16 && gu.scalar_type() == at::kBFloat16 &&
+                   (f32_out || gw.scalar_type() == at::kBFloat16),
+               "gemm64_wgrad_swiglu: bf16 operands, bf16 / fp32 weight gradient");
+  LLMCTL_CHECK(dy.is_cuda() && act.is_cuda() && gw.is_cuda() && dact.is_cuda() && gu.is_cuda(),
+               "gemm64_wgrad_swiglu: GPU tensors");
+  const long T = dy.size(0), M = dy.size(1), N = act.size(1);
+  LLMCTL_CHECK(act.size(0) == T && gw.size(0) == M && gw.size(1) == N, "gemm64_wgrad_swiglu: dy [T,H], act [T,F], gw [H,F]");
+  LLMCTL_CHECK(dact.is_contiguous() && gu.is_contiguous() && dact.size(0) == T && dact.size(1) == N &&
+                   gu.size(0) == T && gu.size(1) == 2 * N,
+               "gemm64_wgrad_swiglu: contiguous dact [T, F], gu [T, 2F]");
+  LLMCTL_CHECK(dy.stride(1) == 1 && act.stride(1) == 1 && gw.stride(1) == 1, "gemm64_wgrad_swiglu: unit inner stride");
+  LLMCTL_CHECK(gemm64_supported(M, N, T), "gemm64_wgrad_swiglu: H, F multiples of 256, T of 128 (got ", M, "x", N, "x", T,
+               ")");
+  LLMCTL_CHECK(dy.stride(0) % 8 == 0 && act.stride(0) % 8 == 0 && gw.stride(0) % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(act.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(gw.data_ptr()) & (f32_out ? 15 : 7)) == 0 &&
+                   (reinterpret_cast<uintptr_t>(dact.data_ptr()) & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(gu.data_ptr()) & 3) == 0,
+               "gemm64_wgrad_swiglu: aligned operand rows");
+  LLMCTL_CHECK(T * dy.stride(0) * 2 < (1L << 31) && T * act.stride(0) * 2 < (1L << 31),
+               "gemm64_wgrad_swiglu: operand too large for 32-bit offsets");
+  const int ch = side_chunks(M, N, T, T, N);
+  LLMCTL_CHECK(ch > 0, "gemm64_wgrad_swiglu: side job does not fit (", T, " x ", N, " elements over ", M, " x ", N,
+               " x ", T, ")");
+  const c10::DeviceGuard dg(dy.device());
+  auto dgu = at::empty_like(gu);
+  G64Args g{reinterpret_cast<const unsigned short*>(dy.data_ptr()), reinterpret_cast<const unsigned short*>(act.data_ptr()),
+            reinterpret_cast<unsigned short*>(gw.data_ptr()), dy.stride(0), act.stride(0), gw.stride(0),
+            (int)M, (int)N, (int)T, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr, nullptr};
+  g.s_dact = reinterpret_cast<const unsigned short*>(dact.data_ptr());
+  g.s_gu = reinterpret_cast<const unsigned short*>(gu.data_ptr());
+  g.s_dgu = reinterpret_cast<unsigned short*>(dgu.data_ptr());
+  g.s_E = (unsigned)(T * N);
+  g.s_F = (int)N;
+  if (const char* d = std::getenv("LLMCTL_SIDE_DIAG"); d && std::string(d) == "nomem") g.s_E = 0;  // timing only
+  plan_split(g, (int)(config / 1000));
+  at::Tensor ws;
+  if (g.splits > 1) {
+    ws = at::empty({(long)(g.tiles_m * g.tiles_n - g.n_main) * g.splits * TM * TN}, dy.options().dtype(at::kFloat));
+    g.ws = ws.data_ptr<float>();
+  }
+  if (f32_out) {
+    if (accumulate) launch_side_ch<EPI_ACC_F32>(g, ch);
+    else launch_side_ch<EPI_STORE_F32>(g, ch);
+  } else {
+    if (accumulate) launch_side_ch<EPI_ACC>(g, ch);
+    else launch_side_ch<EPI_STORE>(g, ch);
+  }
+  return dgu;
+}
+
 // Gate/up projection fused with SwiGLU (serving prefill): act [M, F] = silu(x Wg^T) * (x Wu^T) with
 // W_up = [Wg; Wu] [2F, K] (forward layout, both operands K-contiguous); M % 256, F % 128, K % 128.
 at::Tensor gemm64_swiglu_fwd(const at::Tensor& x, const at::Tensor& w, int64_t config) {
@@ -1240,6 +1458,7 @@ TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("gemm64_swiglu_fwd", &gemm64_swiglu_fwd);
   m.impl("gemm64_ex", &gemm64_ex);
   m.impl("gemm64_swiglu_dgrad", &gemm64_swiglu_dgrad);
+  m.impl("gemm64_wgrad_swiglu", &gemm64_wgrad_swiglu);
 }
 
 }  // namespace llmctl

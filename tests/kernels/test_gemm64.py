@@ -189,3 +189,70 @@ def test_gemm64_wgrad_fp32_output(native_lib, cfg):
     out = c0.clone()
     native_lib.gemm64_ex(A, B, out, True, True, True, cfg)
     assert (out - (want + c0)).abs().max().item() < 2e-3 * want.abs().max().item()
+
+
+def _swiglu_bwd_ref(dact, gu):
+    F = dact.shape[1]
+    g, u = gu[:, :F].float(), gu[:, F:].float()
+    sg = torch.sigmoid(g)
+    return torch.cat([dact.float() * u * sg * (1 + g * (1 - sg)), dact.float() * g * sg], dim=1)
+
+
+@pytest.mark.parametrize("T,H,F,cfg", [(512, 4096, 1024, 104),   # one chunk per K-tile, exact fit
+                                       (512, 2048, 2048, 104),   # two chunks per K-tile
+                                       (512, 3072, 2304, 104),   # elements past E (range-checked)
+                                       (2048, 4096, 1024, 4104),  # every tile split into 4 K-ranges
+                                       (2048, 4096, 1024, 1104)])
+@pytest.mark.parametrize("gdt,acc", [(torch.bfloat16, False), (torch.bfloat16, True), (torch.float32, False),
+                                     (torch.float32, True)])
+def test_gemm64_wgrad_swiglu(native_lib, T, H, F, cfg, gdt, acc):
+    """Down-projection weight gradient with the SwiGLU backward as a side job: gw (+)= dy^T act
+    and dgu = swiglu_bwd(dact, gu), both against fp32 references."""
+    from llmctl.exec.linear import side_chunks
+
+    assert side_chunks(H, F, T, T, F) > 0
+    dy, act = _bf(T, H, seed=11), _bf(T, F, seed=12)
+    dact, gu = _bf(T, F, seed=13), _bf(T, 2 * F, seed=14)
+    g0 = torch.randn(H, F, device=DEV).to(gdt)
+    gw = g0.clone() if acc else torch.full((H, F), float("nan"), device=DEV, dtype=gdt)
+    dgu = native_lib.gemm64_wgrad_swiglu(dy, act, gw, acc, dact, gu, cfg)
+    want = dy.float().t() @ act.float() + (g0.float() if acc else 0.0)
+    assert torch.isfinite(gw.float()).all() and torch.isfinite(dgu.float()).all()
+    assert row_err(gw, want) < TOL
+    ref = _swiglu_bwd_ref(dact, gu)
+    assert row_err(dgu[:, :F], ref[:, :F]) < TOL and row_err(dgu[:, F:], ref[:, F:]) < TOL
+
+
+@pytest.mark.parametrize("main_grad", [False, True])
+def test_swiglu_down_side_job_autograd(native_lib, monkeypatch, main_grad):
+    """_SwiGLUDown with a grad-sink weight: plain data gradient + weight gradient carrying the
+    SwiGLU backward (LLMCTL_SWIGLU_BWD=side); two backward passes accumulate into the sink's
+    view (bf16 .grad or fp32 main_grad); matches fp32 autograd and the epilogue-fused path."""
+    from llmctl.exec.linear import GradSink, wgrad_swiglu_ok
+    from llmctl.models.transformer import _SwiGLUDown
+
+    T, H, F = 512, 4096, 1024
+    gu0 = _bf(T, 2 * F, seed=21)
+    w = torch.nn.Parameter(_bf(H, F, seed=22) * 0.02)
+    dy = _bf(T, H, seed=23)
+    sink = GradSink()
+    sink.attach(w)
+    if main_grad:
+        w.main_grad = torch.zeros(H, F, device=DEV)
+    else:
+        w.grad = torch.zeros_like(w)
+    assert wgrad_swiglu_ok(w, T, F)
+    g32, w32 = gu0.float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    ref_out = torch.nn.functional.linear(torch.nn.functional.silu(g32[:, :F]) * g32[:, F:], w32)
+    ref_out.backward(dy.float())
+    for step in (1, 2):
+        gu = gu0.clone().requires_grad_(True)
+        out = _SwiGLUDown.apply(gu, w, False)
+        out.backward(dy)
+        gw = w.main_grad if main_grad else w.grad
+        assert row_err(gu.grad, g32.grad) < 2e-2
+        assert row_err(gw, step * w32.grad) < 2e-2
+    monkeypatch.setenv("LLMCTL_SWIGLU_BWD", "epilogue")
+    gu = gu0.clone().requires_grad_(True)
+    _SwiGLUDown.apply(gu, w, False).backward(dy)
+    assert row_err(gu.grad, g32.grad) < 2e-2
