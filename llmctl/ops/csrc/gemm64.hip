@@ -305,13 +305,17 @@ __device__ __forceinline__ void epi_acc_bf16(const f32x4_t (&acc)[8][4], unsigne
 // weight-gradient GEMM (independent of dgu) computes dgu = swiglu_bwd(dact, gu) on the side:
 // every K-tile of every work item handles SIDE chunks of 1024 consecutive elements (2 per
 // thread: one dword of dact / gate / up loaded, one dword of dgate / dup stored), so the
-// elementwise traffic streams evenly under the MFMAs.  Element ranges follow the global K-tile
+// elementwise traffic streams evenly under the MFMAs.  Measured at T 24576, H 4096, F 11008
+// (tools/swiglu_side_bench.py): wgrad 1.71 ms alone, 1.99 ms with the side job (1.82 ms with
+// every side access out of range, i.e. instruction cost only); dgrad + fused epilogue 2.10 ms
+// vs plain dgrad (hipBLASLt via W^T) 1.59 ms; per layer 3.49 ms against 3.72 (epilogue form) and
+// 3.60 (separate swiglu_bwd kernel).  Element ranges follow the global K-tile
 // order (item base + t); range-checked buffer resources turn the elements past E (and the
 // prologue's dummy ops) into zero loads and dropped stores, with no branch in the loop.
 // Pipelining (variant-1 schedule; P = t & 1 selects one of two register slots), all in phase
 // j = 3, the one without LDS fragment reads (its wave group's read section has the most slack
-// under the other group's MFMA segment; in phase 0, beside 24 ds_read_b64_tr_b16, the same VALU
-// cost ~3x as much wall time):
+// under the other group's MFMA segment; the stores in phase 0 and the loads in phase 1 measured
+// 2.02 ms against 1.98 ms here):
 //   tile t, j = 1:  ... A_hi(t+1), vmcnt(8 + 5 SIDE)
 //   tile t, j = 3:  ... B_h0(t+2), W(t-2) [SwiGLU backward of slot P, 2 SIDE dword stores],
 //                   L(t) [3 SIDE dword loads into slot P], vmcnt(6 + 5 SIDE)
@@ -321,7 +325,7 @@ __device__ __forceinline__ void epi_acc_bf16(const f32x4_t (&acc)[8][4], unsigne
 // L(KT-2) / L(KT-1) are stored after the loop.
 constexpr unsigned SIDE_OOB = 0x80000000u;  // byte offset past every side buffer (E*4 < 2^31)
 #ifndef SIDE_NT
-#define SIDE_NT " nt"  // streamed once: non-temporal, do not displace the GEMM's operand lines
+#define SIDE_NT " nt"  // streamed once: non-temporal (1.986 vs 2.011 ms without the bit)
 #endif
 //  // byte offset past every side buffer (E*4 < 2^31)
 
