@@ -326,7 +326,8 @@ class DecoderLayer(nn.Module):
             qkv = linear(self._col_in(xn), self.wqkv, self.bqkv)
         if rope is not None and self.pc.cp_size == 1 and os.environ.get("LLMCTL_FUSED_ROPE_ATTN", "1") != "0":
             # RoPE + attention with the RoPE backward fused into the attention backward's stores
-            o = ops.rope_flash_attention(qkv, rope[0], rope[1], self.nq, self.nkv, B, S, positions, doc_start)
+            o = ops.rope_flash_attention(qkv, rope[0], rope[1], self.nq, self.nkv, B, S, positions, doc_start,
+                                         inplace=True)
             return self._attn_out(o, B, S)
         if rope is not None:
             q, k, v = ops.rope_qkv(qkv, rope[0], rope[1], self.nq, self.nkv, S, positions)

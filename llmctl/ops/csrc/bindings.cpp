@@ -22,6 +22,7 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mu, Tensor rstd, Tensor? dres) -> (Tensor, Tensor, Tensor)");
   // elementwise (elementwise.hip)
   m.def("rope_qkv_fwd(Tensor qkv, Tensor cos, Tensor sin, int nq, int nkv, int seq_len, Tensor? positions) -> (Tensor, Tensor, Tensor)");
+  m.def("rope_qk_inplace_(Tensor(a!) qkv, Tensor cos, Tensor sin, int nq, int nkv, int seq_len, Tensor? positions) -> ()");
   m.def("rope_qkv_cache_fwd(Tensor qkv, Tensor cos, Tensor sin, int nq, int nkv, int seq_len, Tensor? positions, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> (Tensor, Tensor, Tensor)");
   m.def("rope_qkv_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cos, Tensor sin, int seq_len, Tensor? positions) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");

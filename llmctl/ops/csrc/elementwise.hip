@@ -197,6 +197,40 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const unsigned short* __r
   store8(dx + i * 8, o);
 }
 
+// In-place RoPE of the q / k heads of a contiguous qkv [T, (nq + 2 nkv) D] (training forward): the
+// attention kernels read q / k / v as strided views of qkv, so V is neither copied nor re-read
+// (2/3 of rope_fwd_kernel's traffic).  Thread = 8 column pairs (c, c + D/2) of one (token, head);
+// the grid walks (token, head) rows with 32-bit index math (T * NR * CH < 2^31, checked on the host).
+template <typename PosT>
+__global__ __launch_bounds__(256) void rope_inplace_kernel(unsigned short* __restrict__ qkv, const float* __restrict__ cosT,
+                                                           const float* __restrict__ sinT, const PosT* __restrict__ pos,
+                                                           int NR, int NH, int D, int S, int total) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int CH = D >> 4, half = D >> 1;
+  const int c = idx % CH;
+  const int r = idx / CH;
+  const int h = r % NR, t = r / NR;
+  unsigned short* src = qkv + ((long)t * NH + h) * D;
+  const long p = pos ? (long)pos[t] : (long)(t % S);
+  float a[8], b[8], cs[8], sn[8], o1[8], o2[8];
+  load8(src + c * 8, a);
+  load8(src + half + c * 8, b);
+  const float4* cp = reinterpret_cast<const float4*>(cosT + p * half + c * 8);
+  const float4* sp = reinterpret_cast<const float4*>(sinT + p * half + c * 8);
+  *reinterpret_cast<float4*>(cs) = cp[0];
+  *reinterpret_cast<float4*>(cs + 4) = cp[1];
+  *reinterpret_cast<float4*>(sn) = sp[0];
+  *reinterpret_cast<float4*>(sn + 4) = sp[1];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    o1[j] = a[j] * cs[j] - b[j] * sn[j];
+    o2[j] = b[j] * cs[j] + a[j] * sn[j];
+  }
+  store8(src + c * 8, o1);
+  store8(src + half + c * 8, o2);
+}
+
 inline unsigned blocks_for(long n) { return (unsigned)((n + 255) / 256); }
 
 void check_rope_tables(const at::Tensor& c, const at::Tensor& s, int D) {
@@ -258,6 +292,37 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_qkv_fwd(const at::Tensor& qk
                                                              const at::Tensor& sinT, int64_t nq, int64_t nkv,
                                                              int64_t seq_len, const c10::optional<at::Tensor>& pos) {
   return rope_qkv_impl(qkv, cosT, sinT, nq, nkv, seq_len, pos, nullptr, nullptr, nullptr);
+}
+
+// qkv [T, (nq + 2 nkv) D]: rotate the q / k heads in place (v untouched)
+void rope_qk_inplace_(at::Tensor& qkv, const at::Tensor& cosT, const at::Tensor& sinT, int64_t nq, int64_t nkv,
+                      int64_t seq_len, const c10::optional<at::Tensor>& pos) {
+  LLMCTL_CHECK(qkv.is_cuda() && qkv.dim() == 2 && qkv.is_contiguous() && qkv.scalar_type() == at::kBFloat16,
+               "rope_qk_inplace_: qkv must be a contiguous 2-D bf16 GPU tensor");
+  const long T = qkv.size(0);
+  const int NH = nq + 2 * nkv, NR = nq + nkv;
+  LLMCTL_CHECK(qkv.size(1) % NH == 0, "qkv width not divisible by heads");
+  const int D = qkv.size(1) / NH;
+  LLMCTL_CHECK(D % 16 == 0, "head_dim must be a multiple of 16");
+  check_rope_tables(cosT, sinT, D);
+  const bool has_pos = pos.has_value() && pos->defined() && pos->numel() > 0;
+  if (has_pos) {
+    LLMCTL_CHECK(pos->numel() == T && pos->is_cuda() && pos->is_contiguous(), "positions must be contiguous [T] on GPU");
+  } else {
+    LLMCTL_CHECK(seq_len > 0 && cosT.size(0) >= seq_len, "rope table shorter than seq_len");
+  }
+  const long total = T * NR * (D / 16);
+  LLMCTL_CHECK(total < (1L << 31), "rope_qk_inplace_: too many rows for 32-bit indexing");
+  if (total == 0) return;
+  const c10::DeviceGuard g(qkv.device());
+  if (has_pos && pos->scalar_type() == at::kLong)
+    hipLaunchKernelGGL(rope_inplace_kernel<int64_t>, dim3(blocks_for(total)), dim3(256), 0, stream(), bf_mut(qkv),
+                       cosT.data_ptr<float>(), sinT.data_ptr<float>(), pos->data_ptr<int64_t>(), NR, NH, D,
+                       (int)seq_len, (int)total);
+  else
+    hipLaunchKernelGGL(rope_inplace_kernel<int32_t>, dim3(blocks_for(total)), dim3(256), 0, stream(), bf_mut(qkv),
+                       cosT.data_ptr<float>(), sinT.data_ptr<float>(), has_pos ? pos->data_ptr<int32_t>() : nullptr,
+                       NR, NH, D, (int)std::max<int64_t>(seq_len, 1), (int)total);
 }
 
 // Serving: RoPE + split + paged-KV write in one pass (the separate kv_cache_write re-read K/V).
@@ -347,6 +412,7 @@ at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& x) {
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("rope_qkv_fwd", &rope_qkv_fwd);
+  m.impl("rope_qk_inplace_", &rope_qk_inplace_);
   m.impl("rope_qkv_cache_fwd", &rope_qkv_cache_fwd);
   m.impl("rope_qkv_bwd", &rope_qkv_bwd);
   m.impl("swiglu_fwd", &swiglu_fwd);

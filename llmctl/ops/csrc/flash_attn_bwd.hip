@@ -541,7 +541,10 @@ __device__ __forceinline__ f32x16 acc_copy(const f32x16& acc) {
 }
 __device__ __forceinline__ void acc_zero(f32x16& acc) {  // in place ("+a": no second register set)
   const bf16x8_t z = {};  // MFMA A / B take no inline constants, C does
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "+a"(acc) : "v"(z));
+  // z was just written by a VALU v_mov: the MFMA must not read it within 2 wait states (hipcc pads
+  // none inside asm; without the nop the first zeroing MFMA read stale register contents and seeded
+  // dK with garbage / NaN now and then)
+  asm volatile("s_nop 2\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "+a"(acc) : "v"(z));
 }
 
 // dV / dK of one 16-row step with no softmax work beside it (the previous tile's second half)
@@ -860,10 +863,13 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
   constexpr int NP = TILE_B / 1024 / 4;
   constexpr int RC_B = KV_QT * 4;
   constexpr int BUF_B = 2 * TILE_B + 4 * RC_B;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF_B + 64];
-  // item ids handed from thread 0 to the workgroup: [0] the lookahead popped after a cursor switch
-  // (written after a barrier, read after the next one; switches are >= 2 barriers apart), [1] [2]
-  // the first two items
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF_B + 64];  // + item ids
+  // item ids handed from thread 0 to the workgroup: [1] [2] the first two items; [3 + (k & 1)] the
+  // lookahead popped at the k-th cursor switch (written after a barrier, read after the next one).
+  // Two slots: with 2-tile items (the last key block of a head, one q-head per kv-head) a switch
+  // can follow the previous one right after the barrier at which that one's lookahead is read —
+  // one slot let thread 0 overwrite it before the slower waves had read it (waves then disagreed
+  // on the next item)
   int* item_w = reinterpret_cast<int*>(smem + 2 * BUF_B);
 
   const int tid = threadIdx.x;
@@ -910,7 +916,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
   const unsigned short *qh = nullptr, *dh = nullptr;
   const float* rh = nullptr;
   bool look_pending = false;
-  int pend_item = -1;  // the item the cursor entered while compute is still on the previous one
+  int n_switch = 0;  // cursor switches so far (wave-uniform)
+  // items the cursor entered (or -1: the stream ended) that compute has not started, in order: the
+  // cursor switches when it issues an item's LAST tile, so with a 2-tile next item it can switch
+  // twice during one compute item (one variable lost the first of the two: a skipped item)
+  int pend0 = -1, pend1 = -1, npend = 0;
   auto iss_begin = [&](int item) __attribute__((always_inline)) {
     const int bh = bh_base + item / nkb, kb = item % nkb;
     const int bb = bh / a.Hkv, hkk = bh % a.Hkv;
@@ -946,10 +956,13 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
         iss = nxt;
         if (iss >= 0) {
           iss_begin(iss);
-          if (tid == 0) item_w[0] = pop();
+          if (tid == 0) item_w[3 + (n_switch & 1)] = pop();
           look_pending = true;
+          ++n_switch;
         }
-        pend_item = iss;
+        if (npend == 0) pend0 = iss;
+        else pend1 = iss;
+        ++npend;
       }
     }
   };
@@ -972,14 +985,19 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
   // prologue: tile 0's DMA with the K / V fragments under it, one wait, then tile 1's DMA
   issue(std::integral_constant<int, 0>{});
   load_kv(cur);
-  vm_wait_n<0>();
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+a"(kf[0]), "+a"(kf[1]), "+a"(kf[2]), "+a"(kf[3]), "+a"(kf[4]), "+a"(kf[5]), "+a"(kf[6]),
+                 "+a"(kf[7]), "+a"(vf[0]), "+a"(vf[1]), "+a"(vf[2]), "+a"(vf[3]), "+a"(vf[4]), "+a"(vf[5]),
+                 "+a"(vf[6]), "+a"(vf[7])
+               :
+               : "memory");
   __builtin_amdgcn_s_barrier();
   issue(std::integral_constant<int, 1>{});
   f32x16 dk[NDB], dv[NDB];
 #pragma unroll
   for (int d = 0; d < NDB; ++d) {
     const bf16x8_t z = {};
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(dk[d]) : "v"(z));
+    asm volatile("s_nop 2\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(dk[d]) : "v"(z));  // see acc_zero
     asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(dv[d]) : "v"(z));
   }
   const float c = a.scale_log2;
@@ -1080,7 +1098,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
       vm_wait_n<0>();
       __builtin_amdgcn_s_barrier();
       if (look_pending) {
-        nxt = __builtin_amdgcn_readfirstlane(item_w[0]);
+        nxt = __builtin_amdgcn_readfirstlane(item_w[3 + ((n_switch - 1) & 1)]);
         look_pending = false;
       }
       if (iss >= 0) issue(std::integral_constant<int, SL>{});
@@ -1117,7 +1135,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
             asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(sn[d][g]) : "v"(sr + col) : "memory");
           }
       }
-      load_kv(pend_item >= 0 ? pend_item : cur);  // one code path (no next item: a harmless re-load)
+      load_kv(pend0 >= 0 ? pend0 : cur);  // one code path (no next item: a harmless re-load)
       if (rope) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       // the last MFMAs' results -> the AGPR reads below: 8-pass XDL write, 12+ wait states; the "+a"
       // operands order every read after the padding
@@ -1160,13 +1178,23 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
           st8(dvp + d * 32 + 8 * g + 4 * hh, y, 1.f);
         }
       }
-      asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      // the K / V loads retire here: the fragments are operands of this statement, so hipcc cannot
+      // place a register copy of them (e.g. to coalesce the item loop's back edge) before the data
+      // has landed — without them a v_accvgpr_mov could read the in-flight destination
+      asm volatile("s_waitcnt vmcnt(32)"
+                   : "+a"(kf[0]), "+a"(kf[1]), "+a"(kf[2]), "+a"(kf[3]), "+a"(kf[4]), "+a"(kf[5]), "+a"(kf[6]),
+                     "+a"(kf[7]), "+a"(vf[0]), "+a"(vf[1]), "+a"(vf[2]), "+a"(vf[3]), "+a"(vf[4]), "+a"(vf[5]),
+                     "+a"(vf[6]), "+a"(vf[7])
+                   :
+                   : "memory");
     }
     stamp(2);
     ++n_done;
-    if (pend_item < 0) break;  // the stream ended with this item
-    cur = pend_item;
-    pend_item = -1;
+    if (pend0 < 0) break;  // the stream ended with this item
+    cur = pend0;
+    pend0 = pend1;
+    pend1 = -1;
+    --npend;
   }
 }
 
@@ -1411,7 +1439,8 @@ void launch_bwd(const BwdArgs& a, hipStream_t s, bool do_dq, bool do_dkv, int dk
         if (a.S % KV_KB == 0 && (dkv_impl == 3 || dkv_impl == 4 || (dkv_impl < 0 && dkv_mode() == 2))) {
           int* wq = dkv_queue();
           LLMCTL_HIP_CHECK(hipMemsetAsync(wq, 0, 8 * sizeof(int), s));
-          const int nwg = std::min<long>((long)num_cus(), (long)a.B * a.Hkv * nkb);
+          int nwg = std::min<long>((long)num_cus(), (long)a.B * a.Hkv * nkb);
+          if (const char* e = std::getenv("LLMCTL_DKV_NWG")) nwg = std::max(1, std::min(nwg, atoi(e)));  // debug
           if (a.stamps != nullptr)
             hipLaunchKernelGGL(fa_bwd_dkv_persist_kernel<true>, dim3((unsigned)nwg), dim3(256), 0, s, a, wq);
           else

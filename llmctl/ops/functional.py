@@ -219,10 +219,18 @@ class _RopeFlashAttn(torch.autograd.Function):
     gradient dqkv [T, (nq+2nkv)*D] directly — no dq/dk/dv tensors and no rope_bwd pass."""
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, nq, nkv, B, S, positions, doc_start):
-        q, k, v = native().rope_qkv_fwd(qkv, cos, sin, nq, nkv, S, positions)
-        D = q.shape[-1]
-        q, k, v = q.view(B, S, nq, D), k.view(B, S, nkv, D), v.view(B, S, nkv, D)
+    def forward(ctx, qkv, cos, sin, nq, nkv, B, S, positions, doc_start, inplace=False):
+        if inplace:
+            # the caller owns qkv (a projection output nothing else saved): rotate its q / k heads
+            # in place and attend strided views of it — V is neither copied nor re-read
+            native().rope_qk_inplace_(qkv, cos, sin, nq, nkv, S, positions)
+            D = qkv.shape[-1] // (nq + 2 * nkv)
+            qkv4 = qkv.view(B, S, nq + 2 * nkv, D)
+            q, k, v = qkv4[:, :, :nq], qkv4[:, :, nq:nq + nkv], qkv4[:, :, nq + nkv:]
+        else:
+            q, k, v = native().rope_qkv_fwd(qkv, cos, sin, nq, nkv, S, positions)
+            D = q.shape[-1]
+            q, k, v = q.view(B, S, nq, D), k.view(B, S, nkv, D), v.view(B, S, nkv, D)
         scale = D ** -0.5
         o, lse = native().flash_attn_fwd(q, k, v, scale, True, doc_start)
         pos = positions.reshape(-1).int().contiguous() if positions is not None else None
@@ -235,14 +243,18 @@ class _RopeFlashAttn(torch.autograd.Function):
         q, k, v, o, lse, cos, sin, pos = ctx.saved_tensors
         dqkv = native().flash_attn_bwd_qkv(do.contiguous(), q, k, v, o, lse, ctx.scale, True, ctx.doc_start, cos, sin,
                                            pos if ctx.has_pos else None, ctx.S)
-        return dqkv, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None
 
 
-def rope_flash_attention(qkv, cos, sin, nq: int, nkv: int, B: int, S: int, positions=None, doc_start=None):
+def rope_flash_attention(qkv, cos, sin, nq: int, nkv: int, B: int, S: int, positions=None, doc_start=None,
+                         inplace: bool = False):
     """Causal attention on the QKV projection output: RoPE(q, k) -> flash attention -> o
-    ``[B,S,nq,D]``; the backward returns d(qkv) in one fused pass on the HIP path."""
+    ``[B,S,nq,D]``; the backward returns d(qkv) in one fused pass on the HIP path.  ``inplace``
+    (HIP path; the caller's qkv must not be needed afterwards): RoPE rotates qkv's q / k heads in
+    place and attention reads strided views (``LLMCTL_ROPE_INPLACE=0`` disables)."""
     if use_native(qkv) and qkv.is_contiguous():
-        return _RopeFlashAttn.apply(qkv, cos, sin, nq, nkv, B, S, positions, doc_start)
+        inplace = inplace and os.environ.get("LLMCTL_ROPE_INPLACE", "1") != "0"
+        return _RopeFlashAttn.apply(qkv, cos, sin, nq, nkv, B, S, positions, doc_start, inplace)
     q, k, v = rope_qkv(qkv, cos, sin, nq, nkv, S, positions)
     D = q.shape[-1]
     return flash_attention(q.view(B, S, nq, D), k.view(B, S, nkv, D), v.view(B, S, nkv, D), causal=True,

@@ -713,3 +713,30 @@ def test_sampling_greedy_ties_and_odd_vocab(native_lib, V):
     got = native_lib.sample(logits, temp, topk, topp, u)
     exp = torch.tensor([int(torch.nonzero(r == r.max())[0]) for r in logits.float()], device=DEV)
     assert torch.equal(got, exp)
+
+
+@pytest.mark.parametrize("with_pos", [False, True])
+def test_rope_flash_attention_inplace_matches(native_lib, with_pos):
+    """In-place RoPE (rope_qk_inplace_: q / k heads of qkv rotated in place, attention on strided
+    views of qkv) gives bitwise the output and d(qkv) of the copying path."""
+    from llmctl import ops
+
+    B, S, nq, nkv, D = 2, 256, 4, 2, 128
+    T = B * S
+    base = _bf(T, (nq + 2 * nkv) * D, seed=71)
+    cos, sin = ref.rope_tables(S + 40, D, device=DEV)
+    pos = None
+    if with_pos:
+        p = torch.arange(S, dtype=torch.int32)
+        p[S // 2:] -= S // 2
+        pos = p.repeat(B).to(DEV)
+    do = _bf(B, S, nq, D, seed=72)
+    outs = []
+    for inplace in (False, True):
+        leaf = base.clone().requires_grad_(True)
+        qkv = leaf * 1  # a non-leaf the function may rotate in place, as the model's projection output
+        o = ops.rope_flash_attention(qkv, cos, sin, nq, nkv, B, S, pos, inplace=inplace)
+        o.backward(do)
+        outs.append((o.detach(), leaf.grad))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
