@@ -1112,10 +1112,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
       advance(std::integral_constant<int, 1>{});
     }
     stamp(1);
-    // ---- item end: the next item's K / V fragments load under this item's epilogue (dK scaled with
-    //      the RoPE backward fused, dV).  Its memory operations are inline asm with a fixed count
-    //      per wave, so counted waits separate them: vmcnt(16) = the RoPE tables landed (the 16 K / V
-    //      loads after them may fly), vmcnt(32) after the 32 stores = the K / V fragments landed.
+    // ---- item end: dK (scaled, with the RoPE backward fused) and dV stored, then the next item's
+    //      K / V fragments loaded behind the stores and retired by one wait.  The RoPE tables are
+    //      plain loads (see below); the K / V loads come after their last use, so the compiler's
+    //      own wait for the tables never covers them.
     {
       const long tok = (long)b * a.S + my_key;
       unsigned short* dkp = a.dk + tok * a.dk_st + (long)hk * HD;
@@ -1131,12 +1131,14 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int col = d * 32 + 8 * g + 4 * hh;
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(cs[d][g]) : "v"(cr + col) : "memory");
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(sn[d][g]) : "v"(sr + col) : "memory");
+            // plain loads: the compiler tracks them (its waits are conservative around the asm
+            // ops).  As inline-asm loads, hipcc copied the "=v" destinations into other registers
+            // right after issue and reused them for the next addresses while the data was still
+            // in flight — the landing data corrupted a later load's address (illegal access)
+            cs[d][g] = *reinterpret_cast<const f32x4*>(cr + col);
+            sn[d][g] = *reinterpret_cast<const f32x4*>(sr + col);
           }
       }
-      load_kv(pend0 >= 0 ? pend0 : cur);  // one code path (no next item: a harmless re-load)
-      if (rope) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       // the last MFMAs' results -> the AGPR reads below: 8-pass XDL write, 12+ wait states; the "+a"
       // operands order every read after the padding
 #pragma unroll
@@ -1178,10 +1180,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkv_persist_kernel(BwdArgs a, i
           st8(dvp + d * 32 + 8 * g + 4 * hh, y, 1.f);
         }
       }
+      load_kv(pend0 >= 0 ? pend0 : cur);  // one code path (no next item: a harmless re-load)
       // the K / V loads retire here: the fragments are operands of this statement, so hipcc cannot
       // place a register copy of them (e.g. to coalesce the item loop's back edge) before the data
       // has landed — without them a v_accvgpr_mov could read the in-flight destination
-      asm volatile("s_waitcnt vmcnt(32)"
+      asm volatile("s_waitcnt vmcnt(0)"
                    : "+a"(kf[0]), "+a"(kf[1]), "+a"(kf[2]), "+a"(kf[3]), "+a"(kf[4]), "+a"(kf[5]), "+a"(kf[6]),
                      "+a"(kf[7]), "+a"(vf[0]), "+a"(vf[1]), "+a"(vf[2]), "+a"(vf[3]), "+a"(vf[4]), "+a"(vf[5]),
                      "+a"(vf[6]), "+a"(vf[7])
