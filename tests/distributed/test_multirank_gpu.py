@@ -42,6 +42,23 @@ def test_two_rank_zero1_matches_zero0_on_gpu():
     assert abs(z0["final_loss"] - z1["final_loss"]) < 2e-2, (z0["final_loss"], z1["final_loss"])
 
 
+def test_two_rank_dp_side_job_swiglu_backward(tmp_path, monkeypatch):
+    """DP=2 (ZeRO-1) through the side-job SwiGLU backward (the down projection's wgrad GEMM writes
+    the flat-gradient view, its overlap-engine callback fires, and dgu comes from the same kernel)
+    matches the epilogue-fused form.  A 2-layer model at hidden 4096 / ffn 1024 takes the side path
+    at 512 tokens per rank."""
+    cfg = {"name": "side-2l", "arch": "decoder-only", "layers": 2, "hidden": 4096, "ffn": 1024, "heads": 32,
+           "vocab_size": 4096, "rope": {"base": 10000, "scaling": "linear"}}
+    path = tmp_path / "side.json"
+    path.write_text(json.dumps(cfg))
+    out = {}
+    for mode in ("side", "epilogue"):
+        monkeypatch.setenv("LLMCTL_SWIGLU_BWD", mode)
+        out[mode] = _bench("--zero", "1", "--model", str(path))
+    assert out["side"]["config"]["parallelism"] == "dp2-zero1"
+    assert abs(out["side"]["final_loss"] - out["epilogue"]["final_loss"]) < 2e-2, out
+
+
 def _layout_losses(world, layout):
     from llmctl.testing.harness import run_ranks
     from llmctl.testing.workers import train_layout_gpu
