@@ -88,6 +88,29 @@ __device__ __forceinline__ bf16x8_t tr_frag(const unsigned char* base, int row0,
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// tr_frag with the lane's byte offsets precomputed (tr_frag_offs): for row0 % 16 == 0 the tr-image
+// swizzle of rows row0 + 4h + q (+ 8) depends on the lane only, so the address of every fragment
+// of a tile is base + row0 * 2 HD + the lane's (lo, hi) offset of its 32-column block — the row /
+// slot part folds into the ds_read immediate (no per-read address VALU in the loop)
+template <int HD>
+__device__ __forceinline__ void tr_frag_offs(int col0, int lane, int& lo, int& hi) {
+  const int h = lane >> 5;
+  const int i16 = lane & 15;
+  const int q = i16 >> 2, p = i16 & 3;
+  const int col = col0 + 16 * ((lane >> 4) & 1) + 4 * p;
+  const int chunk = col >> 3;
+  const int sub = (col & 7) * 2;
+  lo = tr_off<HD>(4 * h + q, chunk) + sub;
+  hi = tr_off<HD>(8 + 4 * h + q, chunk) + sub;
+}
+template <int HD>
+__device__ __forceinline__ bf16x8_t tr_frag_at(const unsigned char* base, int row0, int lo, int hi) {
+  s4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + row0 * (HD * 2) + lo));
+  s4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + row0 * (HD * 2) + hi));
+  s8_t v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
 // natural-order A fragment of X^T (k = 8h + j) from a tr image: X[row0 + 8h + j][col0 + r]
 template <int HD>
 __device__ __forceinline__ bf16x8_t tr_frag_nat(const unsigned char* base, int row0, int col0, int lane) {

@@ -1298,6 +1298,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     t0 = __builtin_amdgcn_readfirstlane(ds[min(qblk * DQ_QB, a.S - 1)]) / DQ_KB;
   }
   const int key_hi = CAUSAL ? qc : a.S - 1;  // last key this lane's row sees
+  // K^T fragment offsets per 32-column d block (tr_frag_at; the rows kb * 32 + 16 st are multiples
+  // of 16): no per-read address arithmetic in the tile loop
+  int klo[NDB], khi[NDB];
+#pragma unroll
+  for (int d = 0; d < NDB; ++d) tr_frag_offs<HD>(d * 32, lane, klo[d], khi[d]);
 
   // ---- DMA ring (see the forward kernel): K as a tr image, V as a row image
   unsigned vk[PPW], vv[PPW];
@@ -1364,7 +1369,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
       for (int st = 0; st < 2; ++st) {
         const bf16x8_t sbf = to_bf16x8(dsv + 8 * st);
 #pragma unroll
-        for (int d = 0; d < NDB; ++d) dq[d] = mfma32(tr_frag<HD>(Ks, kb * 32 + 16 * st, d * 32, lane), sbf, dq[d]);
+        for (int d = 0; d < NDB; ++d) dq[d] = mfma32(tr_frag_at<HD>(Ks, kb * 32 + 16 * st, klo[d], khi[d]), sbf, dq[d]);
       }
     }
   };

@@ -182,6 +182,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
 
   const float c = a.scale_log2;
   const int key_hi = CAUSAL ? min(my_q, a.S - 1) : a.S - 1;  // last key this lane's row sees
+  // V^T fragment offsets per 32-column d block (tr_frag_at): rows kb * 32 + 16 st are multiples of 16
+  int vlo[NDB], vhi[NDB];
+#pragma unroll
+  for (int d = 0; d < NDB; ++d) tr_frag_offs<HD>(d * 32, lane, vlo[d], vhi[d]);
   // retire the Q loads here: the first in-loop use would otherwise carry a compiler vmcnt(0)
   // on every iteration, i.e. wait for the just-issued DMA of the next tile
 #pragma unroll
@@ -254,7 +258,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int d = 0; d < NDB; ++d) o[d] = mfma32(tr_frag<HD>(Vs, kb * 32 + 16 * st, d * 32, lane), pb[kb][st], o[d]);
+        for (int d = 0; d < NDB; ++d) o[d] = mfma32(tr_frag_at<HD>(Vs, kb * 32 + 16 * st, vlo[d], vhi[d]), pb[kb][st], o[d]);
     if (a.prio) __builtin_amdgcn_s_setprio(0);
   };
 
