@@ -1303,6 +1303,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   int klo[NDB], khi[NDB];
 #pragma unroll
   for (int d = 0; d < NDB; ++d) tr_frag_offs<HD>(d * 32, lane, klo[d], khi[d]);
+  // K (tr image) / V (row image) row-fragment offsets per k-step: both swizzles of rows kb * 32 + r
+  // depend on r only, so kb folds into the ds_read immediate
+  int kro[NKS], vro[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    kro[ks] = tr_off<HD>(r, 2 * ks + hh);
+    vro[ks] = row_off<HD>(r, 2 * ks + hh);
+  }
 
   // ---- DMA ring (see the forward kernel): K as a tr image, V as a row image
   unsigned vk[PPW], vv[PPW];
@@ -1349,8 +1357,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
       for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        s = mfma32(lds_read_b128(Ks, tr_off<HD>(kb * 32 + r, 2 * ks + hh)), qf[ks], s);
-        dp = mfma32(lds_read_b128(Vs, row_off<HD>(kb * 32 + r, 2 * ks + hh)), df[ks], dp);
+        s = mfma32(lds_read_b128(Ks, kb * 32 * (HD * 2) + kro[ks]), qf[ks], s);
+        dp = mfma32(lds_read_b128(Vs, kb * 32 * (HD * 2) + vro[ks]), df[ks], dp);
       }
       if (need_mask) {  // wave-uniform: a scalar branch around branch-free selects
 #pragma unroll

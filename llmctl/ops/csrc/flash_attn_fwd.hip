@@ -186,6 +186,11 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
   int vlo[NDB], vhi[NDB];
 #pragma unroll
   for (int d = 0; d < NDB; ++d) tr_frag_offs<HD>(d * 32, lane, vlo[d], vhi[d]);
+  // K row-fragment offsets per k-step: the row-image swizzle of rows kb * 32 + r depends on r only
+  // (swz_row<HD>(kb * 32 + r) == swz_row<HD>(r)), so kb folds into the ds_read immediate
+  int kofs[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) kofs[ks] = row_off<HD>(r, 2 * ks + hh);
   // retire the Q loads here: the first in-loop use would otherwise carry a compiler vmcnt(0)
   // on every iteration, i.e. wait for the just-issued DMA of the next tile
 #pragma unroll
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) s[kb] = mfma32(lds_read_b128(Ks, row_off<HD>(kb * 32 + r, 2 * ks + hh)), qf[ks], s[kb]);
+      for (int ks = 0; ks < NKS; ++ks) s[kb] = mfma32(lds_read_b128(Ks, kb * 32 * (HD * 2) + kofs[ks]), qf[ks], s[kb]);
     }
     if (need_mask) {  // wave-uniform: a scalar branch around branch-free selects
 #pragma unroll
