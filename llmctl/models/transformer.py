@@ -25,7 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from llmctl import ops
-from llmctl.exec.linear import data_grad, linear, swiglu_data_grad, weight_grad
+from llmctl.exec.linear import data_grad, dgrad64, linear, swiglu_data_grad, weight_grad
 from llmctl.parallel import async_tp
 from llmctl.parallel import context_parallel as cp
 from llmctl.parallel import tensor_parallel as tp
@@ -92,8 +92,11 @@ class _SwiGLUDown(torch.autograd.Function):
         out = F.linear(act, w_down)
         T = gu.numel() // gu.shape[-1]
         ctx.side = gu.requires_grad and wgrad_swiglu_ok(w_down, T, w_down.shape[1])
-        if ctx.side:
-            _prep_weight_t(w_down, T)  # the plain data gradient reads W^T (hipBLASLt forward layout)
+        # the plain data gradient: hipBLASLt's forward layout through W^T (default) or gemm64 reading
+        # W K-major (LLMCTL_SIDE_DGRAD=g64: no W^T copy / transpose for the down projection)
+        ctx.dgrad_g64 = ctx.side and os.environ.get("LLMCTL_SIDE_DGRAD", "blas") == "g64"
+        if ctx.side and not ctx.dgrad_g64:
+            _prep_weight_t(w_down, T)
         ctx.recompute = recompute
         if recompute:
             ctx.save_for_backward(gu, w_down)
@@ -117,7 +120,10 @@ class _SwiGLUDown(torch.autograd.Function):
         if ctx.side:
             # plain data gradient, then the weight gradient computing dgu on the side (gemm64.hip
             # "side job"): the HBM-bound SwiGLU backward streams under the wgrad's MFMAs
-            dact = data_grad(dout2, ctx.wparam)
+            if ctx.dgrad_g64 and _gemm64_dgrad_ok(dout2, w_down):
+                dact = dgrad64(dout2, w_down)
+            else:
+                dact = data_grad(dout2, ctx.wparam)
             dgu = ctx.wparam._llmctl_grad_sink.write_swiglu(ctx.wparam, dout2, act2, dact, gu.reshape(-1, gu.shape[-1]))
             if dgu is not None:
                 return dgu.view(gu.shape), None, None
@@ -128,6 +134,14 @@ class _SwiGLUDown(torch.autograd.Function):
         dw = weight_grad(ctx.wparam, dout2, act2)
         dgu = swiglu_data_grad(dout, ctx.wparam, gu)
         return dgu, dw, None
+
+
+def _gemm64_dgrad_ok(dy2: torch.Tensor, w: torch.Tensor) -> bool:
+    """``dy2 @ w`` on gemm64 (shape / alignment / 32-bit offset limits of ``gemm64_ex``)."""
+    from llmctl.exec.linear import _gemm64_ok
+
+    T, H = dy2.shape
+    return (_gemm64_ok(T, w.shape[1], H, dy2, w) and w.is_contiguous() and H * w.stride(0) * 2 < 2**31)
 
 
 def _fused_fwd_enabled() -> bool:

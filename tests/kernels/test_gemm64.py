@@ -224,13 +224,15 @@ def test_gemm64_wgrad_swiglu(native_lib, T, H, F, cfg, gdt, acc):
 
 
 @pytest.mark.parametrize("main_grad", [False, True])
-def test_swiglu_down_side_job_autograd(native_lib, monkeypatch, main_grad):
+@pytest.mark.parametrize("side_dgrad", ["blas", "g64"])
+def test_swiglu_down_side_job_autograd(native_lib, monkeypatch, main_grad, side_dgrad):
     """_SwiGLUDown with a grad-sink weight: plain data gradient + weight gradient carrying the
     SwiGLU backward (LLMCTL_SWIGLU_BWD=side); two backward passes accumulate into the sink's
     view (bf16 .grad or fp32 main_grad); matches fp32 autograd and the epilogue-fused path."""
     from llmctl.exec.linear import GradSink, wgrad_swiglu_ok
     from llmctl.models.transformer import _SwiGLUDown
 
+    monkeypatch.setenv("LLMCTL_SIDE_DGRAD", side_dgrad)
     T, H, F = 512, 4096, 1024
     gu0 = _bf(T, 2 * F, seed=21)
     w = torch.nn.Parameter(_bf(H, F, seed=22) * 0.02)
