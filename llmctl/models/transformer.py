@@ -149,7 +149,8 @@ def _fused_fwd_enabled() -> bool:
     when ``LLMCTL_FUSED_FWD=1``.  Off by default: on the GPT-7B step the saved RoPE / SwiGLU passes
     (~0.45 ms per layer) are outweighed by gemm64's forward running 4-7 % below hipBLASLt's tuned
     forward kernels (1474-1477 vs 1543-1588 TF on the QKV / gate-up shapes): 842 / 845 ms per step
-    fused vs 837 / 839 ms unfused, same box (profiles/fused_fwd_ab_r3.txt)."""
+    fused vs 837 / 839 ms unfused, same box (profiles/fused_fwd_ab_r3.txt); at micro-batch 16 with the
+    re-tuned hipBLASLt solutions and the in-place RoPE pass, 1111.8 / 1112.9 vs 1091.9 / 1094.3 ms."""
     return os.environ.get("LLMCTL_FUSED_FWD", "0") == "1"
 
 
