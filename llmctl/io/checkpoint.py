@@ -27,6 +27,7 @@ import json
 import os
 import shutil
 import threading
+import time
 from pathlib import Path
 from typing import Any, Dict, List, Optional
 
@@ -159,6 +160,8 @@ class CheckpointManager:
             "zero_stage": c.zero_stage,
         }
 
+        timeout = float(getattr(c, "collective_timeout_s", 1800) or 1800)
+
         def _write():
             try:
                 from safetensors.torch import save_file
@@ -174,64 +177,68 @@ class CheckpointManager:
                     (path / "optimizer" / f"rank_{rank:05d}.index.json").write_text(json.dumps(opt_index))
                 (path / "rng").mkdir(exist_ok=True)
                 torch.save(rng, path / "rng" / f"rank_{rank:05d}.pt")
+                (path / ".done").mkdir(exist_ok=True)
+                (path / ".done" / f"rank_{rank:05d}").write_text("")
+                if e.is_main:
+                    self._commit(path, state, n_shards, world, timeout)
             except BaseException as ex:  # surfaced by wait()
                 self._error = ex
 
         if c.async_checkpoint and not final:
-            self._thread = threading.Thread(target=_write, daemon=True)
+            self._thread = threading.Thread(target=_write, name=f"llmctl-ckpt-{name}", daemon=True)
             self._thread.start()
         else:
             _write()
-        self._commit_after(path, state, n_shards)
+            self.wait()
         return path
 
-    def _commit_after(self, path: Path, state: Dict[str, Any], n_shards: int) -> None:
-        """Metadata + barrier + latest pointer; runs after the shard writes complete."""
+    def _commit(self, path: Path, state: Dict[str, Any], n_shards: int, world: int, timeout: float) -> None:
+        """Rank 0, off the training thread: once every rank's done-marker exists (each rank
+        writes its marker after its own shards), write the metadata and move ``latest``.
+
+        No collective is involved, so a checkpoint becomes durable as soon as the slowest rank's
+        write finishes -- not at the next save -- and a rank killed mid-run never leaves the
+        others blocked in a commit barrier.  A checkpoint whose markers never all appear (a rank
+        died while writing) stays uncommitted: ``latest`` keeps pointing at the previous one."""
         e = self.engine
+        done = path / ".done"
+        deadline = time.time() + timeout
+        while len(list(done.glob("rank_*"))) < world:
+            if time.time() > deadline:
+                raise TimeoutError(f"checkpoint {path}: not every rank finished writing within {timeout:.0f} s")
+            time.sleep(0.05)
+        (path / "config.json").write_text(json.dumps(e.model_config.to_dict(), indent=2))
+        if n_shards > 1:
+            weight_map = {}
+            for f in sorted(path.glob("model-*.safetensors")):
+                from safetensors import safe_open
 
-        def _finish():
-            if self._thread is not None:
-                self._thread.join()
-            if self._error is not None:
-                raise self._error
-
-        self._pending_commit = (path, state, n_shards, _finish)
-        if not (e.config.async_checkpoint and self._thread is not None):
-            self._do_commit()
-
-    def _do_commit(self):
-        pc = getattr(self, "_pending_commit", None)
-        if pc is None:
-            return
-        path, state, n_shards, finish = pc
-        self._pending_commit = None
-        finish()
-        e = self.engine
-        if dist.is_initialized():
-            dist.barrier()
-        if e.is_main:
-            (path / "config.json").write_text(json.dumps(e.model_config.to_dict(), indent=2))
-            (path / "training_state.json").write_text(json.dumps(state, indent=2, default=str))
-            if n_shards > 1:
-                weight_map = {}
-                for f in sorted(path.glob("model-*.safetensors")):
-                    from safetensors import safe_open
-
-                    with safe_open(str(f), "pt") as sf:
-                        for k in sf.keys():
-                            weight_map.setdefault(k, []).append(f.name)
-                (path / "model.safetensors.index.json").write_text(json.dumps(
-                    {"metadata": {"tp": state["layout"]["tp"], "pp": state["layout"]["pp"]},
-                     "weight_map": weight_map}, indent=2))
-            if e.config.plan_file and Path(e.config.plan_file).exists():
-                shutil.copy(e.config.plan_file, path / "plan.toml")
-            (self.root / "latest").write_text(path.name)
-            self._gc()
+                with safe_open(str(f), "pt") as sf:
+                    for k in sf.keys():
+                        weight_map.setdefault(k, []).append(f.name)
+            (path / "model.safetensors.index.json").write_text(json.dumps(
+                {"metadata": {"tp": state["layout"]["tp"], "pp": state["layout"]["pp"]},
+                 "weight_map": weight_map}, indent=2))
+        if e.config.plan_file and Path(e.config.plan_file).exists():
+            shutil.copy(e.config.plan_file, path / "plan.toml")
+        # training_state.json last: its presence marks a complete checkpoint (resume keys on it)
+        tmp = path / "training_state.json.tmp"
+        tmp.write_text(json.dumps(state, indent=2, default=str))
+        os.replace(tmp, path / "training_state.json")
+        shutil.rmtree(done, ignore_errors=True)
+        lt = self.root / "latest.tmp"
+        lt.write_text(path.name)
+        os.replace(lt, self.root / "latest")
+        self._gc()
 
     def wait(self) -> None:
-        if getattr(self, "_pending_commit", None) is not None:
-            self._do_commit()
-        self._thread = None
+        """Join this rank's pending write (rank 0: and its commit); re-raise its error."""
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._error is not None:
+            err, self._error = self._error, None
+            raise err
 
     def _gc(self) -> None:
         keep = self.engine.config.keep_latest or self.engine.config.save_total_limit

@@ -50,7 +50,9 @@ __device__ __forceinline__ void car_signal_wait(const CarArgs& a, unsigned* my_s
     __hip_atomic_store(peer + fo + b * CAR_MAX_RANKS + a.rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* f = my_sig + fo + b * CAR_MAX_RANKS + tid;
     long spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+    // wrap-aware: a peer already one epoch ahead may have overwritten this flag with epoch + 1
+    // (it finished epoch `epoch` after seeing our signal, before we read its) -- that counts too
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1L << 26)) {  // ~seconds: a peer is gone; report instead of hanging
         __hip_atomic_store(my_sig + CAR_ERROR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -169,7 +169,9 @@ class TrainingEngine:
                 # overlapped with backward / forward get their workgroups dispatched ahead of
                 # the GEMM grids, so the last buckets are not left exposed after backward
                 os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
-            dist.init_process_group(backend=backend, **kw)
+            from llmctl.utils.env import init_process_group
+
+            init_process_group(backend, **kw)
         if self.env.world_size > 1 and backend == "gloo" and self.device.type == "cuda":
             # single-GPU multi-rank rehearsal: device tensors cross gloo through host copies
             from llmctl.comms import host_staging
@@ -487,6 +489,9 @@ class TrainingEngine:
             resume = c.output_dir if (Path(c.output_dir) / "latest").exists() else None
         if resume:
             ckpt.load(resume)
+            if self.is_main:
+                log.info("resumed from %s at step %d (restart attempt %s)", resume, self.global_step,
+                         os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
         accum = max(c.gradient_accumulation_steps, 1)
         if self.pipeline is not None:
             accum = self.pipeline.num_microbatches

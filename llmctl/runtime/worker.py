@@ -128,6 +128,9 @@ def resolve(args: argparse.Namespace) -> Dict[str, Any]:
 
 def main(argv: Optional[List[str]] = None) -> int:
     map_mpi_env()
+    from llmctl.utils.env import install_hang_dump
+
+    install_hang_dump()
     args = build_parser().parse_args(argv)
     opts = resolve(args)
     from llmctl.runtime.engine import TrainingEngine, create_training_config

@@ -43,7 +43,10 @@ class TPInferenceEngine(InferenceEngine):
         self.tp_group = tp_group
         self.tp_size = dist.get_world_size(tp_group)
         self.tp_rank = dist.get_rank(tp_group)
+        self._own_control = control_group is None
         self.control = control_group if control_group is not None else dist.new_group(backend="gloo")
+        self._closed = False
+        self._car_checks = 0
         pc = ParallelContext(tp_group=tp_group, tp_size=self.tp_size, tp_rank=self.tp_rank)
         if kw.get("use_graphs", True) and os.environ.get("LLMCTL_TP_GRAPHS", "1") == "0":
             kw["use_graphs"] = False
@@ -136,7 +139,13 @@ class TPInferenceEngine(InferenceEngine):
 
     @torch.inference_mode()
     def decode(self, seqs: List[Sequence]) -> torch.Tensor:
-        return self.decode_exec(self._bcast(self.decode_plan(seqs)))
+        out = self.decode_exec(self._bcast(self.decode_plan(seqs)))
+        self._car_checks += 1
+        if self.car is not None and self._car_checks % self.CAR_CHECK_EVERY == 0:
+            self.car.check()  # a peer timed out inside the custom all-reduce: fail loudly, never serve it
+        return out
+
+    CAR_CHECK_EVERY = 64  # decode steps between reads of the custom all-reduce's error word (one D2H copy)
 
     @torch.inference_mode()
     def mixed(self, chunks, seqs: List[Sequence]) -> torch.Tensor:
@@ -146,6 +155,34 @@ class TPInferenceEngine(InferenceEngine):
         if self.tp_rank == 0:
             self._bcast({"op": "stop"})
         self.release_graphs()
+
+    def close(self) -> None:
+        """Deterministic teardown, never left to garbage collection: drop the captured decode
+        graphs (they hold the RCCL communicator's captured work and the custom all-reduce's peer
+        pointers), drain the device, check + unmap the custom all-reduce buffers after a barrier
+        (no peer may still be reading this rank's IPC memory) and destroy the gloo control group
+        this engine created.  Call after :meth:`stop_workers` (rank 0) / :meth:`worker_loop`
+        returned (other ranks); the default process group stays the caller's."""
+        if self._closed:
+            return
+        self._closed = True
+        self.release_graphs()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        err = None
+        if self.car is not None:
+            try:
+                self.car.check()
+            except RuntimeError as e:
+                err = e
+            dist.barrier(group=self.control)
+            self.car.close()
+            self.car = None
+        if self._own_control and self.control is not None:
+            dist.destroy_process_group(self.control)
+        self.control = None
+        if err is not None:
+            raise err
 
     @torch.inference_mode()
     def worker_loop(self) -> None:
@@ -174,7 +211,9 @@ def init_tp(backend: str = "auto"):
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(env.local_rank)
-        dist.init_process_group(backend=backend)
+        from llmctl.utils.env import init_process_group
+
+        init_process_group(backend)
     dev = f"cuda:{env.local_rank}" if torch.cuda.is_available() else "cpu"
     return None, dev  # the whole world is one TP group (one node, TP <= 8)
 
@@ -201,6 +240,7 @@ def main(argv=None) -> int:
                             block_size=a.block_size, scheduler=a.scheduler, use_graphs=not a.no_graphs)
     if eng.tp_rank != 0:
         eng.worker_loop()
+        eng.close()
         dist.destroy_process_group()
         return 0
     from .server import InferenceServer
@@ -210,6 +250,7 @@ def main(argv=None) -> int:
                         max_batch_tokens=a.max_batch_tokens, max_concurrent=a.max_concurrent, engine=eng).run()
     finally:
         eng.stop_workers()
+        eng.close()
         dist.destroy_process_group()
     return 0
 

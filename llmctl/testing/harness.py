@@ -23,10 +23,9 @@ def _entry(rank, world, port, fn, args, q):
     import torch
 
     torch.set_num_threads(1)
-    if os.environ.get("LLMCTL_HANG_DUMP"):  # debugging aid: stacks of every rank after N s
-        import faulthandler
+    from llmctl.utils.env import install_hang_dump
 
-        faulthandler.dump_traceback_later(float(os.environ["LLMCTL_HANG_DUMP"]), exit=False)
+    install_hang_dump()  # debugging aid: LLMCTL_HANG_DUMP=<s> prints every rank's stacks after s seconds
     try:
         out = fn(rank, world, *args)
         import io

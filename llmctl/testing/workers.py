@@ -144,6 +144,7 @@ def serve_generate(rank: int, world: int, max_tokens: int = 8, model: str = "tin
         eng = TPInferenceEngine(model, **kw)
         if eng.tp_rank != 0:
             eng.worker_loop()
+            eng.close()
             return {}
     seqs = eng.generate(PROMPTS, SamplingParams(max_tokens=max_tokens, temperature=0.0))
     # Sequence-object prefill: two fresh prompts through the public entry point
@@ -158,53 +159,38 @@ def serve_generate(rank: int, world: int, max_tokens: int = 8, model: str = "tin
         eng.kv.free_sequence(s.seq_id)
     if world > 1:
         eng.stop_workers()
+        eng.close()
     return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": eng.kv_cache.k.shape[-2],
             "prefill_logits": logits}
 
 
-def serve_generate_gpu(rank: int, world: int, max_tokens: int = 8) -> dict:
-    """GPU serving with TP=world ranks sharing cuda:0 (gloo control/data plane; RCCL cannot put
-    two ranks on one device): the decode step, including the custom IPC all-reduces and the
-    vocab gather, is captured in a hipGraph and replayed.  world == 1: the plain engine."""
-    import os
-
-    import torch
+def serve_tp_rccl_gpu(rank: int, world: int, max_tokens: int = 10) -> dict:
+    """The TP serving engine on an RCCL process group (world 1: one GPU per rank is RCCL's
+    rule) with decode hipGraphs: the vocab-parallel embedding's all-reduce and the logits gather
+    run as RCCL collectives captured inside the graph.  Teardown is explicit (``close()`` then
+    ``destroy_process_group``), never garbage collection; returns the TP and the plain
+    engine's greedy tokens."""
     import torch.distributed as dist
 
+    from llmctl.serve.engine import InferenceEngine
     from llmctl.serve.scheduler import SamplingParams
+    from llmctl.serve.tp import TPInferenceEngine
 
     torch.cuda.set_device(0)
-    kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=64, block_size=16, max_model_len=256,
-              max_batch_tokens=512, seed=0, use_graphs=True)
-    kw.update(engine_kw or {})
-    prompts = PROMPTS + [[(5 * i) % 500 + 1 for i in range(40)]]
-    if world == 1:
-        from llmctl.serve.engine import InferenceEngine
-
-        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
-            os.environ.pop(k, None)
-        eng = InferenceEngine("tiny", **kw)
-    else:
-        from llmctl.serve.tp import TPInferenceEngine
-
-        dist.init_process_group("gloo")
-        eng = TPInferenceEngine("tiny", **kw)
-        assert eng.car is not None, "custom all-reduce not active"
-        if eng.tp_rank != 0:
-            eng.worker_loop()
-            eng.release_graphs()
-            dist.barrier()
-            eng.car.close()
-            return {}
-    seqs = eng.generate(prompts, SamplingParams(max_tokens=max_tokens, temperature=0.0))
-    out = {"tokens": [s.output_ids for s in seqs], "graph_replays": eng.stats["graph_replays"]}
-    if world > 1:
-        eng.stop_workers()
-        eng.release_graphs()
-        eng.car.check()
-        dist.barrier()
-        eng.car.close()
-    return out
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    prompts = [[1, 2, 3, 4, 5], [9] * 37, [7, 7]]
+    p = SamplingParams(max_tokens=max_tokens, temperature=0.0)
+    kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16, max_model_len=512)
+    tpe = TPInferenceEngine("tiny", use_graphs=True, **kw)
+    a = [s.output_ids for s in tpe.generate(prompts, p)]
+    replays = tpe.stats["graph_replays"]
+    tpe.stop_workers()
+    tpe.close()
+    del tpe
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+    b = [s.output_ids for s in InferenceEngine("tiny", use_graphs=False, **kw).generate(prompts, p)]
+    return {"tp": a, "plain": b, "graph_replays": replays}
 
 
 def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters: int = 20,
@@ -499,9 +485,7 @@ def serve_forced_gpu(rank: int, world: int, max_tokens: int = 8, model: str = "t
         assert eng.car is not None, "custom all-reduce not active"
         if eng.tp_rank != 0:
             eng.worker_loop()
-            eng.release_graphs()
-            dist.barrier()
-            eng.car.close()
+            eng.close()
             return {}
     seqs = [eng.add_request(p, SamplingParams(max_tokens=max_tokens, temperature=0.0)) for p in prompts]
     idx = {s.seq_id: i for i, s in enumerate(seqs)}
@@ -530,8 +514,5 @@ def serve_forced_gpu(rank: int, world: int, max_tokens: int = 8, model: str = "t
            "logits": torch.stack([torch.stack(rec[i]) for i in range(len(seqs))])}
     if world > 1:
         eng.stop_workers()
-        eng.release_graphs()
-        eng.car.check()
-        dist.barrier()
-        eng.car.close()
+        eng.close()
     return res

@@ -53,3 +53,38 @@ def local_device(prefer: str = "auto"):
     if prefer in ("cuda", "gpu", "hip"):
         raise RuntimeError("a GPU was requested but torch.cuda.is_available() is False")
     return torch.device("cpu")
+
+
+def init_process_group(backend: str, **kw) -> None:
+    """``torch.distributed.init_process_group`` that survives torchrun's elastic restarts.
+
+    Under torchrun's static rendezvous the agent hosts ONE TCPStore for the whole job and hands
+    it to every restart attempt unprefixed (``torch/distributed/rendezvous.py``: "We create a new
+    TCPStore for every retry" -- not true for the static handler).  The restarted workers then
+    read the dead attempt's keys: gloo's full-mesh bootstrap picks up a killed peer's listening
+    address ("connectFullMesh failed ... Connection refused") and the store barrier counts stale
+    arrivals.  Here every attempt gets its own key space, ``llmctl/attempt_<restart count>/``,
+    on a client of the agent's store."""
+    import datetime
+
+    import torch.distributed as dist
+
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True" and "store" not in kw:
+        from torch.distributed import PrefixStore, TCPStore
+
+        env = dist_env()
+        timeout = kw.get("timeout") or datetime.timedelta(seconds=300)
+        base = TCPStore(env.master_addr, env.master_port, env.world_size, is_master=False, timeout=timeout)
+        attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+        kw.update(store=PrefixStore(f"llmctl/attempt_{attempt}", base), rank=env.rank, world_size=env.world_size)
+    dist.init_process_group(backend=backend, **kw)
+
+
+def install_hang_dump() -> None:
+    """``LLMCTL_HANG_DUMP=<seconds>``: every thread's Python stack goes to stderr after that many
+    seconds (and again every period), so a hung rank names the call it is stuck in."""
+    s = os.environ.get("LLMCTL_HANG_DUMP")
+    if s:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(s), repeat=True, exit=False)

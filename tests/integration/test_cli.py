@@ -130,8 +130,12 @@ def test_health_check_json(tmp_path):
 
 
 def test_elastic_restart_after_rank_kill(tmp_path):
-    """Fault injection (LLMCTL_FAULT) kills rank 1 after step 3 of a 2-process gloo run; the
-    elastic restart resumes from checkpoint-2 and finishes all 5 steps."""
+    """Fault injection (LLMCTL_FAULT) kills rank 1 after step 3 of a 2-process gloo run.
+    torchrun's own restart (not the orchestrator's whole-job relaunch) re-forms the group on a
+    fresh store key space, resumes from checkpoint-2 (committed asynchronously right after its
+    write, before the fault) and finishes all 5 steps.  The run is its own process group and is
+    killed as a whole on timeout; ranks dump their stacks if they hang."""
+    import signal
     import socket
 
     with socket.socket() as s:
@@ -139,13 +143,30 @@ def test_elastic_restart_after_rank_kill(tmp_path):
         port = s.getsockname()[1]
     out = tmp_path / "run"
     env = dict(os.environ, PYTHONPATH=str(ROOT), LLMCTL_DEVICE="cpu", LLMCTL_FAULT="kill_rank:1@step:3",
-               LLMCTL_MASTER_PORT=str(port), OMP_NUM_THREADS="2")
-    r = subprocess.run([sys.executable, "-m", "llmctl", "train", "launch", "--model", "tiny", "--device", "cpu",
-                        "--gpus-per-node", "2", "--max-steps", "5", "--batch-size", "2", "--seq-len", "32",
-                        "--save-steps", "2", "--max-restarts", "1", "--mixed-precision", "fp32",
-                        "--output-dir", str(out)], capture_output=True, text=True, env=env, timeout=900)
-    _ok(r)
+               LLMCTL_MASTER_PORT=str(port), OMP_NUM_THREADS="2", LLMCTL_HANG_DUMP="150")
+    p = subprocess.Popen([sys.executable, "-m", "llmctl", "train", "launch", "--model", "tiny", "--device", "cpu",
+                          "--gpus-per-node", "2", "--max-steps", "5", "--batch-size", "2", "--seq-len", "32",
+                          "--save-steps", "2", "--max-restarts", "1", "--mixed-precision", "fp32",
+                          "--output-dir", str(out)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         env=env, start_new_session=True)
+    try:
+        stdout, _ = p.communicate(timeout=300)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        stdout, _ = p.communicate()
+        raise AssertionError("elastic run hung; output tail:\n" + stdout[-6000:])
+    finally:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)  # nothing of the run may outlive the test
+        except ProcessLookupError:
+            pass
+    assert p.returncode == 0, stdout[-6000:]
     assert (out / ".faults" / "kill_rank-1-3").exists()
+    assert "[orchestrator] exit code" not in stdout, "recovered by the orchestrator, not torchrun"
+    import re
+
+    flat = " ".join(stdout.split())  # the console wraps long log lines
+    assert re.search(r"resumed from \S+ at step 2 \(restart attempt 1\)", flat), stdout[-4000:]
     st = json.loads((out / "final" / "training_state.json").read_text())
     assert st["global_step"] == 5
     man = json.loads((out / "run_manifest.json").read_text())

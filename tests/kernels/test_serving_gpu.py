@@ -44,36 +44,15 @@ def test_sampling_params_respected(native_lib):
 
 
 def test_tp_engine_rccl_world1_with_graphs(native_lib):
-    """The TP serving path on RCCL (world size 1 in-process): vocab-parallel embedding,
+    """The TP serving path on RCCL (world size 1, in a child process so that a native fault in
+    communicator teardown fails this test, not the session): vocab-parallel embedding,
     all-reduces and the logits all-gather run inside the captured decode hipGraph."""
-    import os
+    from llmctl.testing.harness import run_ranks
+    from llmctl.testing.workers import serve_tp_rccl_gpu
 
-    import torch.distributed as dist
-
-    from llmctl.serve.engine import InferenceEngine
-    from llmctl.serve.scheduler import SamplingParams
-    from llmctl.serve.tp import TPInferenceEngine
-    from llmctl.testing.harness import free_port
-
-    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port())})
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    try:
-        prompts = [[1, 2, 3, 4, 5], [9] * 37, [7, 7]]
-        p = SamplingParams(max_tokens=10, temperature=0.0)
-        kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16, max_model_len=512)
-        tpe = TPInferenceEngine("tiny", use_graphs=True, **kw)
-        a = tpe.generate(prompts, p)
-        tpe.stop_workers()
-        b = InferenceEngine("tiny", use_graphs=False, **kw).generate(prompts, p)
-        assert tpe.stats["graph_replays"] > 0
-        assert [s.output_ids for s in a] == [s.output_ids for s in b]
-    finally:
-        import gc
-
-        tpe = None
-        gc.collect()
-        torch.cuda.synchronize()
-        dist.destroy_process_group()
+    out = run_ranks(serve_tp_rccl_gpu, 1, 10, timeout=240)[0]
+    assert out["graph_replays"] > 0
+    assert out["tp"] == out["plain"]
 
 
 def _row_err(got, want):
