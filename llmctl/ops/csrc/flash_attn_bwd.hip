@@ -30,6 +30,8 @@
 // delta = rowsum(dO * O) is computed by the dQ kernel (its dO rows are in registers) and read by
 // the dK/dV kernel launched after it.
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "attn_common.h"
 
@@ -1427,14 +1429,18 @@ int dkv_mode() {
   return m;
 }
 
-// the persistent dK/dV kernel's per-XCD item counters (one buffer per device, zeroed before every
-// launch on the launch's stream)
-int* dkv_queue() {
-  static int* q[64] = {nullptr};
+// the persistent dK/dV kernel's per-XCD item counters: one buffer per (device, stream), zeroed
+// before every launch on that stream.  Launches on one stream are ordered, so they may share a
+// buffer; two streams (or threads launching on them) never do.  The map is mutex-guarded.
+int* dkv_queue(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, int*> bufs;
   int dev = 0;
   LLMCTL_HIP_CHECK(hipGetDevice(&dev));
-  if (q[dev] == nullptr) LLMCTL_HIP_CHECK(hipMalloc(&q[dev], 64 * sizeof(int)));
-  return q[dev];
+  std::lock_guard<std::mutex> lk(mu);
+  int*& q = bufs[{dev, s}];
+  if (q == nullptr) LLMCTL_HIP_CHECK(hipMalloc(&q, 64 * sizeof(int)));
+  return q;
 }
 
 // dkv_impl: -1 = default (LLMCTL_DKV_PIPE), 0 = unpipelined kernel, 1 = pipelined where built
@@ -1454,10 +1460,14 @@ void launch_bwd(const BwdArgs& a, hipStream_t s, bool do_dq, bool do_dkv, int dk
       }
       if constexpr (!DOC) {  // persistent form: S % 128 (>= 2 tiles per item)
         if (a.S % KV_KB == 0 && (dkv_impl == 3 || dkv_impl == 4 || (dkv_impl < 0 && dkv_mode() == 2))) {
-          int* wq = dkv_queue();
+          int* wq = dkv_queue(s);
           LLMCTL_HIP_CHECK(hipMemsetAsync(wq, 0, 8 * sizeof(int), s));
           int nwg = std::min<long>((long)num_cus(), (long)a.B * a.Hkv * nkb);
-          if (const char* e = std::getenv("LLMCTL_DKV_NWG")) nwg = std::max(1, std::min(nwg, atoi(e)));  // debug
+          // per-XCD queues (B*Hkv % 8 == 0) are drained by blocks with blockIdx & 7 == queue:
+          // fewer than 8 workgroups would leave queues without a consumer
+          const int min_wg = ((long)a.B * a.Hkv) % 8 == 0 ? 8 : 1;
+          if (const char* e = std::getenv("LLMCTL_DKV_NWG")) nwg = std::max(min_wg, std::min(nwg, atoi(e)));  // debug
+          nwg = std::max(nwg, min_wg);
           if (a.stamps != nullptr)
             hipLaunchKernelGGL(fa_bwd_dkv_persist_kernel<true>, dim3((unsigned)nwg), dim3(256), 0, s, a, wq);
           else

@@ -193,9 +193,9 @@ __device__ __forceinline__ int tile_pos(int ip) {
 }
 
 // per-thread byte offset (relative to the operand's tile origin at k = 0) of DMA piece i
-template <bool T, int KIND>
+template <bool T, int KIND, int NT = NTHR>
 __device__ __forceinline__ unsigned stage_voff(int i, int tid, long ld) {
-  const int c = i * NTHR + tid;  // 16-B chunk index in the half-tile image
+  const int c = i * NT + tid;  // 16-B chunk index in the half-tile image
   if constexpr (!T) {
     const int ir = c >> 3, pc = c & 7;
     const int row = tile_pos<KIND>(ir);
@@ -768,6 +768,261 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   }
 }
 
+
+// ---- 4-wave kernel (config variant 6): one 128x128 output block per wave ---------------------
+// The 8-wave kernel above reads (128 + 64) x 64 operand elements from LDS per wave per K-tile for
+// a 128x64 block: 192 KB of ds_read per CU per K-tile, 75 % of the MFMA time of the tile at the
+// LDS's 256 B/clk.  hipBLASLt's MT256x256x64 kernel (rocprof: 256 threads, 130 KB LDS, 252 VGPRs)
+// gives each of 4 waves a 128x128 block instead: (128 + 128) x 64 per wave, 128 KB per CU per
+// K-tile (-33 % LDS traffic per FLOP; a ds_read costs power the MFMA clock pays for).  Same
+// staging as above (half-tile images, LDS-DMA, swizzles, clamped tail items, XCD remap, split
+// tail); what changes:
+//   * waves (wr, wc) = (wave >> 1, wave & 1): rows wr*128 + [0,128) = m-tiles 0-3 in A_lo at image
+//     positions wr*64.., m-tiles 4-7 in A_hi; cols wc*128 + [0,128) = all of half-tile B_h{wc}.
+//     acc[8][8] (256 fp32 per lane) lives in the accumulation registers (one wave per SIMD).
+//   * one wave per SIMD means no ping-pong partner: each phase's MFMAs run on fragments read in
+//     the PREVIOUS phase, while this phase's ds_reads (for the next) and DMA issue go out under
+//     them.  Phase plan of K-tile t (buffer t & 1), 32 MFMAs each, one barrier at the end:
+//        P0  MFMA (m0-3, n0-3) [a_lo, b03]   read b47   <- B(t)      issue A_lo(t+2)  vmcnt(20)
+//        P1  MFMA (m0-3, n4-7) [a_lo, b47]   read a_hi  <- A_hi(t)   issue B_h0(t+2)  vmcnt(20)
+//        P2  MFMA (m4-7, n4-7) [a_hi, b47]   read a_lo  <- A_lo(t+1) issue B_h1(t+2)  vmcnt(16)
+//        P3  MFMA (m4-7, n0-3) [a_hi, b03]   read b03'  <- B(t+1)    issue A_hi(t+2)  -
+//     b03 is double-buffered by K-tile parity (it is read for t+1 while t's is still in use).
+//     RAW: each phase ends with vmcnt(N) retiring exactly the half-tile the next phase reads, then
+//     lgkmcnt(0) + s_barrier.  WAR: every DMA goes into a slot whose last ds_reads were issued at
+//     least one phase earlier (so retired before that phase's closing barrier).  The waits keep 4-5
+//     half-tiles (16-20 DMA instructions per thread) in flight.
+constexpr int NT4 = 256;
+// one row of a 4x4 MFMA block: accumulators %(4i + j) += B frag %(20 + j) x A frag %(16 + i)
+#define G4W_MF(d, b, a) "v_mfma_f32_16x16x32_bf16 %" #d ", %" #b ", %" #a ", %" #d "\n\t"
+#define G4W_ROW_(d0, d1, d2, d3, a) G4W_MF(d0, 20, a) G4W_MF(d1, 21, a) G4W_MF(d2, 22, a) G4W_MF(d3, 23, a)
+#define G4W_ROW(i, a) G4W_ROW_I(i, a)
+#define G4W_ROW_I(i, a) G4W_ROW_##i(a)
+#define G4W_ROW_0(a) G4W_ROW_(0, 1, 2, 3, a)
+#define G4W_ROW_1(a) G4W_ROW_(4, 5, 6, 7, a)
+#define G4W_ROW_2(a) G4W_ROW_(8, 9, 10, 11, a)
+#define G4W_ROW_3(a) G4W_ROW_(12, 13, 14, 15, a)
+
+// a 64x64 quadrant x K = 64: two asm statements of 16 MFMAs with the accumulators pinned to the
+// accumulation registers ("+a"; hipcc's own MFMA selection moved them through VGPRs and spilled:
+// 256 accumulators + 160 fragment registers exceed the 256 VGPRs).  Hazards (guide §5.7 item 2):
+// s_nop 1 ahead for operands a compiler VALU / v_accvgpr_write just wrote; MFMA -> MFMA
+// accumulate chains need none; the epilogue's reads are fenced after the loop.
+template <int m0, int n0>
+__device__ __forceinline__ void g4w_mma(f32x4_t (&acc)[8][8], const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    asm volatile("s_nop 1\n\t"
+                 G4W_ROW(0, 16) G4W_ROW(1, 17) G4W_ROW(2, 18) G4W_ROW(3, 19)
+                 : "+a"(acc[m0][n0]), "+a"(acc[m0][n0 + 1]), "+a"(acc[m0][n0 + 2]), "+a"(acc[m0][n0 + 3]),
+                   "+a"(acc[m0 + 1][n0]), "+a"(acc[m0 + 1][n0 + 1]), "+a"(acc[m0 + 1][n0 + 2]), "+a"(acc[m0 + 1][n0 + 3]),
+                   "+a"(acc[m0 + 2][n0]), "+a"(acc[m0 + 2][n0 + 1]), "+a"(acc[m0 + 2][n0 + 2]), "+a"(acc[m0 + 2][n0 + 3]),
+                   "+a"(acc[m0 + 3][n0]), "+a"(acc[m0 + 3][n0 + 1]), "+a"(acc[m0 + 3][n0 + 2]), "+a"(acc[m0 + 3][n0 + 3])
+                 : "v"(A[0][ks]), "v"(A[1][ks]), "v"(A[2][ks]), "v"(A[3][ks]),
+                   "v"(B[0][ks]), "v"(B[1][ks]), "v"(B[2][ks]), "v"(B[3][ks]));
+  }
+}
+
+__device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
+  asm volatile("s_nop 7\n\ts_nop 7"
+               : "+a"(acc[4][0]), "+a"(acc[4][1]), "+a"(acc[4][2]), "+a"(acc[4][3]), "+a"(acc[5][0]), "+a"(acc[5][1]),
+                 "+a"(acc[5][2]), "+a"(acc[5][3]), "+a"(acc[6][0]), "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][3]),
+                 "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]));
+}
+
+template <bool AT, bool BT, int EPI, int GROUP>
+__global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(G64Args args) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  const int bid = blockIdx.x;
+  int wg, sp = -1, u = 0;
+  if (bid < args.n_main) {
+    const int nwg = args.n_main;
+    const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
+    wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
+  } else {
+    const int i = bid - args.n_main;
+    u = i / args.splits;
+    sp = i - u * args.splits;
+    wg = args.n_main + u;
+  }
+  const int per_group = GROUP * args.tiles_n;
+  const int grp = wg / per_group;
+  const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
+  const int inner = wg - grp * per_group;
+  const int tm = grp * GROUP + inner % gsz;
+  const int tn = inner / gsz;
+
+  const long lda = args.lda, ldb = args.ldb;
+  const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
+  const unsigned short* Bb = BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
+  const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
+  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
+  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
+  const int KT = sp < 0 ? args.K / TK : args.kt_part;
+  const unsigned kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
+
+  unsigned vo[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    vo[A_LO][i] = stage_voff<AT, A_LO, NT4>(i, tid, lda);
+    vo[A_HI][i] = stage_voff<AT, A_HI, NT4>(i, tid, lda);
+    vo[B_H0][i] = stage_voff<BT, B_H0, NT4>(i, tid, ldb);
+    vo[B_H1][i] = stage_voff<BT, B_H1, NT4>(i, tid, ldb);
+  }
+  const unsigned lds0 = lds_addr(smem) + wave * 1024;
+  auto issue = [&](auto kind_c, int t) {
+    constexpr int kind = decltype(kind_c)::value;
+    const unsigned tc = kt0 + (unsigned)(t < KT ? t : KT - 1);
+    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
+    const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
+    const i32x4_t r = kind <= A_HI ? ra : rb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bdma16(r, vo[kind][i], so, l + i * 4096);
+  };
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ap = wr * 64;
+  const int bo = (B_H0 + wc) * HALF;
+  bf16x8_t a_lo[4][2], a_hi[4][2], b47[4][2], b03[2][4][2];
+  auto rdA = [&](bf16x8_t (&d)[4][2], const unsigned char* img) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) d[i][ks] = frag<AT>(img, ap + 16 * i, ks, lane);
+  };
+  auto rdB = [&](bf16x8_t (&d)[4][2], const unsigned char* img, int n0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) d[j][ks] = frag<BT>(img, 16 * (n0 + j), ks, lane);
+  };
+  auto mma = [&](auto m0_c, auto n0_c, const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2]) {
+    g4w_mma<decltype(m0_c)::value, decltype(n0_c)::value>(acc, A, B);
+  };
+  // lgkmcnt(0) through the builtin: hipcc's waitcnt pass then knows the fragment reads are done
+  // (an asm wait is opaque to it, and it re-waited lgkmcnt(0) ahead of the next MFMA block --
+  // after the NEXT phase's reads had been issued, serialising them)
+  auto sync = [&](auto n_c) {
+    constexpr int N = decltype(n_c)::value;
+    if constexpr (N >= 0) wait_vm<N>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
+    bar();
+  };
+
+  // prologue: K-tiles 0 and 1 in flight; retire A_lo(0) / B(0), read a_lo / b03 of K-tile 0
+  issue(K_<A_LO>{}, 0);
+  issue(K_<B_H0>{}, 0);
+  issue(K_<B_H1>{}, 0);
+  issue(K_<A_HI>{}, 0);
+  issue(K_<A_LO>{}, 1);
+  issue(K_<B_H0>{}, 1);
+  issue(K_<B_H1>{}, 1);
+  issue(K_<A_HI>{}, 1);
+  wait_vm<20>();
+  bar();
+  rdA(a_lo, smem + A_LO * HALF);
+  rdB(b03[0], smem + bo, 0);
+  sync(K_<-1>{});  // WAR: P0 restages A_lo of this buffer
+
+  auto ktile = [&](int t, auto par_c) {
+    constexpr int P = decltype(par_c)::value;
+    const unsigned char* buf = smem + P * BUF;
+    const unsigned char* nbuf = smem + (P ^ 1) * BUF;
+    // P0
+    rdB(b47, buf + bo, 4);
+    issue(K_<A_LO>{}, t + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(K_<0>{}, K_<0>{}, a_lo, b03[P]);
+    sync(K_<20>{});
+    // P1
+    rdA(a_hi, buf + A_HI * HALF);
+    issue(K_<B_H0>{}, t + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(K_<0>{}, K_<4>{}, a_lo, b47);
+    sync(K_<20>{});
+    // P2
+    rdA(a_lo, nbuf + A_LO * HALF);
+    issue(K_<B_H1>{}, t + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(K_<4>{}, K_<4>{}, a_hi, b47);
+    sync(K_<16>{});
+    // P3
+    rdB(b03[P ^ 1], nbuf + bo, 0);
+    issue(K_<A_HI>{}, t + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(K_<4>{}, K_<0>{}, a_hi, b03[P]);
+    sync(K_<-1>{});
+  };
+  for (int t = 0; t < KT; t += 2) {
+    ktile(t, K_<0>{});
+    ktile(t + 1, K_<1>{});
+  }
+  wait_vm<0>();  // the clamped tail items are still landing
+  // the last phase's MFMA results -> the epilogue's accumulator reads: 16 wait states (every
+  // other accumulator was last written >= 32 MFMAs earlier)
+  g4w_fence(acc);
+
+  // ---- epilogue: lane holds C[wr*128 + 16 i + (l & 15)][wc*128 + 16 j + 4 (l >> 4) + r]
+  const int g = lane >> 4, i16 = lane & 15;
+  if (sp >= 0) {
+    float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 128 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + 16 * j) = acc[i][j];
+    return;
+  }
+  if constexpr (epi_f32(EPI)) {
+    float* Cf = reinterpret_cast<float*>(args.c) + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (EPI == EPI_ACC_F32) {
+        f32x4_t old[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j) = old[j] + acc[i][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j) = acc[i][j];
+      }
+    }
+    return;
+  }
+  unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + 4 * g;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s2_t old[8];
+    if constexpr (EPI == EPI_ACC) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f32x4_t v = acc[i][j];
+      if constexpr (EPI == EPI_ACC) {
+        v[0] += bf2f(old[j][0] & 0xffff);
+        v[1] += bf2f(old[j][0] >> 16);
+        v[2] += bf2f(old[j][1] & 0xffff);
+        v[3] += bf2f(old[j][1] >> 16);
+      }
+      s2_t o;
+      o[0] = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+      o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      *reinterpret_cast<s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j) = o;
+    }
+  }
+}
+
 // ---- persistent variant ------------------------------------------------------------------------
 // Measured (profiles/gemm_ld_probe_r3.txt): the same kernel runs ~1450 TF at K = 4096 and
 // ~1525 TF at K = 11008-32000 — a fixed per-tile cost (workgroup launch, the prologue's pipeline
@@ -1104,6 +1359,12 @@ void launch_g(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
   const dim3 grid(n_items), block(NTHR);
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
+  if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI)) {
+    if (variant == 6) {  // 4-wave kernel: 128x128 per wave
+      hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP>), grid, dim3(NT4), 0, stream(), g);
+      variant = -1;
+    }
+  }
   if constexpr (!fused_fwd) {
     if (variant == 5) {  // persistent: one workgroup per CU walks the items
       const dim3 pgrid(min(n_items, num_cus()));
@@ -1218,8 +1479,9 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
     g.ws = ws.data_ptr<float>();
   }
   const int grp = (int)(config % 1000);
-  if (f32_out) {  // fp32 main gradients: the persistent or the variant-1 schedule only
-    const int c = (grp / 100) % 10 == 5 ? 500 + grp % 100 : 100 + grp % 100;
+  if (f32_out) {  // fp32 main gradients: the 4-wave, persistent or variant-1 schedule only
+    const int v = (grp / 100) % 10;
+    const int c = (v == 5 || v == 6 ? v * 100 : 100) + grp % 100;
     if (accumulate) launch<true, true, EPI_ACC_F32>(g, c);
     else launch<true, true, EPI_STORE_F32>(g, c);
     return;

@@ -362,6 +362,8 @@ class PipelineSchedule:
         return loss
 
     # ------------------------------------------------------------------ interleaved 1F1B
+    INFLIGHT_ROUNDS = 2  # interleaved schedule: send/recv groups kept un-waited behind the current round
+
     def _run_interleaved(self, batches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Virtual-stage schedule: rank s owns model chunks c = 0..V-1 = virtual stages
         c*P + s; activations go to virtual stage +1 (rank s+1, or rank 0's next chunk after
@@ -432,6 +434,14 @@ class PipelineSchedule:
                 for k in keys:
                     arrive[k] = works
                 inflight.append((works, sent))
+                # bounded backlog: a round's sends are retired two rounds later, so the sent
+                # activations / input gradients (and their irecv twins) are freed as the schedule
+                # goes instead of all M*V of them living until the end of the step.  Both ends
+                # posted round r-2's group in round r-2, so this wait never blocks on the future
+                while len(inflight) > self.INFLIGHT_ROUNDS:
+                    inflight.pop(0)[0].wait()
+                self.peak_inflight_tensors = max(getattr(self, "peak_inflight_tensors", 0),
+                                                 sum(len(t) for _, t in inflight))
         for works, _ in inflight:
             works.wait()
         self._set_sync(True)

@@ -228,6 +228,12 @@ class TrainingEngine:
         align = 64 * max(dp, 1)
         grad_dtype = self._main_grad_dtype()
         self.grad_dtype = grad_dtype
+        if grad_dtype != c.dtype and self.is_main:
+            n = sum(p.numel() for p in self.model.parameters())
+            log.info("main gradients in %s (main_grads=%s: grad accumulation / PP): +%.2f GB of gradient memory "
+                     "and %dx the DP bucket bytes vs %s", str(grad_dtype).replace("torch.", ""), c.main_grads,
+                     n * (4 - torch.tensor([], dtype=c.dtype).element_size()) / 1e9,
+                     4 // torch.tensor([], dtype=c.dtype).element_size(), str(c.dtype).replace("torch.", ""))
         bucket_numel = int(c.bucket_mb * 2**20 / torch.tensor([], dtype=grad_dtype).element_size())
         self.grad_sink = None
         if c.zero_stage >= 3 and dp > 1:
@@ -286,7 +292,9 @@ class TrainingEngine:
         if pg.layout.ep > 1:
             experts = [(n, p) for n, p in self.model.named_parameters() if getattr(p, "expert", False)]
             edp = dp // pg.layout.ep
-            self.eflat = FlatParameters(experts, bucket_numel=bucket_numel, align=64 * edp)
+            # expert gradients stay in the parameter dtype: size their buckets by that element
+            ebucket = int(c.bucket_mb * 2**20 / torch.tensor([], dtype=c.dtype).element_size())
+            self.eflat = FlatParameters(experts, bucket_numel=ebucket, align=64 * edp)
             self.eopt = FlatAdamW(self.eflat, lr=c.learning_rate, betas=tuple(c.betas), eps=c.eps,
                                   weight_decay=c.weight_decay, max_grad_norm=c.gradient_clipping,
                                   dp_group=pg.edp_group, zero_stage=0)

@@ -89,7 +89,8 @@ def train_layout(rank: int, world: int, steps: int, layout: dict, model: str = "
             losses.append(float(lt))
     ev = eng.evaluate([make_batch(vocab, cfg.seq_len, cfg.batch_size, 99, 0)])
     full = eng.gather_full_state_dict()
-    return {"losses": losses, "state": full if rank == 0 else None, "eval": ev}
+    return {"losses": losses, "state": full if rank == 0 else None, "eval": ev,
+            "peak_inflight": getattr(eng.pipeline, "peak_inflight_tensors", None)}
 
 
 def train_reference(steps: int, dp: int, model: str = "tiny", micro_per_rank: int = 1,

@@ -76,4 +76,12 @@ def test_dp4_accum4_fp32_main_grads_drift():
     d32 = max(abs(a - b) for a, b in zip(f32["losses"], ref["losses"]))
     d16 = max(abs(a - b) for a, b in zip(b16["losses"], ref["losses"]))
     assert d32 < 0.05, (d32, d16)
-    assert d32 <= d16 * 1.25 + 2e-3, (d32, d16)
+
+    # the discriminating metric: relative distance of the final parameters from the fp32-gradient
+    # run's.  The loss curves of the two modes are indistinguishable at this scale (both drift
+    # ~2e-3); the parameters are not (recorded 0.18 vs 0.22): fp32 main grads must land closer.
+    def pdist(run):  # max over tensors of |p - p_ref| / |p_ref| (as recorded in the profile)
+        return max(float((run["state"][k] - v).norm() / v.norm().clamp_min(1e-30)) for k, v in ref["state"].items())
+
+    p32, p16 = pdist(f32), pdist(b16)
+    assert p32 < 0.9 * p16, (p32, p16)

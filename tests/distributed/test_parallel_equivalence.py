@@ -131,6 +131,12 @@ def test_interleaved_pp_matches_single(pp, vstages, micro):
     _losses_close(out[0]["losses"], ref["losses"])
     _losses_close([out[0]["eval"]], [ref["eval"]])
     _close(out[0]["state"], ref["state"])
+    # bounded send backlog: at most INFLIGHT_ROUNDS rounds x (one activation + one gradient)
+    # sent tensors alive on any rank, not every micro-batch's (M * V) for the whole step
+    from llmctl.parallel.pipeline import PipelineSchedule
+
+    for o in out:
+        assert o["peak_inflight"] is not None and o["peak_inflight"] <= 2 * PipelineSchedule.INFLIGHT_ROUNDS
 
 
 def test_interleaved_pp2_dp2_zero1_matches_single():
