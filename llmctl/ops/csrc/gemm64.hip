@@ -823,6 +823,21 @@ __device__ __forceinline__ void g4w_mma(f32x4_t (&acc)[8][8], const bf16x8_t (&A
   }
 }
 
+// one row block (4 MFMAs: acc row i x n-tiles n0..n0+3, one K-slice).  The "memory" clobber pins
+// the LDS fragment reads and DMA issues placed between two such statements to their gap: the
+// K-loop interleaves its loads with the MFMA stream instead of issuing them all ahead of it
+// (one wave per SIMD: an instruction waiting behind a busy MFMA pipe stalls the wave's issue).
+__device__ __forceinline__ void g4w_row(f32x4_t& c0, f32x4_t& c1, f32x4_t& c2, f32x4_t& c3, const bf16x8_t& a,
+                                        const bf16x8_t& b0, const bf16x8_t& b1, const bf16x8_t& b2, const bf16x8_t& b3) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %5, %4, %0\n\t"
+               "v_mfma_f32_16x16x32_bf16 %1, %6, %4, %1\n\t"
+               "v_mfma_f32_16x16x32_bf16 %2, %7, %4, %2\n\t"
+               "v_mfma_f32_16x16x32_bf16 %3, %8, %4, %3"
+               : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
+               : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+               : "memory");
+}
+
 __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
   asm volatile("s_nop 7\n\ts_nop 7"
                : "+a"(acc[4][0]), "+a"(acc[4][1]), "+a"(acc[4][2]), "+a"(acc[4][3]), "+a"(acc[5][0]), "+a"(acc[5][1]),
@@ -830,7 +845,7 @@ __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
                  "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]));
 }
 
-template <bool AT, bool BT, int EPI, int GROUP>
+template <bool AT, bool BT, int EPI, int GROUP, bool IL>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(G64Args args) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -918,6 +933,30 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     bar();
   };
 
+  // interleaved phase (IL): 8 row blocks of 4 MFMAs (K-slice ks = r >> 2, row i = r & 3); after
+  // block r the r-th fragment read of the next phase's set (A: m-tile f >> 1 / K-slice f & 1; B:
+  // n-tile / K-slice) and, after even r, one quarter of the phase's DMA half-tile
+  auto il_phase = [&](auto m0_c, auto n0_c, const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2], auto rd_b_c,
+                      bf16x8_t (&dst)[4][2], const unsigned char* img, int p0, auto kind_c, int t) {
+    constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
+    constexpr bool RDB = decltype(rd_b_c)::value;
+    constexpr int kind = decltype(kind_c)::value;
+    const unsigned tc = kt0 + (unsigned)(t < KT ? t : KT - 1);
+    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
+    const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
+    const i32x4_t rr = kind <= A_HI ? ra : rb;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int ks = r >> 2, i = r & 3;
+      g4w_row(acc[m0 + i][n0], acc[m0 + i][n0 + 1], acc[m0 + i][n0 + 2], acc[m0 + i][n0 + 3], A[i][ks], B[0][ks],
+              B[1][ks], B[2][ks], B[3][ks]);
+      const int f = r >> 1, fk = r & 1;
+      if constexpr (RDB) dst[f][fk] = frag<BT>(img, p0 + 16 * f, fk, lane);
+      else dst[f][fk] = frag<AT>(img, p0 + 16 * f, fk, lane);
+      if ((r & 1) == 0) bdma16(rr, vo[kind][r >> 1], so, l + (r >> 1) * 4096);
+    }
+  };
+
   // prologue: K-tiles 0 and 1 in flight; retire A_lo(0) / B(0), read a_lo / b03 of K-tile 0
   issue(K_<A_LO>{}, 0);
   issue(K_<B_H0>{}, 0);
@@ -962,9 +1001,27 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     mma(K_<4>{}, K_<0>{}, a_hi, b03[P]);
     sync(K_<-1>{});
   };
+  auto ktile_il = [&](int t, auto par_c) {
+    constexpr int P = decltype(par_c)::value;
+    const unsigned char* buf = smem + P * BUF;
+    const unsigned char* nbuf = smem + (P ^ 1) * BUF;
+    il_phase(K_<0>{}, K_<0>{}, a_lo, b03[P], std::true_type{}, b47, buf + bo, 64, K_<A_LO>{}, t + 2);
+    sync(K_<20>{});
+    il_phase(K_<0>{}, K_<4>{}, a_lo, b47, std::false_type{}, a_hi, buf + A_HI * HALF, ap, K_<B_H0>{}, t + 2);
+    sync(K_<20>{});
+    il_phase(K_<4>{}, K_<4>{}, a_hi, b47, std::false_type{}, a_lo, nbuf + A_LO * HALF, ap, K_<B_H1>{}, t + 2);
+    sync(K_<16>{});
+    il_phase(K_<4>{}, K_<0>{}, a_hi, b03[P], std::true_type{}, b03[P ^ 1], nbuf + bo, 0, K_<A_HI>{}, t + 2);
+    sync(K_<-1>{});
+  };
   for (int t = 0; t < KT; t += 2) {
-    ktile(t, K_<0>{});
-    ktile(t + 1, K_<1>{});
+    if constexpr (IL) {
+      ktile_il(t, K_<0>{});
+      ktile_il(t + 1, K_<1>{});
+    } else {
+      ktile(t, K_<0>{});
+      ktile(t + 1, K_<1>{});
+    }
   }
   wait_vm<0>();  // the clamped tail items are still landing
   // the last phase's MFMA results -> the epilogue's accumulator reads: 16 wait states (every
@@ -1360,8 +1417,9 @@ void launch_g(const G64Args& g, int variant) {
   const dim3 grid(n_items), block(NTHR);
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
   if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI)) {
-    if (variant == 6) {  // 4-wave kernel: 128x128 per wave
-      hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP>), grid, dim3(NT4), 0, stream(), g);
+    if (variant == 6 || variant == 7) {  // 4-wave kernel: 128x128 per wave (7: loads interleaved)
+      if (variant == 7) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, true>), grid, dim3(NT4), 0, stream(), g);
+      else hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, false>), grid, dim3(NT4), 0, stream(), g);
       variant = -1;
     }
   }
@@ -1481,7 +1539,7 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   const int grp = (int)(config % 1000);
   if (f32_out) {  // fp32 main gradients: the 4-wave, persistent or variant-1 schedule only
     const int v = (grp / 100) % 10;
-    const int c = (v == 5 || v == 6 ? v * 100 : 100) + grp % 100;
+    const int c = (v >= 5 ? v * 100 : 100) + grp % 100;
     if (accumulate) launch<true, true, EPI_ACC_F32>(g, c);
     else launch<true, true, EPI_STORE_F32>(g, c);
     return;

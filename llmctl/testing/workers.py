@@ -394,7 +394,7 @@ def async_tp_check(rank: int, world: int, T: int = 24, K: int = 16, N: int = 12)
 
 
 def train_layout_gpu(rank: int, world: int, steps: int, layout: dict, model: str = "tiny",
-                     micro_per_rank: int = 4) -> dict:
+                     micro_per_rank: int = 4, ref_dp: int = 1) -> dict:
     """``train_layout`` on the GPU kernel path (bf16, HIP kernels) with every rank on cuda:0:
     world > 1 runs over gloo with host-staged collectives (``llmctl.comms.host_staging`` — RCCL
     cannot put two ranks on one device), world == 1 is the single-process reference (the
@@ -420,14 +420,18 @@ def train_layout_gpu(rank: int, world: int, steps: int, layout: dict, model: str
     nmb = eng.pipeline.num_microbatches if eng.pipeline is not None else micro_per_rank
     dev = torch.device("cuda", 0)
     losses = []
+    # world == 1 with ref_dp > 1: the single process accumulates every DP rank's micro-batches
+    dps = [eng.pg.dp_rank] if world > 1 else list(range(ref_dp))
     for s in range(steps):
-        batches = [tuple(t.to(dev) for t in make_batch(vocab, cfg.seq_len, cfg.batch_size, s, eng.pg.dp_rank, i))
-                   for i in range(nmb)]
+        batches = [tuple(t.to(dev) for t in make_batch(vocab, cfg.seq_len, cfg.batch_size, s, d, i))
+                   for d in dps for i in range(nmb)]
         loss = eng.train_step(batches)["loss"]
         losses.append(eng.pipeline.broadcast_loss(loss) if eng.pipeline is not None else float(loss))
     ev = eng.evaluate([tuple(t.to(dev) for t in make_batch(vocab, cfg.seq_len, cfg.batch_size, 99, 0))])
     torch.cuda.synchronize()
-    return {"losses": losses, "eval": ev, "native": bool(_lib.load()), "backend": eng.backend}
+    return {"losses": losses, "eval": ev, "native": bool(_lib.load()), "backend": eng.backend,
+            "zero3": getattr(eng, "zero3", None) is not None, "pp": eng.pg.layout.pp, "dp": eng.pg.layout.dp,
+            "max_mem_gb": torch.cuda.max_memory_allocated() / 2**30}
 
 
 def train_drift(rank: int, world: int, steps: int, main_grads: str, precision: str = "bf16") -> dict:

@@ -59,11 +59,11 @@ def test_two_rank_dp_side_job_swiglu_backward(tmp_path, monkeypatch):
     assert abs(out["side"]["final_loss"] - out["epilogue"]["final_loss"]) < 2e-2, out
 
 
-def _layout_losses(world, layout):
+def _layout_losses(world, layout, model="tiny", ref_dp=1, timeout=150):
     from llmctl.testing.harness import run_ranks
     from llmctl.testing.workers import train_layout_gpu
 
-    return run_ranks(train_layout_gpu, world, 3, layout, timeout=150)
+    return run_ranks(train_layout_gpu, world, 3, layout, model, 4, ref_dp, timeout=timeout)
 
 
 @pytest.mark.parametrize("async_tp", ["1", "0"])
@@ -75,6 +75,21 @@ def test_tp2_pp2_sp2_four_ranks_one_gpu(monkeypatch, async_tp):
     ref = _layout_losses(1, {})[0]
     out = _layout_losses(4, {"tp": 2, "pp": 2, "sp": True, "microbatches": 4})
     assert all(o["native"] for o in out) and out[0]["backend"] == "gloo"
+    for a, b in zip(out[0]["losses"], ref["losses"]):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (out[0]["losses"], ref["losses"])
+    assert abs(out[0]["eval"] - ref["eval"]) < 3e-2, (out[0]["eval"], ref["eval"])
+
+
+def test_config4_pp4_dp2_zero3_eight_ranks_one_gpu():
+    """BASELINE config #4's layout (PP4 x DP2 with ZeRO-3, the planner's Llama-3-70B plan) as 8
+    ranks on cuda:0 over host-staged gloo: bf16 HIP kernels, ZeRO-3 per-layer parameter
+    all-gathers + gradient reduce-scatters across the DP pair of every stage, and the 1F1B
+    schedule's device-tensor p2p.  An 8-layer model (2 per stage); the losses follow one process
+    accumulating both DP ranks' micro-batches."""
+    ref = _layout_losses(1, {}, "tiny-deep", ref_dp=2)[0]
+    out = _layout_losses(8, {"pp": 4, "zero": 3, "microbatches": 4}, "tiny-deep", timeout=240)
+    assert all(o["native"] and o["zero3"] and o["pp"] == 4 and o["dp"] == 2 for o in out)
+    assert out[0]["backend"] == "gloo"
     for a, b in zip(out[0]["losses"], ref["losses"]):
         assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (out[0]["losses"], ref["losses"])
     assert abs(out[0]["eval"] - ref["eval"]) < 3e-2, (out[0]["eval"], ref["eval"])
