@@ -38,7 +38,7 @@ def parse():
     # micro-batch 16 (round 3): 30.44k vs 29.97k tok/s at mb 12 on one box (the per-step optimizer
     # pass and the GEMM tails amortise over 33 % more tokens), 244 vs 212 GB of the 288 GB HBM3E
     # (profiles/bench_r3_mb16.txt); round 1 had measured mb 12-16 flat within noise
-    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("LLMCTL_BENCH_MB", "16")))
+    ap.add_argument("--micro-batch", type=int, default=16)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)

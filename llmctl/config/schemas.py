@@ -138,6 +138,15 @@ class TrainConfigSchema(_Open):
     checkpoint: CheckpointSection = CheckpointSection()
     training: TrainingSection = TrainingSection()
     telemetry: Dict[str, Any] = {}
+    # performance knobs (llmctl.config.knobs.PerfKnobs fields): kernel / schedule choices
+    perf: Dict[str, Any] = {}
+
+    @field_validator("perf")
+    @classmethod
+    def _known_knobs(cls, v: Dict[str, Any]) -> Dict[str, Any]:
+        from llmctl.config.knobs import _coerce
+
+        return {k: _coerce(k, x) for k, x in v.items()}  # unknown names / bad values raise
 
 
 class DataConfigSchema(_Open):
@@ -231,6 +240,8 @@ def resolve_training_config(train_file: Optional[Dict[str, Any]] = None, plan: O
         mx = t.data.get("max_length") if isinstance(t.data, dict) else None
         if mx:
             out["seq_len"] = int(mx)
+        if t.perf:
+            out["perf_knobs"] = dict(t.perf)
         if t.model.get("config_file"):
             out["model_name_or_path"] = t.model["config_file"]
         elif t.model.get("name"):

@@ -26,14 +26,16 @@ _state = {"enabled": None}
 
 
 def enable_tuned_gemms(path: Optional[str] = None) -> bool:
-    """Load pre-tuned GEMM solutions (idempotent).  ``LLMCTL_GEMM_TUNING=0`` disables;
+    """Load pre-tuned GEMM solutions (idempotent).  knob ``gemm_tuning`` off disables;
     ``LLMCTL_GEMM_TUNING_FILE`` overrides the file."""
     if _state["enabled"] is not None:
         return _state["enabled"]
     _state["enabled"] = False
     import torch
 
-    if os.environ.get("LLMCTL_GEMM_TUNING", "1") == "0" or not torch.cuda.is_available() or torch.version.hip is None:
+    from llmctl.config.knobs import knobs
+
+    if not knobs().gemm_tuning or not torch.cuda.is_available() or torch.version.hip is None:
         return False
     f = Path(path or os.environ.get("LLMCTL_GEMM_TUNING_FILE", str(DEFAULT_FILE)))
     if not f.is_file():

@@ -22,33 +22,32 @@ Round 2: weight gradients run on the in-house 64-deep MFMA kernel (``gemm64_ex``
 llmctl/ops/csrc/gemm64.hip; 20-40 % over hipBLASLt on the GPT-7B shapes).  Data gradients: the
 down projection's runs on gemm64 with the SwiGLU backward in its epilogue; the others run on
 hipBLASLt's forward layout through the ``W^T`` copies, which measured 0.7 % faster per step
-than gemm64 for all of them (``LLMCTL_DGRAD64``, see ``dgrad64_shape_ok``).
+than gemm64 for all of them (knob ``dgrad64``, see ``dgrad64_shape_ok``).
 """
 
 from __future__ import annotations
 
 from typing import Callable, List, Optional
 
-import os
-
 import torch
 import torch.nn.functional as F
 
+from llmctl.config.knobs import knobs
 
-# gemm64_ex config: tile-order group 4, schedule variant 1 (DMA issued in the read section)
-# — the fastest of the A/B in profiles/gemm64_variants_r2.jsonl on every GPT-7B shape.  A
-# tuning cache (llmctl.plugins.tuning_cache) can override it per layout or per exact shape.
-GEMM64_CONFIG = int(os.environ.get("LLMCTL_GEMM64_CONFIG", "104"))
-GEMM64_CONFIGS = {"dgrad": GEMM64_CONFIG, "wgrad": GEMM64_CONFIG, "fwd": GEMM64_CONFIG}
+
+# gemm64_ex config: knob gemm64_config (default: tile-order group 4, schedule variant 1 — the
+# fastest 8-wave schedule of profiles/gemm64_variants_r2.jsonl).  A tuning cache
+# (llmctl.plugins.tuning_cache) can override it per layout or per exact shape.
+GEMM64_CONFIGS: dict = {}  # layout -> config
 GEMM64_SHAPE_CONFIGS: dict = {}  # (layout, M, N, K) -> config
 
 
 def gemm64_config(layout: str, M: int, N: int, K: int) -> int:
-    return GEMM64_SHAPE_CONFIGS.get((layout, M, N, K), GEMM64_CONFIGS.get(layout, GEMM64_CONFIG))
+    return GEMM64_SHAPE_CONFIGS.get((layout, M, N, K), GEMM64_CONFIGS.get(layout, knobs().gemm64_config))
 
 
 def _gemm64_enabled() -> bool:
-    return os.environ.get("LLMCTL_GEMM64", "1") != "0"  # =0: A/B against the older paths
+    return knobs().gemm64  # False: A/B against hipBLASLt
 
 
 def _rows_ok(*ts: torch.Tensor) -> bool:
@@ -77,9 +76,9 @@ def fwd64_pick(M: int, N: int, K: int) -> bool:
     profiles/gemm64_fwd_small_m_r2.jsonl (up at 2048: 0.278 vs 0.422 ms); in situ, inside a
     GPT-7B 2k prefill, hipBLASLt picks a better up-projection kernel (0.268 ms) and the gain is
     ~1.5 ms per prefill (TTFT p50 28.0 vs 29.5 ms, profiles/ttft_fwd64_r2.txt).
-    ``LLMCTL_FWD64=0`` disables, ``=all`` forces every supported shape (A/B)."""
-    mode = os.environ.get("LLMCTL_FWD64", "1")
-    if mode == "0" or not _gemm64_enabled():
+    Knob ``fwd64``: ``off`` disables, ``all`` forces every supported shape (A/B)."""
+    mode = knobs().fwd64
+    if mode == "off" or not _gemm64_enabled():
         return False
     if mode == "all":
         return True
@@ -107,14 +106,14 @@ def dgrad64_shape_ok(tokens: int, w: torch.Tensor, fused: bool = False) -> bool:
     """Will ``dx = dy W`` for ``tokens`` rows run on gemm64?  (Decided at forward time: the
     weight's W^T copy is only kept for layers whose data gradient cannot.)  ``fused``: the
     down-projection data gradient with the SwiGLU backward in its epilogue.
-    ``LLMCTL_DGRAD64``: fused (default) = only the SwiGLU-fused down-projection data gradient on
-    gemm64, the rest on hipBLASLt's forward layout through the W^T copies; 1 = every data
-    gradient on gemm64 (no W^T copies, ~10 GB less memory for GPT-7B); 0 = none.  Same-box GPT-7B
+    Knob ``dgrad64``: fused (default) = only the SwiGLU-fused down-projection data gradient on
+    gemm64, the rest on hipBLASLt's forward layout through the W^T copies; all = every data
+    gradient on gemm64 (no W^T copies, ~10 GB less memory for GPT-7B); off = none.  Same-box GPT-7B
     step A/B (profiles/bench_r2_dgrad_modes.txt): fused 832.0 / 833.9 ms, 0 833.9 / 832.7 ms,
     1 837.7 / 839.7 ms."""
     out, inn = w.shape
-    mode = os.environ.get("LLMCTL_DGRAD64", "fused")
-    if mode == "0" or (mode == "fused" and not fused):
+    mode = knobs().dgrad64
+    if mode == "off" or (mode == "fused" and not fused):
         return False
     return _gemm64_ok(tokens, inn, out, w) and out * w.stride(0) * 2 < 2**31
 
@@ -141,7 +140,7 @@ def _gemm_ex_ok(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
         return False
     from llmctl.ops._lib import use_native
 
-    if not use_native(g) or os.environ.get("LLMCTL_WGRAD_KERNEL", "1") == "0":  # =0: hipBLASLt (A/B)
+    if not use_native(g) or not knobs().wgrad_kernel:  # off: hipBLASLt (A/B)
         return False
     M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
     if M % 256 or N % 256 or K % 32 or K == 0:
@@ -199,11 +198,11 @@ def side_chunks(M: int, N: int, K: int, T: int, F: int) -> int:
 
 
 def swiglu_side_mode() -> str:
-    """Where the MLP's SwiGLU backward runs (``LLMCTL_SWIGLU_BWD``): ``side`` (default) = as a side
+    """Where the MLP's SwiGLU backward runs (knob ``swiglu_bwd``): ``side`` (default) = as a side
     job of the down projection's weight-gradient GEMM (``gemm64_wgrad_swiglu``), the data
     gradient a plain GEMM; ``epilogue`` = in the data-gradient GEMM's store epilogue
-    (``gemm64_swiglu_dgrad``, round 2); ``0`` = separate elementwise kernel."""
-    return os.environ.get("LLMCTL_SWIGLU_BWD", "side")
+    (``gemm64_swiglu_dgrad``, round 2); ``separate`` = separate elementwise kernel."""
+    return knobs().swiglu_bwd
 
 
 def wgrad_swiglu_ok(w: torch.nn.Parameter, tokens: int, F: int) -> bool:
@@ -237,7 +236,7 @@ class GradSink:
     def __init__(self, transpose_dgrad: Optional[bool] = None):
         self.callbacks: List[Callable[[torch.nn.Parameter], None]] = []
         if transpose_dgrad is None:
-            transpose_dgrad = os.environ.get("LLMCTL_DGRAD_TRANSPOSE", "1") != "0"
+            transpose_dgrad = knobs().dgrad_transpose
         self.transpose_dgrad = transpose_dgrad
         self.epoch = 0  # bumped by the engine after every optimizer step / weight load
 
@@ -284,7 +283,7 @@ class GradSink:
 
     @staticmethod
     def _side_stream_ok() -> bool:
-        return os.environ.get("LLMCTL_WT_SIDE_STREAM", "1") != "0" and not torch.cuda.is_current_stream_capturing()
+        return knobs().wt_side_stream and not torch.cuda.is_current_stream_capturing()
 
     @classmethod
     def _side_stream(cls, device) -> "torch.cuda.Stream":
@@ -405,7 +404,7 @@ def swiglu_data_grad(dy: torch.Tensor, w: torch.nn.Parameter, gu: torch.Tensor) 
     dy2 = dy.reshape(-1, dy.shape[-1])
     gu2 = gu.reshape(-1, gu.shape[-1])
     if (dgrad64_ok(dy2, w, fused=True) and gu2.is_contiguous() and gu2.data_ptr() % 16 == 0
-            and os.environ.get("LLMCTL_FUSED_SWIGLU", "1") != "0"):  # =0: unfused (A/B)
+            and swiglu_side_mode() != "separate"):  # separate: unfused (A/B)
         from llmctl.ops._lib import native
 
         cfg = gemm64_config("dgrad", dy2.shape[0], w.shape[1], w.shape[0])

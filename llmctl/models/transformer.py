@@ -16,7 +16,6 @@ Parallelism hooks (see ``llmctl.parallel``):
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -25,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from llmctl import ops
+from llmctl.config.knobs import knobs
 from llmctl.exec.linear import data_grad, dgrad64, linear, swiglu_data_grad, weight_grad
 from llmctl.parallel import async_tp
 from llmctl.parallel import context_parallel as cp
@@ -92,9 +92,9 @@ class _SwiGLUDown(torch.autograd.Function):
         out = F.linear(act, w_down)
         T = gu.numel() // gu.shape[-1]
         ctx.side = gu.requires_grad and wgrad_swiglu_ok(w_down, T, w_down.shape[1])
-        # the plain data gradient: hipBLASLt's forward layout through W^T (default) or gemm64 reading
-        # W K-major (LLMCTL_SIDE_DGRAD=g64: no W^T copy / transpose for the down projection)
-        ctx.dgrad_g64 = ctx.side and os.environ.get("LLMCTL_SIDE_DGRAD", "blas") == "g64"
+        # the plain data gradient: gemm64 reading W K-major when knob dgrad64 = all, else
+        # hipBLASLt's forward layout through the W^T copy
+        ctx.dgrad_g64 = ctx.side and knobs().dgrad64 == "all"
         if ctx.side and not ctx.dgrad_g64:
             _prep_weight_t(w_down, T)
         ctx.recompute = recompute
@@ -146,12 +146,12 @@ def _gemm64_dgrad_ok(dy2: torch.Tensor, w: torch.Tensor) -> bool:
 
 def _fused_fwd_enabled() -> bool:
     """Training-forward GEMMs with fused epilogues (gemm64 ``EPI_ROPE_QKV`` / ``EPI_UP_SWIGLU``)
-    when ``LLMCTL_FUSED_FWD=1``.  Off by default: on the GPT-7B step the saved RoPE / SwiGLU passes
+    when knob ``fused_fwd``.  Off by default: on the GPT-7B step the saved RoPE / SwiGLU passes
     (~0.45 ms per layer) are outweighed by gemm64's forward running 4-7 % below hipBLASLt's tuned
     forward kernels (1474-1477 vs 1543-1588 TF on the QKV / gate-up shapes): 842 / 845 ms per step
     fused vs 837 / 839 ms unfused, same box (profiles/fused_fwd_ab_r3.txt); at micro-batch 16 with the
     re-tuned hipBLASLt solutions and the in-place RoPE pass, 1111.8 / 1112.9 vs 1091.9 / 1094.3 ms."""
-    return os.environ.get("LLMCTL_FUSED_FWD", "0") == "1"
+    return knobs().fused_fwd
 
 
 def _gemm64_rows(x2: torch.Tensor, w: torch.Tensor) -> bool:
@@ -326,7 +326,7 @@ class DecoderLayer(nn.Module):
     def _fused_qkv_ok(self, x, rope) -> bool:
         if not (_fused_fwd_enabled() and rope is not None and self.bqkv is None and self.D == 128
                 and self.nq % 2 == 0 and self.nkv % 2 == 0 and self.pc.cp_size == 1 and not self._async_sp()
-                and torch.is_grad_enabled() and os.environ.get("LLMCTL_FUSED_ROPE_ATTN", "1") != "0"):
+                and torch.is_grad_enabled() and knobs().fused_rope_attn):
             return False
         return _gemm64_rows(x.reshape(-1, x.shape[-1]), self.wqkv) and rope[0].shape[-1] == 64
 
@@ -339,7 +339,7 @@ class DecoderLayer(nn.Module):
             qkv = async_tp.column_parallel_sp(xn, self.wqkv, self.bqkv, self.pc.tp_group)
         else:
             qkv = linear(self._col_in(xn), self.wqkv, self.bqkv)
-        if rope is not None and self.pc.cp_size == 1 and os.environ.get("LLMCTL_FUSED_ROPE_ATTN", "1") != "0":
+        if rope is not None and self.pc.cp_size == 1 and knobs().fused_rope_attn:
             # RoPE + attention with the RoPE backward fused into the attention backward's stores
             o = ops.rope_flash_attention(qkv, rope[0], rope[1], self.nq, self.nkv, B, S, positions, doc_start,
                                          inplace=True)

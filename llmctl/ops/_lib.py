@@ -34,6 +34,15 @@ def load(force: bool = False) -> bool:
         _error = None
     except Exception as e:  # pragma: no cover - depends on the box
         _error = f"failed to load {LIB_PATH}: {e}"
+    if _loaded:
+        from llmctl.config.knobs import push_native
+
+        push_native()  # the launchers' knob table starts from the active PerfKnobs
+    return _loaded
+
+
+def loaded() -> bool:
+    """True once the library is loaded (no load attempt)."""
     return _loaded
 
 
@@ -53,6 +62,5 @@ def native():
 def use_native(t: torch.Tensor) -> bool:
     if not t.is_cuda:
         return False
-    if os.environ.get("LLMCTL_FORCE_REF") == "1":  # debugging aid only; tests assert it is unset
-        return False
-    return True
+    # debugging aid only (kernel tests assert it is unset; one oracle test toggles it at run time)
+    return os.environ.get("LLMCTL_FORCE_REF") != "1"

@@ -10,6 +10,8 @@ int64_t car_ipc_open(const at::Tensor& handle);
 void car_ipc_close(int64_t ptr);
 int64_t car_sig_words();
 int64_t car_error(int64_t sig_ptr);
+void set_knob(const std::string& name, int64_t value);  // knobs.cpp
+void clear_knobs();
 }  // namespace llmctl
 
 TORCH_LIBRARY(llmctl, m) {
@@ -50,7 +52,6 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("decode_qkv_rope_cache(Tensor x, Tensor w, Tensor? bias, Tensor cos, Tensor sin, int nq, int nkv, Tensor positions, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> Tensor");
   m.def("decode_up_swiglu(Tensor x, Tensor w, Tensor? bias) -> Tensor");
   m.def("decode_linear_partials(Tensor x, Tensor w) -> Tensor");
-  m.def("paged_attention_decode_qkv(Tensor qkv_ws, Tensor? bias, Tensor cos, Tensor sin, Tensor positions, Tensor slots, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor context_lens, int nq, int nkv, float scale) -> Tensor");
   m.def("decode_linear_add_rmsnorm(Tensor x, Tensor w, Tensor? bias, Tensor residual, Tensor norm_w, float eps) -> (Tensor, Tensor)");
   m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor uniform) -> Tensor");
   // benchmarks / tuning (gemm_bf16.hip, hbm_stream.hip)
@@ -66,6 +67,8 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("car_ipc_close(int ptr) -> ()", &llmctl::car_ipc_close);
   m.def("car_sig_words() -> int", &llmctl::car_sig_words);
   m.def("car_error(int sig_ptr) -> int", &llmctl::car_error);
+  m.def("set_knob(str name, int value) -> ()", &llmctl::set_knob);
+  m.def("clear_knobs() -> ()", &llmctl::clear_knobs);
   m.def("gemm_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int variant=-1) -> ()");
   m.def("hbm_copy(Tensor src, Tensor(a!) dst) -> ()");
   m.def("gemm64_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int config=4) -> ()");

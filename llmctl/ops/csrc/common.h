@@ -29,6 +29,9 @@
 
 namespace llmctl {
 
+// llmctl.config.knobs (knobs.cpp): value pushed from Python, else the default
+int64_t knob(const char* name, int64_t dflt);
+
 using bf16x8 = __attribute__((ext_vector_type(8))) unsigned short;  // 16 B
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 

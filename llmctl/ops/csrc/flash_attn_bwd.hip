@@ -1418,15 +1418,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
   }
 }
 
-// dK/dV kernel (A/B knob LLMCTL_DKV): 0 = unpipelined, 1 = software-pipelined, 2 (default) =
+// dK/dV kernel (A/B knob dkv): 0 = unpipelined, 1 = software-pipelined, 2 (default) =
 // persistent where it applies (causal, head_dim 128, S % 128, no documents), else pipelined.
 // B12 S2048 H32 D128 (tools/attn_ablate.py): 1.24 / 1.12 / 0.98-1.00 ms
 int dkv_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("LLMCTL_DKV");
-    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
-  }();
-  return m;
+  const int64_t m = knob("dkv", 2);
+  return (m >= 0 && m <= 2) ? (int)m : 2;
 }
 
 // the persistent dK/dV kernel's per-XCD item counters: one buffer per (device, stream), zeroed
@@ -1443,7 +1440,7 @@ int* dkv_queue(hipStream_t s) {
   return q;
 }
 
-// dkv_impl: -1 = default (LLMCTL_DKV_PIPE), 0 = unpipelined kernel, 1 = pipelined where built
+// dkv_impl: -1 = default (knob dkv), 0 = unpipelined kernel, 1 = pipelined where built
 template <int HD, bool CAUSAL, bool DOC>
 void launch_bwd(const BwdArgs& a, hipStream_t s, bool do_dq, bool do_dkv, int dkv_impl) {
   if (do_dq) {
@@ -1466,7 +1463,7 @@ void launch_bwd(const BwdArgs& a, hipStream_t s, bool do_dq, bool do_dkv, int dk
           // per-XCD queues (B*Hkv % 8 == 0) are drained by blocks with blockIdx & 7 == queue:
           // fewer than 8 workgroups would leave queues without a consumer
           const int min_wg = ((long)a.B * a.Hkv) % 8 == 0 ? 8 : 1;
-          if (const char* e = std::getenv("LLMCTL_DKV_NWG")) nwg = std::max(min_wg, std::min(nwg, atoi(e)));  // debug
+          if (const int64_t e = knob("dkv_nwg", 0); e > 0) nwg = std::max<int>(min_wg, std::min<int>(nwg, (int)e));  // debug
           nwg = std::max(nwg, min_wg);
           if (a.stamps != nullptr)
             hipLaunchKernelGGL(fa_bwd_dkv_persist_kernel<true>, dim3((unsigned)nwg), dim3(256), 0, s, a, wq);

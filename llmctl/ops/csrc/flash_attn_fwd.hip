@@ -59,7 +59,7 @@ struct FwdArgs {
   const int* doc;    // [B, S] document start per token, or nullptr
   float* o_part;     // SPLIT: [2, B, S, Hq, HD] fp32 normalised partial outputs
   float* lse_part;   // SPLIT: [2, B, Hq, S] natural-log partial LSEs
-  int prio;          // raise the wave priority over its MFMA phases (A/B knob LLMCTL_FA_PRIO)
+  int prio;          // raise the wave priority over its MFMA phases (A/B knob fa_prio)
 };
 
 template <int HD, bool CAUSAL, bool DOC = false, bool SPLIT = false, int NW = 4, int NBUF = 2>
@@ -395,11 +395,9 @@ std::tuple<at::Tensor, at::Tensor> fwd_launch(const at::Tensor& q, at::Tensor& o
   // does: split every block's K/V range over two workgroups
   bool split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 4 &&
                (long)B * Hq * nqb <= (long)WG_PER_CU * num_cus();
-  // LLMCTL_FA_SPLIT=0 / =1 override the heuristic (autotuner knob, llmctl.plugins.autotuning)
-  if (const char* e = std::getenv("LLMCTL_FA_SPLIT")) {
-    if (e[0] == '0') split = false;
-    else if (e[0] == '1') split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 2;
-  }
+  // knob fa_split = 0 / 1 overrides the heuristic (-1: auto; autotuner knob, llmctl.plugins.autotuning)
+  if (const int64_t e = knob("fa_split", -1); e == 0) split = false;
+  else if (e == 1) split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 2;
   if (split) {
     auto o_part = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
     auto lse_part = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));
@@ -468,18 +466,10 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
             (float)(scale * 1.4426950408889634), nullptr, nullptr, nullptr, 0};
-  static const int prio = [] {  // default on: 2-3 % at B12 S2048 (LLMCTL_FA_PRIO=0: off, A/B)
-    const char* e = std::getenv("LLMCTL_FA_PRIO");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  a.prio = prio;
-  // workgroup shape: LLMCTL_FA_NW=8 -> 8 waves (256 rows) with a 3-slot ring, one workgroup per
+  a.prio = knob("fa_prio", 1) != 0 ? 1 : 0;  // default on: 2-3 % at B12 S2048 (0: off, A/B)
+  // workgroup shape: knob fa_nw = 8 -> 8 waves (256 rows) with a 3-slot ring, one workgroup per
   // CU; default 4 waves (128 rows) with a 2-slot ring, two per CU (A/B knob, tools/attn_bench.py)
-  static const int nw = [] {
-    const char* e = std::getenv("LLMCTL_FA_NW");
-    return (e && e[0] == '8') ? 8 : 4;
-  }();
-  if (nw == 8) return fwd_launch<8, 3>(q, o, lse, a, B, S, Hq, D, causal, doc_start);
+  if (knob("fa_nw", 4) == 8) return fwd_launch<8, 3>(q, o, lse, a, B, S, Hq, D, causal, doc_start);
   return fwd_launch<4, 2>(q, o, lse, a, B, S, Hq, D, causal, doc_start);
 }
 

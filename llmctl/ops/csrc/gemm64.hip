@@ -1663,7 +1663,6 @@ at::Tensor gemm64_wgrad_swiglu(const at::Tensor& dy, const at::Tensor& act, at::
   g.s_dgu = reinterpret_cast<unsigned short*>(dgu.data_ptr());
   g.s_E = (unsigned)(T * N);
   g.s_F = (int)N;
-  if (const char* d = std::getenv("LLMCTL_SIDE_DIAG"); d && std::string(d) == "nomem") g.s_E = 0;  // timing only
   plan_split(g, (int)(config / 1000));
   at::Tensor ws;
   if (g.splits > 1) {

@@ -40,62 +40,7 @@ __global__ __launch_bounds__(256) void kv_write_kernel(const unsigned short* __r
   reinterpret_cast<uint4*>(vc)[slot * row8 + c] = reinterpret_cast<const uint4*>(v)[(long)t * row8 + c];
 }
 
-// Fused QKV finalize (round 2): the decode QKV projection leaves fp32 K-chunk partials
-// ws [KS][M][N] (N = (nq + 2 nkv) D, skinny_gemm.hip's decode_linear_partials); the attention
-// kernel sums them itself — q (+ bias, bf16-rounded as the GEMM would store it, RoPE'd and
-// rounded again as rope_fwd_kernel stores it) in the prologue of every workgroup, and the
-// current token's K (RoPE'd) / V rows into the paged cache by the workgroup whose context split
-// holds that token, before its loop reads them back.  No other workgroup reads the current
-// position, so there is no cross-workgroup hand-off; the separate finalize pass is gone.
-struct FusedQKV {
-  const float* ws;
-  const unsigned short* bias;  // [N] or nullptr
-  const float* cosT;
-  const float* sinT;
-  const int* pos;              // [M]
-  const int64_t* slots;        // [M], -1 = no cache write
-  unsigned short* kc;          // writable views of the caches
-  unsigned short* vc;
-  int M, KS, nq, nkv;
-};
-
-// 8 consecutive projection outputs at column n of token row m, as the GEMM stores them (bf16)
-__device__ __forceinline__ void qkv_cols8(const FusedQKV& f, long N, int m, long n, float* o) {
-  const long MN = (long)f.M * N, i = (long)m * N + n;
-  float4 a = *reinterpret_cast<const float4*>(f.ws + i), b = *reinterpret_cast<const float4*>(f.ws + i + 4);
-  for (int s = 1; s < f.KS; ++s) {
-    const float4 x = *reinterpret_cast<const float4*>(f.ws + s * MN + i);
-    const float4 y = *reinterpret_cast<const float4*>(f.ws + s * MN + i + 4);
-    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-    b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
-  }
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(v[j] + (f.bias != nullptr ? bf2f(f.bias[n + j]) : 0.f)));
-}
-
-// RoPE'd 8-column slice [c, c+8) of head h (h < nq + nkv) of token m, rounded to bf16 values
-template <int D>
-__device__ __forceinline__ void rope_slice8(const FusedQKV& f, long N, int m, int h, int c, float* o) {
-  constexpr int half = D / 2;
-  const bool lo = c < half;
-  float a[8], b[8];  // a: this slice, b: its rotation partner
-  qkv_cols8(f, N, m, (long)h * D + c, a);
-  qkv_cols8(f, N, m, (long)h * D + (lo ? c + half : c - half), b);
-  const long p = f.pos[m];
-  const int d = lo ? c : c - half;
-  const float* cp = f.cosT + p * half + d;
-  const float* sp = f.sinT + p * half + d;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    // rope_fwd_kernel: o1 = a cos - b sin (first half), o2 = b cos + a sin (second half), written
-    // in the same operand order so FMA contraction rounds identically (own value first)
-    const float r = lo ? a[j] * cp[j] - b[j] * sp[j] : a[j] * cp[j] + b[j] * sp[j];
-    o[j] = bf2f(f2bf(r));
-  }
-}
-
-template <int D, int G, int U, bool FQ = false>
+template <int D, int G, int U>
 __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short* __restrict__ q,
                                                             const unsigned short* __restrict__ kc,
                                                             const unsigned short* __restrict__ vc,
@@ -104,7 +49,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
                                                             unsigned short* __restrict__ out,
                                                             float* __restrict__ part_o, float* __restrict__ part_ml,
                                                             int Hq, int Hkv, int block_size, int max_blocks,
-                                                            float scale_log2, int nsplit, FusedQKV fq = {}) {
+                                                            float scale_log2, int nsplit) {
   constexpr int LPT = D / 8;          // lanes per token (16 for D=128, 8 for D=64)
   constexpr int TPW = 64 / LPT;       // tokens per wave-instruction
   __shared__ float sm_m[4 * TPW][G], sm_l[4 * TPW][G];
@@ -117,30 +62,8 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
   const int* bt = block_tables + (long)seq * max_blocks;
   // q slices for the group's heads
   float qv[G][8];
-  if constexpr (FQ) {
-    const long N = (long)(fq.nq + 2 * fq.nkv) * D;
 #pragma unroll
-    for (int g = 0; g < G; ++g) rope_slice8<D>(fq, N, seq, hk * G + g, sub * 8, qv[g]);
-    // the current token (position L-1) lives in this workgroup's split: write its K/V rows
-    const int chunk0 = (L + nsplit - 1) / nsplit;
-    const int s0 = min(L, split * chunk0), s1 = min(L, s0 + chunk0);
-    const long sl = fq.slots[seq];
-    if (L - 1 >= s0 && L - 1 < s1 && sl >= 0) {
-      const int t = threadIdx.x;
-      if (t < 2 * (D / 8)) {
-        const bool isk = t < D / 8;
-        const int c = (isk ? t : t - D / 8) * 8;
-        float o[8];
-        if (isk) rope_slice8<D>(fq, N, seq, fq.nq + hk, c, o);
-        else qkv_cols8(fq, N, seq, (long)(fq.nq + fq.nkv + hk) * D + c, o);
-        store8((isk ? fq.kc : fq.vc) + (sl * Hkv + hk) * (long)D + c, o);
-      }
-      __syncthreads();  // (s_waitcnt vmcnt(0) + barrier: the rows are in L2 before the loop reads them)
-    }
-  } else {
-#pragma unroll
-    for (int g = 0; g < G; ++g) load8(q + ((long)seq * Hq + hk * G + g) * D + sub * 8, qv[g]);
-  }
+  for (int g = 0; g < G; ++g) load8(q + ((long)seq * Hq + hk * G + g) * D + sub * 8, qv[g]);
   float m[G], l[G], o[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -257,12 +180,9 @@ __global__ __launch_bounds__(D) void paged_combine_kernel(const float* __restric
 // Context splits per (sequence, kv-head): enough workgroups for ~4-8 per CU, at least 128
 // context slots per split, at most 16.  The batch is rounded up to a power of two, as the
 // serving engine's decode-graph buckets are, so graph replay and eager decode pick the same
-// split.  LLMCTL_DECODE_SPLITS overrides (tests, A/B).
+// split.  Knob decode_splits > 0 overrides (tests, A/B; llmctl.config.knobs).
 int decode_splits(int N, int Hkv, int max_ctx) {
-  if (const char* e = std::getenv("LLMCTL_DECODE_SPLITS")) {
-    const int v = std::atoi(e);
-    if (v > 0) return std::min(v, 64);
-  }
+  if (const int64_t v = knob("decode_splits", 0); v > 0) return (int)std::min<int64_t>(v, 64);
   int np = 1;
   while (np < N) np *= 2;
   const int wgs = std::max(1, np * Hkv);
@@ -294,8 +214,8 @@ void kv_cache_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cach
 }
 
 namespace {
-// launch the decode kernel (+ combine) for N sequences x Hq query heads; q == nullptr: fused QKV
-void launch_paged_decode(const unsigned short* q, const FusedQKV* fq, const at::Tensor& k_cache,
+// launch the decode kernel (+ combine) for N sequences x Hq query heads
+void launch_paged_decode(const unsigned short* q, const at::Tensor& k_cache,
                          const at::Tensor& v_cache, const at::Tensor& block_tables, const at::Tensor& context_lens,
                          at::Tensor& out, int N, int Hq, int D, double scale) {
   const int bs = k_cache.size(1), Hkv = k_cache.size(2);
@@ -313,16 +233,10 @@ void launch_paged_decode(const unsigned short* q, const FusedQKV* fq, const at::
   }
   dim3 grid(N * Hkv, nsplit), block(256);
   auto s = stream();
-  const FusedQKV f = fq != nullptr ? *fq : FusedQKV{};
 #define LAUNCH(DD, GG, UU)                                                                                         \
-  if (fq != nullptr)                                                                                              \
-    hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU, true>), grid, block, 0, s, q, bf_ptr(k_cache),             \
-                       bf_ptr(v_cache), block_tables.data_ptr<int>(), context_lens.data_ptr<int>(), bf_mut(out), po, \
-                       pml, Hq, Hkv, bs, max_blocks, sl2, nsplit, f);                                             \
-  else                                                                                                            \
-    hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU, false>), grid, block, 0, s, q, bf_ptr(k_cache),            \
-                       bf_ptr(v_cache), block_tables.data_ptr<int>(), context_lens.data_ptr<int>(), bf_mut(out), po, \
-                       pml, Hq, Hkv, bs, max_blocks, sl2, nsplit, f)
+  hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU>), grid, block, 0, s, q, bf_ptr(k_cache), bf_ptr(v_cache),   \
+                     block_tables.data_ptr<int>(), context_lens.data_ptr<int>(), bf_mut(out), po, pml, Hq, Hkv, bs,   \
+                     max_blocks, sl2, nsplit)
   if (D == 128) {
     if (G == 1) LAUNCH(128, 1, 4);
     else if (G == 2) LAUNCH(128, 2, 4);
@@ -370,56 +284,13 @@ at::Tensor paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache
   const c10::DeviceGuard g(q.device());
   auto out = at::empty_like(q);
   if (N == 0) return out;
-  launch_paged_decode(bf_ptr(q), nullptr, k_cache, v_cache, block_tables, context_lens, out, N, Hq, D, scale);
-  return out;
-}
-
-// Decode attention straight from the QKV projection's fp32 K-chunk partials qkv_ws [KS, M, N]:
-// q RoPE'd in the prologue, the current token's K/V written into the cache at `slots` by the
-// workgroup that reads that position (see FusedQKV).  Same result as decode_qkv_rope_cache +
-// paged_attention_decode.
-at::Tensor paged_attention_decode_qkv(const at::Tensor& qkv_ws, const c10::optional<at::Tensor>& bias,
-                                      const at::Tensor& cosT, const at::Tensor& sinT, const at::Tensor& positions,
-                                      const at::Tensor& slots, at::Tensor& k_cache, at::Tensor& v_cache,
-                                      const at::Tensor& block_tables, const at::Tensor& context_lens, int64_t nq,
-                                      int64_t nkv, double scale) {
-  LLMCTL_CHECK(qkv_ws.dim() == 3 && qkv_ws.is_contiguous() && qkv_ws.scalar_type() == at::kFloat && qkv_ws.is_cuda(),
-               "qkv_ws: fp32 [KS, M, (nq+2nkv)*D] partials");
-  const int KS = qkv_ws.size(0), N = qkv_ws.size(1);
-  const long W = qkv_ws.size(2);
-  LLMCTL_CHECK(W % (nq + 2 * nkv) == 0, "qkv_ws width not divisible by heads");
-  const int D = W / (nq + 2 * nkv);
-  LLMCTL_CHECK(k_cache.dim() == 4 && k_cache.size(2) == nkv, "k_cache kv heads != nkv");
-  check_paged_inputs(k_cache, v_cache, block_tables, context_lens, N, (int)nq, D);
-  LLMCTL_CHECK(cosT.is_cuda() && sinT.is_cuda() && cosT.scalar_type() == at::kFloat && sinT.scalar_type() == at::kFloat &&
-                   cosT.is_contiguous() && sinT.is_contiguous() && cosT.dim() == 2 && cosT.size(1) == D / 2 &&
-                   cosT.sizes() == sinT.sizes(),
-               "cos/sin must be contiguous fp32 [P, D/2] GPU tables");
-  LLMCTL_CHECK(positions.scalar_type() == at::kInt && positions.is_contiguous() && positions.numel() == N,
-               "positions int32 [M]");
-  LLMCTL_CHECK(slots.scalar_type() == at::kLong && slots.is_contiguous() && slots.numel() == N, "slots int64 [M]");
-  if (bias.has_value() && bias->defined())
-    LLMCTL_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == W, "bias [N] bf16");
-  const c10::DeviceGuard g(qkv_ws.device());
-  auto out = at::empty({N, nq, D}, k_cache.options());
-  if (N == 0) return out;
-  FusedQKV f{qkv_ws.data_ptr<float>(),
-             bias.has_value() && bias->defined() ? bf_ptr(*bias) : nullptr,
-             cosT.data_ptr<float>(),
-             sinT.data_ptr<float>(),
-             positions.data_ptr<int>(),
-             slots.data_ptr<int64_t>(),
-             bf_mut(k_cache),
-             bf_mut(v_cache),
-             N, KS, (int)nq, (int)nkv};
-  launch_paged_decode(nullptr, &f, k_cache, v_cache, block_tables, context_lens, out, N, (int)nq, D, scale);
+  launch_paged_decode(bf_ptr(q), k_cache, v_cache, block_tables, context_lens, out, N, Hq, D, scale);
   return out;
 }
 
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
   m.impl("kv_cache_write", &kv_cache_write);
   m.impl("paged_attention_decode", &paged_attention_decode);
-  m.impl("paged_attention_decode_qkv", &paged_attention_decode_qkv);
 }
 
 }  // namespace llmctl

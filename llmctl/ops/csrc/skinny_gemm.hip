@@ -445,14 +445,8 @@ __global__ __launch_bounds__(1024) void decode_fin_add_rmsnorm_kernel(const floa
 }  // namespace
 
 // v3 (weight loads issued before the x staging) for the fused decode projections and config 25;
-// LLMCTL_DECODE_V3=0 keeps the v2 kernel there (A/B)
-bool decode_v3() {
-  static const bool on = [] {
-    const char* e = std::getenv("LLMCTL_DECODE_V3");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// knob decode_v3 = 0 keeps the v2 kernel there (A/B)
+bool decode_v3() { return knob("decode_v3", 1) != 0; }
 
 // v2 launch: KC = K chunk per workgroup (multiple of 128), GB = K blocks in flight per wave
 template <int GB>

@@ -12,10 +12,11 @@ copies are needed between kernels:
 
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Tuple
 
 import torch
+
+from llmctl.config.knobs import knobs
 
 from . import ref
 from ._lib import native, use_native
@@ -251,9 +252,9 @@ def rope_flash_attention(qkv, cos, sin, nq: int, nkv: int, B: int, S: int, posit
     """Causal attention on the QKV projection output: RoPE(q, k) -> flash attention -> o
     ``[B,S,nq,D]``; the backward returns d(qkv) in one fused pass on the HIP path.  ``inplace``
     (HIP path; the caller's qkv must not be needed afterwards): RoPE rotates qkv's q / k heads in
-    place and attention reads strided views (``LLMCTL_ROPE_INPLACE=0`` disables)."""
+    place and attention reads strided views (knob ``rope_inplace`` off disables)."""
     if use_native(qkv) and qkv.is_contiguous():
-        inplace = inplace and os.environ.get("LLMCTL_ROPE_INPLACE", "1") != "0"
+        inplace = inplace and knobs().rope_inplace
         return _RopeFlashAttn.apply(qkv, cos, sin, nq, nkv, B, S, positions, doc_start, inplace)
     q, k, v = rope_qkv(qkv, cos, sin, nq, nkv, S, positions)
     D = q.shape[-1]
@@ -424,28 +425,21 @@ def decode_linear(x, w, b=None):
     (``profiles/skinny_sweep_r2*.jsonl``): every projection up to 16 tokens (at 16 tokens the
     LDS-staged v2 kernel: QKV 3.78 vs 3.55 TB/s, up 3.89 vs 3.35, down 3.16 vs 2.07) and the
     4096 x 4096 o-projection up to 32; wide projections at 17-32 tokens stay on hipBLASLt.
-    ``LLMCTL_SKINNY_GEMM=0`` / ``=all`` force the library / kernel path, ``=narrow`` the earlier
-    routing (wide projections at 5-16 tokens on hipBLASLt) for A/B."""
+    Knob ``skinny_gemm``: ``off`` / ``all`` force the library / kernel path (A/B)."""
     from llmctl.exec.linear import forward_linear
 
-    mode = os.environ.get("LLMCTL_SKINNY_GEMM", "1")
+    mode = knobs().skinny_gemm
     M = x.shape[0] if x.dim() == 2 else 0
     tuned = SKINNY_CONFIGS.get((M, w.shape[0], w.shape[1])) if SKINNY_CONFIGS and x.dim() == 2 else None
-    if tuned is not None and mode == "1" and use_native(x):
+    if tuned is not None and mode == "auto" and use_native(x):
         if tuned == 0:
             return torch.nn.functional.linear(x, w, b)
         if x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype == torch.bfloat16:
             return native().skinny_linear_cfg(x, w, b, tuned)
-    if (mode != "0" and use_native(x) and x.dim() == 2 and M <= 32 and x.dtype == torch.bfloat16
+    if (mode != "off" and use_native(x) and x.dim() == 2 and M <= 32 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and w.shape[0] % 16 == 0 and x.shape[1] % 128 == 0
             and x.is_contiguous() and w.is_contiguous() and (b is None or b.is_contiguous())
             and (mode == "all" or M <= 16 or (w.shape[0] <= 4096 and x.shape[1] <= 4096))):
-        if mode == "narrow":  # A/B: the previous routing (round-2 r1 kernel only, narrow projections)
-            if M <= 4:
-                return native().skinny_linear_cfg(x, w, b, 3)
-            if w.shape[0] <= 4096:
-                return native().skinny_linear_cfg(x, w, b, 7 if M <= 16 else 3)
-            return forward_linear(x, w, b)
         return native().skinny_linear(x, w, b)
     return forward_linear(x, w, b)
 
@@ -454,8 +448,8 @@ def decode_fused_ok(x, w) -> bool:
     """Can this decode projection run with a fused epilogue (``csrc/skinny_gemm.hip``: the v2
     weight-streaming GEMM's K-chunk partials summed by a finalize pass that also applies RoPE +
     paged-cache write, SwiGLU or residual + RMSNorm)?  <= 16 tokens, bf16, out features a
-    multiple of 64, in features of 128.  ``LLMCTL_DECODE_FUSED=0`` disables (A/B)."""
-    return (os.environ.get("LLMCTL_DECODE_FUSED", "1") != "0" and use_native(x) and x.dim() == 2
+    multiple of 64, in features of 128.  Knob ``decode_fused`` off disables (A/B)."""
+    return (knobs().decode_fused and use_native(x) and x.dim() == 2
             and 1 <= x.shape[0] <= 16 and x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous()
             and w.is_contiguous() and w.shape[0] % 64 == 0 and x.shape[1] % 128 == 0)
 
@@ -471,21 +465,11 @@ def decode_qkv_rope_cache(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cac
 
 def decode_attention_qkv(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cache, v_cache, slots, block_tables,
                          ctx_lens, scale: Optional[float] = None):
-    """Decode QKV projection -> RoPE -> paged-cache write -> paged attention, with the
-    projection's fp32 K-chunk partials summed inside the attention kernel (its prologue ropes q;
-    the workgroup whose context split holds the new token writes that token's K/V rows first):
-    no separate finalize pass.  Same result as ``decode_qkv_rope_cache`` followed by
-    ``paged_attention_decode`` (bit for bit).  Opt-in (``LLMCTL_DECODE_ATTN_QKV=1``): measured
-    0.1-0.2 ms SLOWER per 16 x 2k GPT-7B decode step than the two-step path
-    (``profiles/serve_r2_session6.txt``) — every one of the 2048 attention workgroups re-sums its
-    q head's partials on the critical path of its K/V stream, which costs more than the finalize
-    launch it removes."""
+    """Decode QKV projection -> RoPE -> paged-cache write (one finalize pass) -> paged attention.
+    (Round 2's variant that summed the projection partials inside the attention kernel measured
+    0.1-0.2 ms slower per 16 x 2k GPT-7B step, profiles/serve_r2_session6.txt, and was retired.)"""
     D = w.shape[0] // (nq + 2 * nkv)
     scale = scale if scale is not None else D ** -0.5
-    if decode_fused_ok(x, w) and os.environ.get("LLMCTL_DECODE_ATTN_QKV", "0") == "1":
-        ws = native().decode_linear_partials(x, w)
-        return native().paged_attention_decode_qkv(ws, b, cos, sin, positions.to(torch.int32).contiguous(), slots,
-                                                   k_cache, v_cache, block_tables, ctx_lens, nq, nkv, scale)
     q = decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, positions, k_cache, v_cache, slots)
     return paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
 
@@ -494,11 +478,11 @@ def up_swiglu(x, w, b=None):
     """``silu(gate) * up`` of the gate/up projection ``x @ w^T (+ b)`` (w = [W_gate; W_up]).
     Serving prefill: tokens a multiple of 256 run the gemm64 kernel with the SwiGLU in its
     epilogue (``gemm64_swiglu_fwd``: gate and matching up rows in one output tile, only the
-    [T, F] activation stored — no gu tensor, no SwiGLU pass).  ``LLMCTL_PREFILL_SWIGLU=0``
+    [T, F] activation stored — no gu tensor, no SwiGLU pass).  Knob ``prefill_swiglu`` off
     disables (A/B)."""
     x2 = x.reshape(-1, x.shape[-1])
     T, F = x2.shape[0], w.shape[0] // 2
-    if (b is None and os.environ.get("LLMCTL_PREFILL_SWIGLU", "1") != "0" and use_native(x) and T % 256 == 0
+    if (b is None and knobs().prefill_swiglu and use_native(x) and T % 256 == 0
             and F % 128 == 0 and x2.shape[1] % 128 == 0 and x2.dtype == w.dtype == torch.bfloat16
             and x2.stride(1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and w.is_contiguous()
             and w.data_ptr() % 16 == 0):

@@ -17,22 +17,22 @@ decomposed into ``tp`` ring steps fused with per-chunk GEMMs:
 
 Bytes on the wire are those of the collectives they replace; each ring step's transfer hides
 under a 1/tp-size GEMM.  The reference only modelled this communication (TP term of
-``llmctl/cli/commands/plan.py:110-113``).  ``LLMCTL_ASYNC_TP=0`` restores the plain collectives.
+``llmctl/cli/commands/plan.py:110-113``).  Knob ``async_tp`` off restores the plain collectives.
 """
 
 from __future__ import annotations
 
-import os
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
+from llmctl.config.knobs import knobs
 from llmctl.exec.linear import data_grad, weight_grad
 
 
 def enabled() -> bool:
-    return os.environ.get("LLMCTL_ASYNC_TP", "1") != "0"
+    return knobs().async_tp
 
 
 def _peers(group):
@@ -105,7 +105,7 @@ def _matmul_rs(x_full: torch.Tensor, group, mm) -> torch.Tensor:
 def _save_full() -> bool:
     """Keep the gathered input of a column-parallel SP linear for its weight gradient (tp x the
     shard's activation memory per QKV / up projection) instead of re-gathering it in backward."""
-    return os.environ.get("LLMCTL_ASYNC_TP_SAVE_FULL", "0") == "1"
+    return knobs().async_tp_save_full
 
 
 def _fwd_into(w, b):

@@ -15,7 +15,7 @@ issued before this step's kernels; each rank's bf16 dK/dV contribution to a remo
 straight back to the chunk's owner (one point-to-point hop, posted asynchronously and waited
 for only at the end) and is accumulated there in fp32 — no fp32 dK/dV travelling the ring.
 The per-piece backward uses the *global* output and LSE, so every partial gradient is exact.
-No head-count constraint; per-rank attention memory is O(S/cp).  ``LLMCTL_CP_ZIGZAG=0``
+No head-count constraint; per-rank attention memory is O(S/cp).  Knob ``cp_zigzag`` off
 restores contiguous chunks (A/B).
 
 **ulysses** (``seq_to_head`` / ``head_to_seq``): around attention two all-to-alls
@@ -80,7 +80,9 @@ def head_to_seq(x: torch.Tensor, group) -> torch.Tensor:
 def zigzag_enabled() -> bool:
     import os
 
-    return os.environ.get("LLMCTL_CP_ZIGZAG", "1") != "0"
+    from llmctl.config.knobs import knobs
+
+    return knobs().cp_zigzag
 
 
 def local_positions(B: int, S_local: int, cp_rank: int, device, cp: int = 1, zigzag: bool = False) -> torch.Tensor:

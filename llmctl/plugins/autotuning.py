@@ -225,28 +225,12 @@ class CommunicationTuner(Tunable):
         return _time(fn, self.dev, max(1, config.warmup_iterations // 2), config.measurement_iterations)
 
 
-class _EnvKnob:
-    """Set an environment knob for the duration of one measurement."""
+def _knob(name: str, value: int):
+    """A performance knob (llmctl.config.knobs; native ones reach the HIP launchers' table) set
+    for the duration of one measurement."""
+    from llmctl.config.knobs import override
 
-    def __init__(self, name: str, value: Optional[str]):
-        self.name, self.value = name, value
-
-    def __enter__(self):
-        import os
-
-        self.prev = os.environ.get(self.name)
-        if self.value is None:
-            os.environ.pop(self.name, None)
-        else:
-            os.environ[self.name] = self.value
-
-    def __exit__(self, *a):
-        import os
-
-        if self.prev is None:
-            os.environ.pop(self.name, None)
-        else:
-            os.environ[self.name] = self.prev
+    return override(**{name: value})
 
 
 class Gemm64Tuner(Tunable):
@@ -286,7 +270,7 @@ class Gemm64Tuner(Tunable):
 
 
 class DecodeSplitTuner(Tunable):
-    """Paged-attention decode: context splits per (sequence, kv-head) (``LLMCTL_DECODE_SPLITS``)."""
+    """Paged-attention decode: context splits per (sequence, kv-head) (knob ``decode_splits``)."""
 
     def __init__(self, batch: int, ctx: int, heads: int = 32, kv_heads: int = 32, head_dim: int = 128,
                  block_size: int = 16, device: str = "auto"):
@@ -313,14 +297,14 @@ class DecodeSplitTuner(Tunable):
         from llmctl.ops import _lib
 
         ops = _lib.native()
-        with _EnvKnob("LLMCTL_DECODE_SPLITS", str(self.params["splits"])):
+        with _knob("decode_splits", int(self.params["splits"])):
             fn = lambda: ops.paged_attention_decode(self.q, self.kc, self.vc, self.bt, self.lens, self.D ** -0.5)  # noqa
             return _time(fn, self.dev, config.warmup_iterations, config.measurement_iterations)
 
 
 class FlashSplitTuner(Tunable):
     """Flash-attention forward: split every causal q-block's K/V range over two workgroups
-    (+ combine) or not (``LLMCTL_FA_SPLIT``); pays off on small grids (short prefills)."""
+    (+ combine) or not (knob ``fa_split``); pays off on small grids (short prefills)."""
 
     def __init__(self, batch: int, seq_len: int, heads: int = 32, head_dim: int = 128, device: str = "auto"):
         self.B, self.S, self.H, self.D = batch, seq_len, heads, head_dim
@@ -342,7 +326,7 @@ class FlashSplitTuner(Tunable):
         from llmctl.ops import _lib
 
         ops = _lib.native()
-        with _EnvKnob("LLMCTL_FA_SPLIT", str(self.params["split"])):
+        with _knob("fa_split", int(self.params["split"])):
             fn = lambda: ops.flash_attn_fwd(self.q, self.k, self.v, self.D ** -0.5, True, None)  # noqa: E731
             return _time(fn, self.dev, config.warmup_iterations, config.measurement_iterations)
 

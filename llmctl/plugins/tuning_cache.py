@@ -98,9 +98,19 @@ def apply_training(path, config) -> Dict[str, Any]:
         config.bucket_mb = k["bucket_mb"]
         applied["bucket_mb"] = k["bucket_mb"]
     if k["fa_split"] is not None:
-        os.environ["LLMCTL_FA_SPLIT"] = str(k["fa_split"])
+        _set_knobs(fa_split=k["fa_split"])
         applied["fa_split"] = k["fa_split"]
     return applied
+
+
+def _set_knobs(**kw) -> None:
+    """Tuned values become the active performance knobs (llmctl.config.knobs; recorded in the
+    run manifest like every other knob)."""
+    import dataclasses
+
+    from llmctl.config import knobs as K
+
+    K.apply(dataclasses.replace(K.knobs(), **kw))
 
 
 def apply_serving(path) -> Dict[str, Any]:
@@ -112,9 +122,9 @@ def apply_serving(path) -> Dict[str, Any]:
     if k["skinny"]:
         applied["skinny_shapes"] = len(k["skinny"])
     if k["decode_splits"] is not None:
-        os.environ["LLMCTL_DECODE_SPLITS"] = str(k["decode_splits"])
+        _set_knobs(decode_splits=k["decode_splits"])
         applied["decode_splits"] = k["decode_splits"]
     if k["fa_split"] is not None:
-        os.environ["LLMCTL_FA_SPLIT"] = str(k["fa_split"])
+        _set_knobs(fa_split=k["fa_split"])
         applied["fa_split"] = k["fa_split"]
     return applied

@@ -95,6 +95,9 @@ class TrainingConfig:
     profile_schedule: str = "wait=1,warmup=1,active=2"  # or "step(N)" (telemetry.profiling.schedule)
     collective_timeout_s: float = 1800.0  # RCCL/gloo watchdog: a dead peer fails the job instead of hanging it
     plan_file: Optional[str] = None
+    # performance knobs (llmctl.config.knobs.PerfKnobs field -> value): kernel / schedule choices,
+    # resolved at engine init (+ LLMCTL_KNOBS overrides) and recorded in the run manifest
+    perf_knobs: Dict[str, Any] = field(default_factory=dict)
     extra: Dict[str, Any] = field(default_factory=dict)
 
     @property
@@ -116,6 +119,9 @@ class TrainingEngine:
         self.config = c = config
         logging.basicConfig(level=getattr(logging, c.log_level.upper(), logging.INFO),
                             format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+        from llmctl.config import knobs as perf
+
+        self.knobs = perf.configure(c.perf_knobs)  # tuning-cache values below may refine it
         self.env = dist_env()
         self._setup_distributed()
         set_seed(c.seed, c.deterministic)
@@ -281,7 +287,7 @@ class TrainingEngine:
         if self.zero3 is None and self.optimizer.zero_stage >= 1 and dp > 1:
             self._install_param_gather_hooks()
         elif (self.zero3 is None and self.optimizer.zero_stage == 0 and self.device.type == "cuda" and pp == 1
-              and os.environ.get("LLMCTL_OVERLAP_OPTIMIZER", "0") == "1"):
+              and knobs().overlap_optimizer):
             # opt-in: measured neutral on GPT-7B mb 12 (27.7k vs 27.9k tok/s in one A/B,
             # profiles/bench_r1_overlap_opt_ab.jsonl) — the concurrent AdamW slows the GEMMs
             # about as much as it hides

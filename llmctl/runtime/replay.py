@@ -51,6 +51,8 @@ def write_manifest(engine, history: List[Dict[str, Any]], status: str = "running
         "world": {"world_size": lay.world_size, "tp": lay.tp, "pp": lay.pp, "dp": lay.dp},
         "training_config": {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(c).items()},
         "model_config": engine.model_config.to_dict(),
+        # the resolved performance knobs (config + tuning cache + LLMCTL_KNOBS): replay runs with these
+        "perf_knobs": _active_knobs(),
         "global_step": engine.global_step,
         "history": [{k: float(v) if isinstance(v, (int, float)) else v for k, v in r.items()} for r in history],
     }
@@ -59,6 +61,12 @@ def write_manifest(engine, history: List[Dict[str, Any]], status: str = "running
     tmp.write_text(json.dumps(man, indent=1))
     os.replace(tmp, p)
     return p
+
+
+def _active_knobs() -> Dict[str, Any]:
+    from llmctl.config.knobs import knobs
+
+    return knobs().as_dict()
 
 
 def load_manifest(path: str) -> Dict[str, Any]:
@@ -109,6 +117,8 @@ def replay_run(run: str, steps: int = 0, tolerance: float = 1e-3) -> Dict[str, A
     man = load_manifest(run)
     rec = man.get("history", [])
     tc = dict(man["training_config"])
+    if man.get("perf_knobs"):
+        tc["perf_knobs"] = dict(man["perf_knobs"])  # the knobs the recorded run resolved to
     if steps > 0:
         tc["max_steps"] = steps
     elif man.get("global_step"):

@@ -25,7 +25,6 @@ from __future__ import annotations
 
 import logging
 import math
-import os
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -34,6 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from llmctl import ops
+from llmctl.config.knobs import knobs
 from llmctl.io.artifact import load_model
 from llmctl.models import DecoderLM
 
@@ -50,7 +50,10 @@ class InferenceEngine:
                  max_batch_tokens: int = 8192, max_model_len: Optional[int] = None, kv_cache_fraction: float = 0.85,
                  block_size: int = 16, num_kv_blocks: Optional[int] = None, scheduler: str = "dynamic",
                  use_graphs: bool = True, seed: int = 0, pc=None, prefix_caching: bool = True,
-                 tuning_cache: Optional[str] = None):
+                 tuning_cache: Optional[str] = None, perf_knobs: Optional[Dict] = None):
+        from llmctl.config import knobs as perf
+
+        self.knobs = perf.configure(perf_knobs)  # defaults + perf_knobs + LLMCTL_KNOBS
         if device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -232,9 +235,9 @@ class InferenceEngine:
         work = torch.tensor(plan["work"], dtype=torch.int32).to(d, non_blocking=True)
         # fresh prompts: the training flash-attention kernel over packed documents, K/V straight
         # from the RoPE pass (16 x 2k burst TTFT p50 224.6 -> 218.6 ms, single 2k prompt 27.5 ->
-        # 26.2 ms, profiles/serve_r2_session6.txt); LLMCTL_PREFILL_FA=0 keeps the paged kernel
+        # 26.2 ms, profiles/serve_r2_session6.txt); knob prefill_fa off keeps the paged kernel
         doc = None
-        fa = plan.get("doc") is not None and d.type == "cuda" and os.environ.get("LLMCTL_PREFILL_FA", "1") != "0"
+        fa = plan.get("doc") is not None and d.type == "cuda" and knobs().prefill_fa
         if fa and len(plan["cu"]) > 2:  # several prompts packed: document boundaries
             doc = torch.from_numpy(plan["doc"]).to(d, non_blocking=True).view(1, T)
         # (one prompt: plain causal attention, which also lets the kernel split the K/V range of
@@ -293,7 +296,7 @@ class InferenceEngine:
         work = torch.tensor(pp["work"], dtype=torch.int32).to(d, non_blocking=True)
         bt_d = torch.from_numpy(dp["bt"]).to(d, non_blocking=True)
         ctx_d = torch.tensor(dp["ctx"], dtype=torch.int32).to(d, non_blocking=True)
-        fa = pp.get("doc") is not None and d.type == "cuda" and os.environ.get("LLMCTL_PREFILL_FA", "1") != "0"
+        fa = pp.get("doc") is not None and d.type == "cuda" and knobs().prefill_fa
         doc = torch.from_numpy(pp["doc"]).to(d, non_blocking=True).view(1, Tp) if fa and len(pp["cu"]) > 2 else None
         x = self._embed(ids, pos.long())
         res = None
@@ -323,8 +326,8 @@ class InferenceEngine:
         return self._final(x.index_select(0, rows), res.index_select(0, rows))
 
     def _mixed_ok(self) -> bool:
-        """``LLMCTL_MIXED_STEPS=0`` runs a step's decode and prefill as two forwards (A/B)."""
-        return os.environ.get("LLMCTL_MIXED_STEPS", "1") != "0"
+        """Knob ``mixed_steps`` off runs a step's decode and prefill as two forwards (A/B)."""
+        return knobs().mixed_steps
 
     # ------------------------------------------------------------------ decode
     def _fused_decode(self) -> bool:
@@ -333,13 +336,13 @@ class InferenceEngine:
         (the RoPE/cache-write, SwiGLU and add+RMSNorm passes ride on the projections' finalize).  Needs the GPU path,
         RMSNorm, RoPE and a gated MLP; at TP > 1 the row-parallel projections' all-reduce, bias,
         residual add and next RMSNorm are one custom-all-reduce kernel
-        (``_reduce_add_rmsnorm``); ``LLMCTL_DECODE_FUSED=0`` keeps the unfused layer (A/B)."""
+        (``_reduce_add_rmsnorm``); knob ``decode_fused`` off keeps the unfused layer (A/B)."""
         cfg, m = self.cfg, self.model
         return (self.device.type == "cuda" and (self.tp == 1 or self._fused_reduce_ok()) and self.rope is not None
                 and cfg.gated_mlp
                 and not cfg.is_moe and m.final_norm_b is None
                 and all(l.attn_norm_b is None and l.mlp_norm_b is None for l in m.layers)
-                and os.environ.get("LLMCTL_DECODE_FUSED", "1") != "0")
+                and knobs().decode_fused)
 
     def _decode_body(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
         if self._fused_decode():

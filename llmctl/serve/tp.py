@@ -14,19 +14,19 @@ same step, so every rank posts the identical RCCL sequence.  Ranks != 0 run
 :meth:`TPInferenceEngine.worker_loop` until rank 0 broadcasts ``stop``.
 
 Decode-step hipGraph capture stays on for TP (the collectives are captured with the
-rest) unless ``LLMCTL_TP_GRAPHS=0``.  Decode-sized all-reduces (<= 4 MB) use the one-shot
-xGMI peer-memory kernel (:mod:`llmctl.comms.custom_ar`) unless ``LLMCTL_CUSTOM_AR=0``.
+rest) unless knob ``tp_graphs`` is off.  Decode-sized all-reduces (<= 4 MB) use the one-shot
+xGMI peer-memory kernel (:mod:`llmctl.comms.custom_ar`) unless knob ``custom_ar`` is off.
 """
 
 from __future__ import annotations
 
 import logging
-import os
 from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
+from llmctl.config.knobs import knobs
 from llmctl.models import ParallelContext
 from llmctl.utils.env import dist_env
 
@@ -48,14 +48,14 @@ class TPInferenceEngine(InferenceEngine):
         self._closed = False
         self._car_checks = 0
         pc = ParallelContext(tp_group=tp_group, tp_size=self.tp_size, tp_rank=self.tp_rank)
-        if kw.get("use_graphs", True) and os.environ.get("LLMCTL_TP_GRAPHS", "1") == "0":
+        if kw.get("use_graphs", True) and not knobs().tp_graphs:
             kw["use_graphs"] = False
         self.car = None
         super().__init__(model_path, pc=pc, **kw)
         # decode-sized all-reduces go through the one-shot xGMI kernel (llmctl.comms.custom_ar);
         # prefill-sized ones and CPU runs stay on RCCL / gloo
         if (self.device.type == "cuda" and self.tp_size > 1
-                and os.environ.get("LLMCTL_CUSTOM_AR", "1") != "0"):
+                and knobs().custom_ar):
             from llmctl.comms.custom_ar import CustomAllReduce
 
             # one-shot up to 4 MB (decode), two-shot up to 32 MB (2k-token prefill chunks at d = 8192)
@@ -96,7 +96,7 @@ class TPInferenceEngine(InferenceEngine):
         return x
 
     def _fused_reduce_ok(self) -> bool:
-        return self.car is not None and os.environ.get("LLMCTL_TP_FUSED_DECODE", "1") != "0"
+        return self.car is not None and knobs().tp_fused_decode
 
     def _reduce_add_rmsnorm(self, part, bias, res, norm_w, eps):
         """One kernel (``car_allreduce_add_rmsnorm``): the row-parallel partials' all-reduce, the

@@ -462,15 +462,29 @@ def serve_forced_gpu(rank: int, world: int, max_tokens: int = 8, model: str = "t
     """GPU serving (TP = world ranks sharing cuda:0 over gloo + the custom IPC all-reduce, decode
     steps in hipGraphs) with every sampled token replaced by ``forced[seq][step]`` (teacher
     forcing; None: greedy) and the full-vocabulary logits of every step recorded on rank 0 — so
-    two configurations can be compared row by row over the same token stream."""
+    two configurations can be compared row by row over the same token stream.  ``env`` (e.g.
+    ``{"LLMCTL_KNOBS": "decode_fused=0"}``) is set for the call and restored afterwards."""
+    import os
+
+    saved = {k: os.environ.get(k) for k in (env or {})}  # world 1 runs in the caller's process
+    os.environ.update(env or {})
+    try:
+        return _serve_forced_gpu(rank, world, max_tokens, model, forced, engine_kw)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _serve_forced_gpu(rank, world, max_tokens, model, forced, engine_kw) -> dict:
     import os
 
     import torch.distributed as dist
 
     from llmctl.serve.scheduler import SamplingParams
 
-    for k, v in (env or {}).items():
-        os.environ[k] = v
     torch.cuda.set_device(0)
     kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=64, block_size=16, max_model_len=256,
               max_batch_tokens=512, seed=0, use_graphs=True)

@@ -39,3 +39,14 @@ def native_lib():
     assert _lib.load(), f"HIP library failed to load: {_lib._error}"
     import torch
     return torch.ops.llmctl
+
+
+@pytest.fixture(autouse=True)
+def _reset_perf_knobs():
+    """Engines configure the process-wide performance knobs (llmctl.config.knobs); every test
+    starts and ends with the defaults (+ LLMCTL_KNOBS of the environment, if any)."""
+    from llmctl.config import knobs
+
+    knobs.configure()
+    yield
+    knobs.configure()

@@ -53,7 +53,7 @@ def test_two_rank_dp_side_job_swiglu_backward(tmp_path, monkeypatch):
     path.write_text(json.dumps(cfg))
     out = {}
     for mode in ("side", "epilogue"):
-        monkeypatch.setenv("LLMCTL_SWIGLU_BWD", mode)
+        monkeypatch.setenv("LLMCTL_KNOBS", f"swiglu_bwd={mode}")
         out[mode] = _bench("--zero", "1", "--model", str(path))
     assert out["side"]["config"]["parallelism"] == "dp2-zero1"
     assert abs(out["side"]["final_loss"] - out["epilogue"]["final_loss"]) < 2e-2, out
@@ -71,7 +71,7 @@ def test_tp2_pp2_sp2_four_ranks_one_gpu(monkeypatch, async_tp):
     """Config #3 of the planner (TP2 x PP2, sequence parallel) as 4 ranks on cuda:0: bf16 HIP
     kernels, the 1F1B schedule's device-tensor p2p and the async-TP ring steps (or the plain
     SP collectives) over host-staged gloo; the losses follow the single-process GPU run."""
-    monkeypatch.setenv("LLMCTL_ASYNC_TP", async_tp)
+    monkeypatch.setenv("LLMCTL_KNOBS", f"async_tp={async_tp}")
     ref = _layout_losses(1, {})[0]
     out = _layout_losses(4, {"tp": 2, "pp": 2, "sp": True, "microbatches": 4})
     assert all(o["native"] for o in out) and out[0]["backend"] == "gloo"

@@ -62,8 +62,8 @@ def test_async_tp_linears_match_unsharded(world):
 
 
 def test_tp2_sp_plain_collectives_match_single(ref_dp1, monkeypatch):
-    """LLMCTL_ASYNC_TP=0: Megatron-SP with the synchronous all-gather / reduce-scatter."""
-    monkeypatch.setenv("LLMCTL_ASYNC_TP", "0")
+    """Knob async_tp off: Megatron-SP with the synchronous all-gather / reduce-scatter."""
+    monkeypatch.setenv("LLMCTL_KNOBS", "async_tp=0")
     out = run_ranks(train_layout, 2, STEPS, {"tp": 2, "sp": True})
     _losses_close(out[0]["losses"], ref_dp1["losses"])
     _close(out[0]["state"], ref_dp1["state"])
@@ -213,7 +213,7 @@ def test_cp2_ring_matches_single(ref_dp1):
 
 
 def test_cp2_ring_contiguous_matches_single(ref_dp1, monkeypatch):
-    monkeypatch.setenv("LLMCTL_CP_ZIGZAG", "0")
+    monkeypatch.setenv("LLMCTL_KNOBS", "cp_zigzag=0")
     out = run_ranks(train_layout, 2, STEPS, {"cp": 2, "cp_mode": "ring"})
     _losses_close(out[0]["losses"], ref_dp1["losses"])
     _close(out[0]["state"], ref_dp1["state"])

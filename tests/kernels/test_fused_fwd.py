@@ -1,6 +1,6 @@
 """Fused training-forward GEMM epilogues (llmctl/ops/csrc/gemm64.hip EPI_ROPE_QKV / EPI_UP_SWIGLU)
 against fp32 references of the unfused ops (F.linear + RoPE / SwiGLU), checked per row, plus
-the decoder layer's fused path against the unfused path (LLMCTL_FUSED_FWD=0) forward and
+the decoder layer's fused path against the unfused path (knob fused_fwd off) forward and
 backward — including the gradients the grad sink writes."""
 
 import pytest
@@ -58,7 +58,9 @@ def test_gemm64_up_swiglu_matches_fp32(native_lib, T, K, F):
 
 
 def _layer_grads(fused: bool, monkeypatch, sink: bool):
-    monkeypatch.setenv("LLMCTL_FUSED_FWD", "1" if fused else "0")  # default off: A/B both
+    from llmctl.config.knobs import configure
+
+    configure({"fused_fwd": fused})  # A/B both
     from llmctl.exec.linear import GradSink
     from llmctl.models import ParallelContext, get_model_config
     from llmctl.models.transformer import DecoderLayer

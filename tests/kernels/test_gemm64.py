@@ -111,14 +111,15 @@ def test_gemm64_rejects_bad_shapes(native_lib):
         native_lib.gemm64_ex(a, b, out, False, False, False, 104)
 
 
-@pytest.mark.parametrize("mode", ["1", "fused"])
-def test_linear_backward_on_gemm64(native_lib, monkeypatch, mode):
+@pytest.mark.parametrize("mode", ["all", "fused"])
+def test_linear_backward_on_gemm64(native_lib, mode):
     """exec.linear routes wgrad (into the sink's flat view) through gemm64 at eligible shapes and
-    dgrad through gemm64 (LLMCTL_DGRAD64=1: no W^T copy) or, by default (=fused: only the
-    SwiGLU-fused down projection stays on gemm64), hipBLASLt through the W^T copy; all match fp32."""
+    dgrad through gemm64 (knob dgrad64=all: no W^T copy) or, with dgrad64=fused (only the
+    SwiGLU-fused down projection on gemm64), hipBLASLt through the W^T copy; all match fp32."""
+    from llmctl.config.knobs import configure
     from llmctl.exec.linear import GradSink, dgrad64_ok, linear
 
-    monkeypatch.setenv("LLMCTL_DGRAD64", mode)
+    configure({"dgrad64": mode})
 
     T, inn, out = 512, 768, 1024
     x = _bf(T, inn, seed=5).requires_grad_(True)
@@ -128,7 +129,7 @@ def test_linear_backward_on_gemm64(native_lib, monkeypatch, mode):
     sink.attach(w)
     y = linear(x, w)
     dy = _bf(T, out, seed=7)
-    if mode == "1":
+    if mode == "all":
         assert getattr(w, "_llmctl_wt", None) is None  # gemm64 dgrad: no transposed copy kept
         assert dgrad64_ok(dy, w)
     else:
@@ -225,15 +226,17 @@ def test_gemm64_wgrad_swiglu(native_lib, T, H, F, cfg, gdt, acc):
 
 
 @pytest.mark.parametrize("main_grad", [False, True])
-@pytest.mark.parametrize("side_dgrad", ["blas", "g64"])
-def test_swiglu_down_side_job_autograd(native_lib, monkeypatch, main_grad, side_dgrad):
-    """_SwiGLUDown with a grad-sink weight: plain data gradient + weight gradient carrying the
-    SwiGLU backward (LLMCTL_SWIGLU_BWD=side); two backward passes accumulate into the sink's
-    view (bf16 .grad or fp32 main_grad); matches fp32 autograd and the epilogue-fused path."""
+@pytest.mark.parametrize("dgrad64", ["fused", "all"])
+def test_swiglu_down_side_job_autograd(native_lib, main_grad, dgrad64):
+    """_SwiGLUDown with a grad-sink weight: plain data gradient (hipBLASLt through W^T, or gemm64
+    with dgrad64=all) + weight gradient carrying the SwiGLU backward (swiglu_bwd=side); two
+    backward passes accumulate into the sink's view (bf16 .grad or fp32 main_grad); matches fp32
+    autograd and the epilogue-fused path."""
+    from llmctl.config.knobs import configure
     from llmctl.exec.linear import GradSink, wgrad_swiglu_ok
     from llmctl.models.transformer import _SwiGLUDown
 
-    monkeypatch.setenv("LLMCTL_SIDE_DGRAD", side_dgrad)
+    configure({"dgrad64": dgrad64})
     T, H, F = 512, 4096, 1024
     gu0 = _bf(T, 2 * F, seed=21)
     w = torch.nn.Parameter(_bf(H, F, seed=22) * 0.02)
@@ -255,7 +258,7 @@ def test_swiglu_down_side_job_autograd(native_lib, monkeypatch, main_grad, side_
         gw = w.main_grad if main_grad else w.grad
         assert row_err(gu.grad, g32.grad) < 2e-2
         assert row_err(gw, step * w32.grad) < 2e-2
-    monkeypatch.setenv("LLMCTL_SWIGLU_BWD", "epilogue")
+    configure({"dgrad64": dgrad64, "swiglu_bwd": "epilogue"})
     gu = gu0.clone().requires_grad_(True)
     _SwiGLUDown.apply(gu, w, False).backward(dy)
     assert row_err(gu.grad, g32.grad) < 2e-2

@@ -300,10 +300,9 @@ def test_paged_attention_decode(native_lib, Hq, Hkv, D):
 def test_paged_attention_decode_context_splits(native_lib, monkeypatch, Hq, Hkv, D, splits):
     """Split-context (flash-decoding) path: partials + combine, including splits that are
     empty for short sequences, and the automatic choice."""
-    if splits == "auto":
-        monkeypatch.delenv("LLMCTL_DECODE_SPLITS", raising=False)
-    else:
-        monkeypatch.setenv("LLMCTL_DECODE_SPLITS", splits)
+    from llmctl.config.knobs import configure
+
+    configure({"decode_splits": 0 if splits == "auto" else int(splits)})
     nb, bs, N, maxb = 400, 16, 3, 128
     kc = _bf(nb, bs, Hkv, D, seed=61)
     vc = _bf(nb, bs, Hkv, D, seed=62)
@@ -446,10 +445,10 @@ def test_side_stream_optimizer_matches_inline(native_lib, monkeypatch):
     from llmctl.runtime.engine import TrainingConfig, TrainingEngine
 
     def run(flag):
-        monkeypatch.setenv("LLMCTL_OVERLAP_OPTIMIZER", flag)
         torch.manual_seed(0)
         cfg = TrainingConfig(model_name_or_path="tiny", batch_size=2, seq_len=128, device="cuda", log_level="warning",
-                             learning_rate=1e-3, max_steps=4, bucket_mb=0.25, seed=3)
+                             learning_rate=1e-3, max_steps=4, bucket_mb=0.25, seed=3,
+                             perf_knobs={"overlap_optimizer": flag == "1"})
         eng = TrainingEngine(cfg, get_model_config("tiny"))
         assert eng.optimizer.overlap_update == (flag == "1")
         g = torch.Generator().manual_seed(11)

@@ -185,11 +185,11 @@ def test_mixed_prefill_decode_steps_match_separate(native_lib):
     from llmctl.testing.workers import serve_forced_gpu
 
     kw = {"max_batch_tokens": 24, "max_batch_size": 5}
-    ref = serve_forced_gpu(0, 1, 8, "tiny", None, {"LLMCTL_MIXED_STEPS": "0"}, kw)
-    mix = serve_forced_gpu(0, 1, 8, "tiny", ref["tokens"], {"LLMCTL_MIXED_STEPS": "1"}, kw)
+    ref = serve_forced_gpu(0, 1, 8, "tiny", None, {"LLMCTL_KNOBS": "mixed_steps=0"}, kw)
+    mix = serve_forced_gpu(0, 1, 8, "tiny", ref["tokens"], {"LLMCTL_KNOBS": "mixed_steps=1"}, kw)
     import os
 
-    os.environ.pop("LLMCTL_MIXED_STEPS", None)
+    os.environ.pop("LLMCTL_KNOBS", None)
     assert mix["mixed_steps"] > 0 and ref["mixed_steps"] == 0
     err = row_err(_logit_rows(mix), _logit_rows(ref))
     assert err < 2e-2, err
@@ -204,13 +204,10 @@ def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
     prompts = [[1, 2, 3, 4, 5], [9] * 37, [7, 7], [3] * 70]
     p = SamplingParams(max_tokens=12, temperature=0.0)
     kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=128, block_size=16, max_model_len=512, use_graphs=True)
-    monkeypatch.setenv("LLMCTL_DECODE_FUSED", "1")
-    monkeypatch.setenv("LLMCTL_DECODE_ATTN_QKV", "1")  # also the opt-in attention-side QKV finalize
-    ef = InferenceEngine("tiny", **kw)
+    ef = InferenceEngine("tiny", perf_knobs={"decode_fused": True}, **kw)
     assert ef._fused_decode()
     a = ef.generate(prompts, p)
-    monkeypatch.setenv("LLMCTL_DECODE_FUSED", "0")
-    eu = InferenceEngine("tiny", **kw)
+    eu = InferenceEngine("tiny", perf_knobs={"decode_fused": False}, **kw)
     assert not eu._fused_decode()
     b = eu.generate(prompts, p)
     assert [s.output_ids[0] for s in a] == [s.output_ids[0] for s in b]  # prefill path is shared
@@ -218,13 +215,12 @@ def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
     from llmctl.testing.numerics import row_err
     from llmctl.testing.workers import serve_forced_gpu
 
-    ref = serve_forced_gpu(0, 1, 8, "tiny", None, {"LLMCTL_DECODE_FUSED": "0"})
-    fus = serve_forced_gpu(0, 1, 8, "tiny", ref["tokens"], {"LLMCTL_DECODE_FUSED": "1"})
+    ref = serve_forced_gpu(0, 1, 8, "tiny", None, {"LLMCTL_KNOBS": "decode_fused=0"})
+    fus = serve_forced_gpu(0, 1, 8, "tiny", ref["tokens"], {"LLMCTL_KNOBS": "decode_fused=1"})
     assert fus["fused_decode"] and not ref["fused_decode"]
     err = row_err(_logit_rows(fus), _logit_rows(ref))
     assert err < 2e-2, err
-    monkeypatch.setenv("LLMCTL_DECODE_FUSED", "0")
-    # one decode step from identical cache state: fused vs unfused logits
+    # one decode step from identical cache state: fused vs unfused logits (eu left the knob off)
     for pr in prompts:
         ef.add_request(pr, SamplingParams(max_tokens=4, temperature=0.0))
     while ef.scheduler.waiting or any(s.first_token_time is None for s in ef.scheduler.running):
@@ -237,7 +233,7 @@ def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
         args = (torch.tensor(plan["ids"], device=d), torch.tensor(plan["positions"], dtype=torch.int32, device=d),
                 torch.tensor(plan["slots"], device=d), torch.from_numpy(plan["bt"]).to(d),
                 torch.tensor(plan["ctx"], dtype=torch.int32, device=d))
-        lu = ef._decode_body(*args).float()  # (LLMCTL_DECODE_FUSED=0 here)
+        lu = ef._decode_body(*args).float()  # (knob decode_fused off here)
         lf = ef._decode_body_fused(*args).float()
     assert torch.isfinite(lf).all() and (lf - lu).norm() / lu.norm() < 2e-2
 
@@ -257,10 +253,12 @@ def test_fresh_prefill_flash_attention_matches_paged(native_lib, monkeypatch):
         assert e.kv.add_sequence_shared(s.seq_id, s.num_tokens, [])
     plan = e.prefill_plan([PrefillChunk(s, 0, s.num_tokens) for s in seqs])
     assert plan["doc"] is not None
-    monkeypatch.setenv("LLMCTL_PREFILL_FA", "1")
+    from llmctl.config.knobs import configure
+
+    configure({"prefill_fa": True})
     la = e.prefill_exec(plan).float()
     kc_a = [t.clone() for t in e.kv_cache.k]
-    monkeypatch.setenv("LLMCTL_PREFILL_FA", "0")
+    configure({"prefill_fa": False})
     lb = e.prefill_exec(plan).float()
     assert la.shape == lb.shape == (4, e.cfg.vocab_size)
     assert (la - lb).norm() / lb.norm() < 1e-2

@@ -364,12 +364,10 @@ def test_mixed_prefill_decode_steps_match_separate(monkeypatch, prefix):
     kw = dict(device="cpu", max_batch_size=4, num_kv_blocks=64, block_size=8, max_model_len=256,
               max_batch_tokens=48, prefix_caching=prefix)
     p = SamplingParams(max_tokens=9, temperature=0.0)
-    monkeypatch.setenv("LLMCTL_MIXED_STEPS", "1")
-    e = InferenceEngine("tiny", **kw)
+    e = InferenceEngine("tiny", perf_knobs={"mixed_steps": True}, **kw)
     a = [s.output_ids for s in e.generate(prompts, p)]
     assert e.stats.get("mixed_steps", 0) > 0
-    monkeypatch.setenv("LLMCTL_MIXED_STEPS", "0")
-    e2 = InferenceEngine("tiny", **kw)
+    e2 = InferenceEngine("tiny", perf_knobs={"mixed_steps": False}, **kw)
     b = [s.output_ids for s in e2.generate(prompts, p)]
     assert e2.stats.get("mixed_steps", 0) == 0
     assert a == b

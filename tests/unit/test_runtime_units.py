@@ -341,7 +341,7 @@ def test_tuning_cache_changes_dispatch(tmp_path, monkeypatch):
     }
     p = tmp_path / "tuning_cache.json"
     p.write_text(json.dumps(cache))
-    monkeypatch.delenv("LLMCTL_DECODE_SPLITS", raising=False)
+    monkeypatch.delenv("LLMCTL_KNOBS", raising=False)
     saved = (dict(linear.GEMM64_CONFIGS), dict(linear.GEMM64_SHAPE_CONFIGS), dict(functional.SKINNY_CONFIGS))
     try:
         cfg = TrainingConfig(model_name_or_path="tiny", batch_size=2, seq_len=16, device="cpu", log_level="warning",
@@ -354,7 +354,9 @@ def test_tuning_cache_changes_dispatch(tmp_path, monkeypatch):
         eng.shutdown()
         ie = InferenceEngine("tiny", device="cpu", num_kv_blocks=16, block_size=8, max_model_len=64,
                              tuning_cache=str(p))
-        assert os.environ["LLMCTL_DECODE_SPLITS"] == "4" and ie.tuned["decode_splits"] == 4
+        from llmctl.config.knobs import knobs
+
+        assert knobs().decode_splits == 4 and ie.tuned["decode_splits"] == 4
         assert functional.SKINNY_CONFIGS[(16, 12288, 4096)] == 0
     finally:
         linear.GEMM64_CONFIGS.clear()
@@ -363,7 +365,6 @@ def test_tuning_cache_changes_dispatch(tmp_path, monkeypatch):
         linear.GEMM64_SHAPE_CONFIGS.update(saved[1])
         functional.SKINNY_CONFIGS.clear()
         functional.SKINNY_CONFIGS.update(saved[2])
-        os.environ.pop("LLMCTL_DECODE_SPLITS", None)
 
 
 def test_hw_network_benchmark_gloo_rehearsal():
