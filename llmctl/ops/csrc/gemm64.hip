@@ -845,7 +845,14 @@ __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
                  "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]));
 }
 
-template <bool AT, bool BT, int EPI, int GROUP, bool IL>
+// Side job (SIDE > 0: the down projection's wgrad computing dgu = swiglu_bwd(dact, gu), as in the
+// 8-wave kernel above): SIDE chunks of 1024 elements per K-tile per work item, each thread two
+// element pairs per chunk (256 threads).  Phase P3 of K-tile t, after its DMA, stores W(t-2)
+// (slot t & 1) and loads L(t) into the same slot: S_OPS = 10 SIDE vector-memory ops that the
+// waits count past (P0: 20 + 2 S_OPS, P1: 20 + S_OPS, P2: 16 + S_OPS); L(t) is retired by the P1
+// wait of K-tile t+2, before W(t) at P3 of K-tile t+2.  The prologue issues out-of-range dummies
+// W/L(-2) and W/L(-1) at their stream positions so every count holds from the first phase.
+template <bool AT, bool BT, int EPI, int GROUP, bool IL, int SIDE = 0>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(G64Args args) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -873,8 +880,12 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 
   const long lda = args.lda, ldb = args.ldb;
   const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
-  const unsigned short* Bb = BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
+  constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;  // gate + up rows per tile
+  const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
+                             : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
   const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
+  // paired: B_H1 image rows 128 + ip -> up row N + 128 tn + ip (N = F)
+  const i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
   const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
   const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
   const int KT = sp < 0 ? args.K / TK : args.kt_part;
@@ -894,9 +905,76 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const unsigned tc = kt0 + (unsigned)(t < KT ? t : KT - 1);
     const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
     const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
-    const i32x4_t r = kind <= A_HI ? ra : rb;
+    const i32x4_t r = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
 #pragma unroll
     for (int i = 0; i < 4; ++i) bdma16(r, vo[kind][i], so, l + i * 4096);
+  };
+
+  // ---- side job state: per sub-chunk (2 per chunk) the element index / column / gu row offset
+  // of this thread's next pair, per slot the loaded dwords and the gu byte offsets they came from
+  constexpr int SC = SIDE > 0 ? 2 * SIDE : 1;
+  constexpr unsigned SCH = 1024u * (SIDE > 0 ? SIDE : 1);  // elements per K-tile per work item
+  constexpr int S_OPS = 10 * SIDE;
+  unsigned s_e[SC], s_f[SC], s_row[SC], s_og[2][SC], s_ou[2][SC], s_d[2][SC][3];
+  i32x4_t rs_dact, rs_gu, rs_dgu;
+  const unsigned sF = (unsigned)args.s_F;
+  if constexpr (SIDE > 0) {
+    rs_dact = make_rsrc_n(args.s_dact, args.s_E * 2u);
+    rs_gu = make_rsrc_n(args.s_gu, args.s_E * 4u);
+    rs_dgu = make_rsrc_n(args.s_dgu, args.s_E * 4u);
+    const unsigned ktf = (unsigned)(args.K / TK);
+    const unsigned gk0 = bid < args.n_main ? (unsigned)bid * ktf
+                                           : (unsigned)args.n_main * ktf + (unsigned)(bid - args.n_main) * (unsigned)args.kt_part;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) {
+      const unsigned e = gk0 * SCH + 512u * c + 2u * tid;
+      const unsigned t = e / sF;
+      s_e[c] = e;
+      s_f[c] = e - t * sF;
+      s_row[c] = t * 4u * sF;
+      s_og[0][c] = s_ou[0][c] = s_og[1][c] = s_ou[1][c] = SIDE_OOB;
+    }
+  }
+  auto side_load = [&](auto slot_c, auto dummy_c) {
+    constexpr int S = decltype(slot_c)::value;
+    constexpr bool DUMMY = decltype(dummy_c)::value;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) {
+      const bool ok = !DUMMY && s_e[c] < args.s_E;
+      const unsigned oa = ok ? 2u * s_e[c] : SIDE_OOB;
+      const unsigned og = ok ? s_row[c] + 2u * s_f[c] : SIDE_OOB;
+      const unsigned ou = ok ? og + 2u * sF : SIDE_OOB;
+      const i32x4_t ra_ = rs_dact, rg_ = rs_gu;
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" SIDE_NT : "=v"(s_d[S][c][0]) : "v"(oa), "s"(ra_) : "memory");
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" SIDE_NT : "=v"(s_d[S][c][1]) : "v"(og), "s"(rg_) : "memory");
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" SIDE_NT : "=v"(s_d[S][c][2]) : "v"(ou), "s"(rg_) : "memory");
+      s_og[S][c] = og;
+      s_ou[S][c] = ou;
+      if constexpr (!DUMMY) {
+        s_e[c] += SCH;
+        s_f[c] += SCH;
+        const bool wrap = s_f[c] >= sF;  // SCH <= F (side_chunks): at most one row wrap per K-tile
+        s_f[c] -= wrap ? sF : 0u;
+        s_row[c] += wrap ? 4u * sF : 0u;
+      }
+    }
+  };
+  auto side_store = [&](auto slot_c) {
+    constexpr int S = decltype(slot_c)::value;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) {
+      asm volatile("" : "+v"(s_d[S][c][0]), "+v"(s_d[S][c][1]), "+v"(s_d[S][c][2]));
+      const unsigned d = s_d[S][c][0], gg = s_d[S][c][1], uu = s_d[S][c][2];
+      float dg0, du0, dg1, du1;
+      swiglu_bwd1_fast(bf2f(d & 0xffff), bf2f(gg & 0xffff), bf2f(uu & 0xffff), dg0, du0);
+      swiglu_bwd1_fast(bf2f(d >> 16), bf2f(gg >> 16), bf2f(uu >> 16), dg1, du1);
+      const unsigned pg = (unsigned)f2bf(dg0) | ((unsigned)f2bf(dg1) << 16);
+      const unsigned pu = (unsigned)f2bf(du0) | ((unsigned)f2bf(du1) << 16);
+      const unsigned og = s_og[S][c], ou = s_ou[S][c];
+      const i32x4_t r = rs_dgu;
+      asm volatile("buffer_store_dword %0, %1, %2, 0 offen" SIDE_NT ::"v"(pg), "v"(og), "s"(r) : "memory");
+      asm volatile("buffer_store_dword %0, %1, %2, 0 offen" SIDE_NT ::"v"(pu), "v"(ou), "s"(r) : "memory");
+    }
   };
 
   f32x4_t acc[8][8];
@@ -906,7 +984,11 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int ap = wr * 64;
-  const int bo = (B_H0 + wc) * HALF;
+  // B fragments: n-tiles 0-3 (b03) and 4-7 (b47) are positions 0-63 / 64-127 of half-tile
+  // B_h{wc}; paired (gate/up) tiles take this wave's 64 gate columns wc*64.. of B_h0 as b03 and
+  // the matching 64 up columns of B_h1 as b47, so acc[i][j] / acc[i][j + 4] are a gate/up pair
+  const int bo03 = PAIRED_B ? B_H0 * HALF : (B_H0 + wc) * HALF, p03 = PAIRED_B ? wc * 64 : 0;
+  const int bo47 = PAIRED_B ? B_H1 * HALF : (B_H0 + wc) * HALF, p47 = PAIRED_B ? wc * 64 : 64;
   bf16x8_t a_lo[4][2], a_hi[4][2], b47[4][2], b03[2][4][2];
   auto rdA = [&](bf16x8_t (&d)[4][2], const unsigned char* img) {
 #pragma unroll
@@ -914,11 +996,11 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) d[i][ks] = frag<AT>(img, ap + 16 * i, ks, lane);
   };
-  auto rdB = [&](bf16x8_t (&d)[4][2], const unsigned char* img, int n0) {
+  auto rdB = [&](bf16x8_t (&d)[4][2], const unsigned char* img, int p0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) d[j][ks] = frag<BT>(img, 16 * (n0 + j), ks, lane);
+      for (int ks = 0; ks < 2; ++ks) d[j][ks] = frag<BT>(img, p0 + 16 * j, ks, lane);
   };
   auto mma = [&](auto m0_c, auto n0_c, const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2]) {
     g4w_mma<decltype(m0_c)::value, decltype(n0_c)::value>(acc, A, B);
@@ -944,7 +1026,7 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const unsigned tc = kt0 + (unsigned)(t < KT ? t : KT - 1);
     const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
     const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
-    const i32x4_t rr = kind <= A_HI ? ra : rb;
+    const i32x4_t rr = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int ks = r >> 2, i = r & 3;
@@ -962,14 +1044,22 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   issue(K_<B_H0>{}, 0);
   issue(K_<B_H1>{}, 0);
   issue(K_<A_HI>{}, 0);
+  if constexpr (SIDE > 0) {  // W(-2) / L(-2): out-of-range dummies at their stream position
+    side_store(K_<0>{});
+    side_load(K_<0>{}, std::true_type{});
+  }
   issue(K_<A_LO>{}, 1);
   issue(K_<B_H0>{}, 1);
   issue(K_<B_H1>{}, 1);
   issue(K_<A_HI>{}, 1);
-  wait_vm<20>();
+  if constexpr (SIDE > 0) {  // W(-1) / L(-1)
+    side_store(K_<1>{});
+    side_load(K_<1>{}, std::true_type{});
+  }
+  wait_vm<20 + 2 * S_OPS>();
   bar();
   rdA(a_lo, smem + A_LO * HALF);
-  rdB(b03[0], smem + bo, 0);
+  rdB(b03[0], smem + bo03, p03);
   sync(K_<-1>{});  // WAR: P0 restages A_lo of this buffer
 
   auto ktile = [&](int t, auto par_c) {
@@ -977,26 +1067,30 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const unsigned char* buf = smem + P * BUF;
     const unsigned char* nbuf = smem + (P ^ 1) * BUF;
     // P0
-    rdB(b47, buf + bo, 4);
+    rdB(b47, buf + bo47, p47);
     issue(K_<A_LO>{}, t + 2);
     __builtin_amdgcn_sched_barrier(0);
     mma(K_<0>{}, K_<0>{}, a_lo, b03[P]);
-    sync(K_<20>{});
+    sync(K_<20 + 2 * S_OPS>{});
     // P1
     rdA(a_hi, buf + A_HI * HALF);
     issue(K_<B_H0>{}, t + 2);
     __builtin_amdgcn_sched_barrier(0);
     mma(K_<0>{}, K_<4>{}, a_lo, b47);
-    sync(K_<20>{});
+    sync(K_<20 + S_OPS>{});
     // P2
     rdA(a_lo, nbuf + A_LO * HALF);
     issue(K_<B_H1>{}, t + 2);
     __builtin_amdgcn_sched_barrier(0);
     mma(K_<4>{}, K_<4>{}, a_hi, b47);
-    sync(K_<16>{});
+    sync(K_<16 + S_OPS>{});
     // P3
-    rdB(b03[P ^ 1], nbuf + bo, 0);
+    rdB(b03[P ^ 1], nbuf + bo03, p03);
     issue(K_<A_HI>{}, t + 2);
+    if constexpr (SIDE > 0) {
+      side_store(K_<P>{});                   // W(t-2)
+      side_load(K_<P>{}, std::false_type{});  // L(t)
+    }
     __builtin_amdgcn_sched_barrier(0);
     mma(K_<4>{}, K_<0>{}, a_hi, b03[P]);
     sync(K_<-1>{});
@@ -1005,13 +1099,17 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     constexpr int P = decltype(par_c)::value;
     const unsigned char* buf = smem + P * BUF;
     const unsigned char* nbuf = smem + (P ^ 1) * BUF;
-    il_phase(K_<0>{}, K_<0>{}, a_lo, b03[P], std::true_type{}, b47, buf + bo, 64, K_<A_LO>{}, t + 2);
-    sync(K_<20>{});
+    il_phase(K_<0>{}, K_<0>{}, a_lo, b03[P], std::true_type{}, b47, buf + bo47, p47, K_<A_LO>{}, t + 2);
+    sync(K_<20 + 2 * S_OPS>{});
     il_phase(K_<0>{}, K_<4>{}, a_lo, b47, std::false_type{}, a_hi, buf + A_HI * HALF, ap, K_<B_H0>{}, t + 2);
-    sync(K_<20>{});
+    sync(K_<20 + S_OPS>{});
     il_phase(K_<4>{}, K_<4>{}, a_hi, b47, std::false_type{}, a_lo, nbuf + A_LO * HALF, ap, K_<B_H1>{}, t + 2);
-    sync(K_<16>{});
-    il_phase(K_<4>{}, K_<0>{}, a_hi, b03[P], std::true_type{}, b03[P ^ 1], nbuf + bo, 0, K_<A_HI>{}, t + 2);
+    sync(K_<16 + S_OPS>{});
+    il_phase(K_<4>{}, K_<0>{}, a_hi, b03[P], std::true_type{}, b03[P ^ 1], nbuf + bo03, p03, K_<A_HI>{}, t + 2);
+    if constexpr (SIDE > 0) {
+      side_store(K_<P>{});                   // W(t-2)
+      side_load(K_<P>{}, std::false_type{});  // L(t)
+    }
     sync(K_<-1>{});
   };
   for (int t = 0; t < KT; t += 2) {
@@ -1024,12 +1122,108 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     }
   }
   wait_vm<0>();  // the clamped tail items are still landing
+  if constexpr (SIDE > 0) {  // W(KT-2), W(KT-1)
+    side_store(K_<0>{});
+    side_store(K_<1>{});
+  }
   // the last phase's MFMA results -> the epilogue's accumulator reads: 16 wait states (every
   // other accumulator was last written >= 32 MFMAs earlier)
   g4w_fence(acc);
 
   // ---- epilogue: lane holds C[wr*128 + 16 i + (l & 15)][wc*128 + 16 j + 4 (l >> 4) + r]
   const int g = lane >> 4, i16 = lane & 15;
+  if constexpr (EPI == EPI_ROPE_QKV) {
+    // a 256-column tile = 2 heads of D = 128: wave wc owns head 2 tn + wc whole; n-tile j (< 4)
+    // holds dims d = 16 j + 4 g + r, n-tile j + 4 the rotation partners d + 64
+    const int h = 2 * tn + wc;
+    const int nrot = args.nq + args.nkv;  // heads [0, nrot) rotate
+    unsigned short* dst0;
+    long dst_ld;
+    if (h < args.nq) {
+      dst0 = args.c + (long)h * 128;
+      dst_ld = (long)args.nq * 128;
+    } else if (h < nrot) {
+      dst0 = args.out2 + (long)(h - args.nq) * 128;
+      dst_ld = (long)args.nkv * 128;
+    } else {
+      dst0 = args.out3 + (long)(h - nrot) * 128;
+      dst_ld = (long)args.nkv * 128;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = tm * TM + wr * 128 + 16 * i + i16;
+      unsigned short* drow = dst0 + (long)t * dst_ld;
+      const long p = args.pos ? (long)args.pos[t] : (long)(t % args.seq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = 16 * j + 4 * g;
+        float o1[4], o2[4];
+        if (h < nrot) {  // as rope_fwd_kernel on the bf16-stored projection
+          const f32x4_t cs = *reinterpret_cast<const f32x4_t*>(args.cosT + p * 64 + d);
+          const f32x4_t sn = *reinterpret_cast<const f32x4_t*>(args.sinT + p * 64 + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = bf2f(f2bf(acc[i][j][e])), b = bf2f(f2bf(acc[i][j + 4][e]));
+            o1[e] = a * cs[e] - b * sn[e];
+            o2[e] = b * cs[e] + a * sn[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o1[e] = acc[i][j][e];
+            o2[e] = acc[i][j + 4][e];
+          }
+        }
+        s2_t a1, a2;
+        a1[0] = (unsigned)f2bf(o1[0]) | ((unsigned)f2bf(o1[1]) << 16);
+        a1[1] = (unsigned)f2bf(o1[2]) | ((unsigned)f2bf(o1[3]) << 16);
+        a2[0] = (unsigned)f2bf(o2[0]) | ((unsigned)f2bf(o2[1]) << 16);
+        a2[1] = (unsigned)f2bf(o2[2]) | ((unsigned)f2bf(o2[3]) << 16);
+        *reinterpret_cast<s2_t*>(drow + d) = a1;
+        *reinterpret_cast<s2_t*>(drow + 64 + d) = a2;
+      }
+    }
+    return;
+  }
+  if constexpr (PAIRED_B) {
+    // n-tile j (< 4): gate cols 128 tn + wc * 64 + 16 j + 4 g + r; n-tile j + 4: the same up cols.
+    // EPI_UP_SWIGLU stores gu [T, 2F] and act [T, F]; EPI_SWIGLU_FWD only act (into C, ldc = F)
+    const long F = args.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long t = (long)tm * TM + wr * 128 + 16 * i + i16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = tn * 128 + wc * 64 + 16 * j + 4 * g;
+        float o[4];
+        unsigned short gb[4], ub[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // as swiglu_fwd_kernel on the bf16-stored g / u
+          gb[e] = f2bf(acc[i][j][e]);
+          ub[e] = f2bf(acc[i][j + 4][e]);
+          const float gg = bf2f(gb[e]), uu = bf2f(ub[e]);
+          o[e] = gg * (1.f / (1.f + __expf(-gg))) * uu;
+        }
+        s2_t pa;
+        pa[0] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+        pa[1] = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+        if constexpr (EPI == EPI_UP_SWIGLU) {
+          s2_t pg, pu;
+          pg[0] = (unsigned)gb[0] | ((unsigned)gb[1] << 16);
+          pg[1] = (unsigned)gb[2] | ((unsigned)gb[3] << 16);
+          pu[0] = (unsigned)ub[0] | ((unsigned)ub[1] << 16);
+          pu[1] = (unsigned)ub[2] | ((unsigned)ub[3] << 16);
+          unsigned short* gurow = args.c + t * args.ldc;
+          *reinterpret_cast<s2_t*>(gurow + col) = pg;
+          *reinterpret_cast<s2_t*>(gurow + F + col) = pu;
+          *reinterpret_cast<s2_t*>(args.out2 + t * F + col) = pa;
+        } else {
+          *reinterpret_cast<s2_t*>(args.c + t * args.ldc + col) = pa;
+        }
+      }
+    }
+    return;
+  }
   if (sp >= 0) {
     float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 128 + 4 * g;
 #pragma unroll
@@ -1416,7 +1610,8 @@ void launch_g(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
   const dim3 grid(n_items), block(NTHR);
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
-  if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI)) {
+  if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU ||
+                EPI == EPI_SWIGLU_FWD) {
     if (variant == 6 || variant == 7) {  // 4-wave kernel: 128x128 per wave (7: loads interleaved)
       if (variant == 7) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, true>), grid, dim3(NT4), 0, stream(), g);
       else hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, false>), grid, dim3(NT4), 0, stream(), g);
@@ -1595,18 +1790,21 @@ at::Tensor gemm64_swiglu_dgrad(const at::Tensor& dy, const at::Tensor& w, const 
 }
 
 template <int EPI, int SIDE>
-void launch_side(const G64Args& g) {
+void launch_side(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
-  hipLaunchKernelGGL((gemm64_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NTHR), 0, stream(), g);
+  if (variant == 6 || variant == 7)  // 4-wave kernel (7: loads interleaved)
+    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, true, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
+  else
+    hipLaunchKernelGGL((gemm64_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NTHR), 0, stream(), g);
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
   if (n_tail > 0)
     hipLaunchKernelGGL((gemm64_split_reduce<EPI, 4>), dim3(n_tail * (TM * TN / 8 / 256)), dim3(256), 0, stream(), g);
 }
 
 template <int EPI>
-void launch_side_ch(const G64Args& g, int ch) {
-  if (ch == 1) launch_side<EPI, 1>(g);
-  else launch_side<EPI, 2>(g);
+void launch_side_ch(const G64Args& g, int ch, int variant) {
+  if (ch == 1) launch_side<EPI, 1>(g, variant);
+  else launch_side<EPI, 2>(g, variant);
 }
 
 // chunks of 1024 elements per K-tile the side job needs for E = T * F elements over the K-tiles
@@ -1669,12 +1867,13 @@ at::Tensor gemm64_wgrad_swiglu(const at::Tensor& dy, const at::Tensor& act, at::
     ws = at::empty({(long)(g.tiles_m * g.tiles_n - g.n_main) * g.splits * TM * TN}, dy.options().dtype(at::kFloat));
     g.ws = ws.data_ptr<float>();
   }
+  const int variant = (int)((config % 1000) / 100);
   if (f32_out) {
-    if (accumulate) launch_side_ch<EPI_ACC_F32>(g, ch);
-    else launch_side_ch<EPI_STORE_F32>(g, ch);
+    if (accumulate) launch_side_ch<EPI_ACC_F32>(g, ch, variant);
+    else launch_side_ch<EPI_STORE_F32>(g, ch, variant);
   } else {
-    if (accumulate) launch_side_ch<EPI_ACC>(g, ch);
-    else launch_side_ch<EPI_STORE>(g, ch);
+    if (accumulate) launch_side_ch<EPI_ACC>(g, ch, variant);
+    else launch_side_ch<EPI_STORE>(g, ch, variant);
   }
   return dgu;
 }

@@ -23,7 +23,8 @@ def _bf(*shape, seed=0, scale=1.0):
 
 @pytest.mark.parametrize("T,K,nq,nkv", [(512, 256, 4, 2), (1024, 384, 2, 2), (2048, 512, 8, 4)])
 @pytest.mark.parametrize("with_pos", [False, True])
-def test_gemm64_qkv_rope_matches_fp32(native_lib, T, K, nq, nkv, with_pos):
+@pytest.mark.parametrize("config", [104, 704])
+def test_gemm64_qkv_rope_matches_fp32(native_lib, T, K, nq, nkv, with_pos, config):
     D = 128
     x = _bf(T, K, seed=1)
     w = _bf((nq + 2 * nkv) * D, K, seed=2, scale=K ** -0.5)
@@ -32,7 +33,7 @@ def test_gemm64_qkv_rope_matches_fp32(native_lib, T, K, nq, nkv, with_pos):
     pos = None
     if with_pos:
         pos = torch.randint(0, 4096, (T,), device=DEV, dtype=torch.int32)
-    q, k, v = native_lib.gemm64_qkv_rope(x, w, cos, sin, pos, nq, nkv, S, 104)
+    q, k, v = native_lib.gemm64_qkv_rope(x, w, cos, sin, pos, nq, nkv, S, config)
     qkv = (x.float() @ w.float().t())
     rq, rk, rv = ref.rope_qkv_fwd(qkv, cos, sin, nq, nkv, S, pos)
     for got, want in ((q, rq), (k, rk), (v, rv)):
@@ -46,10 +47,13 @@ def test_gemm64_qkv_rope_matches_fp32(native_lib, T, K, nq, nkv, with_pos):
 
 
 @pytest.mark.parametrize("T,K,F", [(256, 256, 128), (512, 384, 384), (1024, 512, 1024)])
-def test_gemm64_up_swiglu_matches_fp32(native_lib, T, K, F):
+@pytest.mark.parametrize("config", [104, 704])
+def test_gemm64_up_swiglu_matches_fp32(native_lib, T, K, F, config):
     x = _bf(T, K, seed=3)
     w = _bf(2 * F, K, seed=4, scale=K ** -0.5)
-    gu, act = native_lib.gemm64_up_swiglu(x, w, 104)
+    gu, act = native_lib.gemm64_up_swiglu(x, w, config)
+    act2 = native_lib.gemm64_swiglu_fwd(x, w, config)  # serving prefill form: act only
+    assert torch.equal(act2, act)
     gu_ref = x.float() @ w.float().t()
     assert row_err(gu, gu_ref) < TOL
     act_ref = ref.swiglu_fwd(gu_ref)

@@ -204,7 +204,11 @@ def _swiglu_bwd_ref(dact, gu):
                                        (512, 2048, 2048, 104),   # two chunks per K-tile
                                        (512, 3072, 2304, 104),   # elements past E (range-checked)
                                        (2048, 4096, 1024, 4104),  # every tile split into 4 K-ranges
-                                       (2048, 4096, 1024, 1104)])
+                                       (2048, 4096, 1024, 1104),
+                                       (512, 4096, 1024, 704),    # 4-wave kernel: one chunk per K-tile
+                                       (512, 2048, 2048, 704),    # two chunks
+                                       (512, 3072, 2304, 704),    # range-checked tail
+                                       (2048, 4096, 1024, 4704)])
 @pytest.mark.parametrize("gdt,acc", [(torch.bfloat16, False), (torch.bfloat16, True), (torch.float32, False),
                                      (torch.float32, True)])
 def test_gemm64_wgrad_swiglu(native_lib, T, H, F, cfg, gdt, acc):
