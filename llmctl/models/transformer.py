@@ -223,7 +223,7 @@ class _UpSwiGLUDown(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_up, w_down):
-        from llmctl.exec.linear import forward_linear, gemm64_config
+        from llmctl.exec.linear import forward_linear, gemm64_config, wgrad_swiglu_ok
         from llmctl.ops._lib import native
 
         x2 = x.reshape(-1, x.shape[-1])
@@ -232,6 +232,11 @@ class _UpSwiGLUDown(torch.autograd.Function):
         out = forward_linear(act, w_down)
         if ctx.needs_input_grad[0]:
             _prep_weight_t(w_up, T)
+        # the SwiGLU backward as the down projection wgrad's side job (swiglu_bwd = side), as
+        # _SwiGLUDown; the down data gradient then runs plain (gemm64 or hipBLASLt through W^T)
+        ctx.side = gu.requires_grad and wgrad_swiglu_ok(w_down, T, w_down.shape[1])
+        if ctx.side:
+            _prep_weight_t(w_down, T)
         ctx.save_for_backward(x2, gu, act)
         ctx.w_up, ctx.w_down, ctx.xshape = w_up, w_down, x.shape
         return out.view(*x.shape[:-1], w_down.shape[0])
@@ -240,8 +245,19 @@ class _UpSwiGLUDown(torch.autograd.Function):
     def backward(ctx, dout):
         x2, gu, act = ctx.saved_tensors
         dout2 = dout.reshape(-1, dout.shape[-1])
-        dw_down = weight_grad(ctx.w_down, dout2, act)
-        dgu = swiglu_data_grad(dout2, ctx.w_down, gu)
+        dgu = None
+        if ctx.side:
+            dact = data_grad(dout2, ctx.w_down)
+            dgu = ctx.w_down._llmctl_grad_sink.write_swiglu(ctx.w_down, dout2, act, dact, gu)
+            dw_down = None
+            if dgu is None:  # operands the side kernel cannot take: weight gradient + elementwise pass
+                from llmctl.ops._lib import native
+
+                dw_down = weight_grad(ctx.w_down, dout2, act)
+                dgu = native().swiglu_bwd(dact, gu)
+        else:
+            dw_down = weight_grad(ctx.w_down, dout2, act)
+            dgu = swiglu_data_grad(dout2, ctx.w_down, gu)
         dw_up = weight_grad(ctx.w_up, dgu, x2) if ctx.needs_input_grad[1] else None
         dx = data_grad(dgu, ctx.w_up).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         return dx, dw_up, dw_down

@@ -61,16 +61,17 @@ def test_gemm64_up_swiglu_matches_fp32(native_lib, T, K, F, config):
     assert row_err(act, ref.swiglu_fwd(gu)) < 8e-3  # act is computed from the stored bf16 gu
 
 
-def _layer_grads(fused: bool, monkeypatch, sink: bool):
+def _layer_grads(fused: bool, monkeypatch, sink: bool, extra=None, dims=(512, 4, 2, 1024)):
     from llmctl.config.knobs import configure
 
-    configure({"fused_fwd": fused})  # A/B both
+    configure({"fused_fwd": fused, **(extra or {})})  # A/B both
     from llmctl.exec.linear import GradSink
     from llmctl.models import ParallelContext, get_model_config
     from llmctl.models.transformer import DecoderLayer
 
     cfg = get_model_config("tiny")
-    cfg.hidden, cfg.heads, cfg.kv_heads, cfg.ffn, cfg.head_dim = 512, 4, 2, 1024, 128
+    cfg.hidden, cfg.heads, cfg.kv_heads, cfg.ffn = dims
+    cfg.head_dim = 128
     torch.manual_seed(0)
     layer = DecoderLayer(cfg, ParallelContext(), 0, device=DEV, dtype=torch.bfloat16)
     grads = {}
@@ -102,6 +103,24 @@ def layer_rope(cfg, S):
 def test_decoder_layer_fused_forward_matches_unfused(native_lib, monkeypatch, sink):
     out_f, g_f = _layer_grads(True, monkeypatch, sink)
     out_u, g_u = _layer_grads(False, monkeypatch, sink)
+    assert row_err(out_f, out_u.float()) < TOL
+    for n in g_u:
+        a, b = g_f[n].float(), g_u[n].float()
+        a2 = a.reshape(a.shape[0], -1) if a.dim() > 1 else a.view(1, -1)
+        b2 = b.reshape(b.shape[0], -1) if b.dim() > 1 else b.view(1, -1)
+        assert row_err(a2, b2) < 3e-2, n
+
+
+@pytest.mark.parametrize("config", [104, 704])
+def test_decoder_layer_all_gemm64_matches_hipblaslt(native_lib, monkeypatch, config):
+    """Every projection of the layer on gemm64 (fused RoPE-QKV / up-SwiGLU forward epilogues,
+    forward + data gradients with W read K-major, weight gradients, the SwiGLU backward as the
+    down wgrad's side job at hidden 4096 / ffn 1024) against the library path (hipBLASLt
+    forward / data gradients, unfused RoPE / SwiGLU), forward and every gradient."""
+    knobs = {"gemm64_config": config, "fwd64": "all", "dgrad64": "all"}
+    dims = (4096, 32, 8, 1024)
+    out_f, g_f = _layer_grads(True, monkeypatch, True, knobs, dims)
+    out_u, g_u = _layer_grads(False, monkeypatch, True, {"gemm64": False, "wgrad_kernel": False}, dims)
     assert row_err(out_f, out_u.float()) < TOL
     for n in g_u:
         a, b = g_f[n].float(), g_u[n].float()
