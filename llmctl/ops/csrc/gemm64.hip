@@ -838,6 +838,25 @@ __device__ __forceinline__ void g4w_row(f32x4_t& c0, f32x4_t& c1, f32x4_t& c2, f
                : "memory");
 }
 
+// g4w_row with one LDS-DMA piece issued between its second and third MFMA (variant 8): M0 is
+// written ahead of the first MFMA, so the two MFMAs cover the M0 -> LDS-DMA wait state that the
+// stand-alone bdma16 pays with an s_nop (4 issue cycles), and the DMA issue shares a gap with no
+// other filler (an MFMA gap leaves 8 of its 16 cycles to other instructions).
+__device__ __forceinline__ void g4w_row_dma(f32x4_t& c0, f32x4_t& c1, f32x4_t& c2, f32x4_t& c3, const bf16x8_t& a,
+                                            const bf16x8_t& b0, const bf16x8_t& b1, const bf16x8_t& b2,
+                                            const bf16x8_t& b3, unsigned voff, i32x4_t rsrc, unsigned soff,
+                                            unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %12\n\t"
+               "v_mfma_f32_16x16x32_bf16 %0, %5, %4, %0\n\t"
+               "v_mfma_f32_16x16x32_bf16 %1, %6, %4, %1\n\t"
+               "buffer_load_dwordx4 %9, %10, %11 offen lds\n\t"
+               "v_mfma_f32_16x16x32_bf16 %2, %7, %4, %2\n\t"
+               "v_mfma_f32_16x16x32_bf16 %3, %8, %4, %3"
+               : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
+               : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(voff), "s"(rsrc), "s"(soff), "s"(lds_byte)
+               : "memory");
+}
+
 __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
   asm volatile("s_nop 7\n\ts_nop 7"
                : "+a"(acc[4][0]), "+a"(acc[4][1]), "+a"(acc[4][2]), "+a"(acc[4][3]), "+a"(acc[5][0]), "+a"(acc[5][1]),
@@ -852,7 +871,9 @@ __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
 // waits count past (P0: 20 + 2 S_OPS, P1: 20 + S_OPS, P2: 16 + S_OPS); L(t) is retired by the P1
 // wait of K-tile t+2, before W(t) at P3 of K-tile t+2.  The prologue issues out-of-range dummies
 // W/L(-2) and W/L(-1) at their stream positions so every count holds from the first phase.
-template <bool AT, bool BT, int EPI, int GROUP, bool IL, int SIDE = 0>
+// IL: 0 = loads ahead of each phase's MFMAs (variant 6), 1 = loads interleaved between MFMA row
+// blocks (variant 7), 2 = as 1 with the DMA pieces inside the MFMA statements (variant 8)
+template <bool AT, bool BT, int EPI, int GROUP, int IL, int SIDE = 0>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(G64Args args) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1030,12 +1051,17 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int ks = r >> 2, i = r & 3;
-      g4w_row(acc[m0 + i][n0], acc[m0 + i][n0 + 1], acc[m0 + i][n0 + 2], acc[m0 + i][n0 + 3], A[i][ks], B[0][ks],
-              B[1][ks], B[2][ks], B[3][ks]);
+      if (IL == 2 && (r & 1) == 0) {
+        g4w_row_dma(acc[m0 + i][n0], acc[m0 + i][n0 + 1], acc[m0 + i][n0 + 2], acc[m0 + i][n0 + 3], A[i][ks],
+                    B[0][ks], B[1][ks], B[2][ks], B[3][ks], vo[kind][r >> 1], rr, so, l + (r >> 1) * 4096);
+      } else {
+        g4w_row(acc[m0 + i][n0], acc[m0 + i][n0 + 1], acc[m0 + i][n0 + 2], acc[m0 + i][n0 + 3], A[i][ks], B[0][ks],
+                B[1][ks], B[2][ks], B[3][ks]);
+      }
       const int f = r >> 1, fk = r & 1;
       if constexpr (RDB) dst[f][fk] = frag<BT>(img, p0 + 16 * f, fk, lane);
       else dst[f][fk] = frag<AT>(img, p0 + 16 * f, fk, lane);
-      if ((r & 1) == 0) bdma16(rr, vo[kind][r >> 1], so, l + (r >> 1) * 4096);
+      if (IL != 2 && (r & 1) == 0) bdma16(rr, vo[kind][r >> 1], so, l + (r >> 1) * 4096);
     }
   };
 
@@ -1113,7 +1139,7 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     sync(K_<-1>{});
   };
   for (int t = 0; t < KT; t += 2) {
-    if constexpr (IL) {
+    if constexpr (IL > 0) {
       ktile_il(t, K_<0>{});
       ktile_il(t + 1, K_<1>{});
     } else {
@@ -1612,9 +1638,10 @@ void launch_g(const G64Args& g, int variant) {
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
   if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU ||
                 EPI == EPI_SWIGLU_FWD) {
-    if (variant == 6 || variant == 7) {  // 4-wave kernel: 128x128 per wave (7: loads interleaved)
-      if (variant == 7) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, true>), grid, dim3(NT4), 0, stream(), g);
-      else hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, false>), grid, dim3(NT4), 0, stream(), g);
+    if (variant >= 6 && variant <= 8) {  // 4-wave kernel: 128x128 per wave (7/8: loads interleaved)
+      if (variant == 8) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 2>), grid, dim3(NT4), 0, stream(), g);
+      else if (variant == 7) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 1>), grid, dim3(NT4), 0, stream(), g);
+      else hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 0>), grid, dim3(NT4), 0, stream(), g);
       variant = -1;
     }
   }
@@ -1792,8 +1819,10 @@ at::Tensor gemm64_swiglu_dgrad(const at::Tensor& dy, const at::Tensor& w, const 
 template <int EPI, int SIDE>
 void launch_side(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
-  if (variant == 6 || variant == 7)  // 4-wave kernel (7: loads interleaved)
-    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, true, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
+  if (variant == 8)  // 4-wave kernel, loads interleaved (8: DMA inside the MFMA statements)
+    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 2, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
+  else if (variant == 6 || variant == 7)
+    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
   else
     hipLaunchKernelGGL((gemm64_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NTHR), 0, stream(), g);
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
