@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 
 from llmctl.comms.overlap import GradSyncEngine
+from llmctl.config.knobs import knobs
 from llmctl.models import ModelConfig, ParallelContext, build_model, get_model_config
 from llmctl.parallel.groups import ProcessGroups, build_process_groups
 from llmctl.runtime.faults import FaultInjector

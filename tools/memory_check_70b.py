@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Per-GPU memory of BASELINE config #4 (Llama-3-70B, PP4 x DP2, ZeRO-3) from a 1-GPU slice,
+against the planner's estimate (llmctl/partition/planner.py ``compute_memory_requirement``).
+
+Two slices of the real 70B layer (hidden 8192, ffn 28672, 64 q / 8 kv heads, vocab 128256) with
+L0 and L1 decoder layers train one step each on one MI355X (ZeRO-0, one rank).  Their difference
+gives, per decoder layer:
+  * state bytes (bf16 param + grad, fp32 master + Adam m / v): allocated after a step;
+  * activation bytes per micro-batch: the step's peak minus the state.
+The intercept is the embedding / LM head / logits share.  The PP4 x DP2 ZeRO-3 layout's stage
+(20 layers; stage 0 holds the embedding, stage 3 the LM head) then needs
+  state / dp  (ZeRO-3 shards params, grads and optimizer state over the DP pair)
+  + 2 gathered layers of bf16 parameters (current + prefetched)
+  + activations x layers x in-flight micro-batches (1F1B: min(pp, microbatches) on stage 0)
+  + the edge (embedding or LM head + logits) share,
+which is printed next to the planner's number for the same micro-batch / recompute setting.
+
+    python tools/memory_check_70b.py --layers 1 2 --micro-batch 1 --ac selective
+"""
+
+import argparse
+import dataclasses
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+GiB = 2**30
+
+
+def measure(model, layers, mb, seq, ac):
+    import torch
+
+    from llmctl.io.synthetic import SyntheticTokens
+    from llmctl.models import get_model_config
+    from llmctl.runtime.engine import TrainingConfig, TrainingEngine
+
+    mc = dataclasses.replace(get_model_config(model), layers=layers)
+    cfg = TrainingConfig(model_name_or_path=model, batch_size=mb, seq_len=seq, max_steps=4, learning_rate=1e-4,
+                         device="cuda", log_level="warning", activation_checkpoint=ac)
+    eng = TrainingEngine(cfg, mc)
+    data = SyntheticTokens(mc.vocab_size, seq, mb, seed=1, rank=0, device=eng.device)
+    eng.train_step([data.batch(0)])  # allocates everything lazy (grads, optimizer state)
+    torch.cuda.synchronize()
+    state = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    eng.train_step([data.batch(1)])
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated()
+    res = {"layers": layers, "state_gb": round(state / GiB, 2), "peak_gb": round(peak / GiB, 2),
+           "params": sum(p.numel() for p in eng.model.parameters())}
+    eng.shutdown()
+    del eng
+    torch.cuda.empty_cache()
+    return res, mc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-70b")
+    ap.add_argument("--layers", type=int, nargs=2, default=[1, 2])
+    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--ac", default="selective")
+    ap.add_argument("--pp", type=int, default=4)
+    ap.add_argument("--dp", type=int, default=2)
+    ap.add_argument("--microbatches", type=int, default=8)
+    a = ap.parse_args()
+    rows = []
+    for L in a.layers:
+        r, mc = measure(a.model, L, a.micro_batch, a.seq_len, a.ac)
+        print(json.dumps(r), flush=True)
+        rows.append(r)
+    (r0, r1) = rows
+    dl = r1["layers"] - r0["layers"]
+    state_layer = (r1["state_gb"] - r0["state_gb"]) / dl
+    act_layer = ((r1["peak_gb"] - r1["state_gb"]) - (r0["peak_gb"] - r0["state_gb"])) / dl
+    edge_state = r0["state_gb"] - state_layer * r0["layers"]
+    edge_act = (r0["peak_gb"] - r0["state_gb"]) - act_layer * r0["layers"]
+    from llmctl.models import get_model_config
+    from llmctl.partition.planner import ParallelismPlanner
+
+    full = get_model_config(a.model)
+    layers_stage = math.ceil(full.layers / a.pp)
+    inflight = min(a.pp, a.microbatches)
+    layer_bf16_gb = 2.0 * (full.num_parameters(include_embedding=False) / full.layers) / GiB
+    # stage 0: embedding (+ its optimizer state) is about half the measured edge state (embedding +
+    # LM head in the slice); stage 3 holds the LM head and the logits
+    stage0 = (state_layer * layers_stage + edge_state / 2) / a.dp + 2 * layer_bf16_gb + act_layer * layers_stage * inflight
+    stage_last = (state_layer * layers_stage + edge_state / 2) / a.dp + 2 * layer_bf16_gb + \
+        act_layer * layers_stage * 1 + edge_act
+    planner = ParallelismPlanner(full.to_dict(), {"gpu": {"count": a.pp * a.dp}}, seq_len=a.seq_len)
+    est = planner.compute_memory_requirement(1, a.pp, a.dp, 3, a.micro_batch, sp=False, ac=a.ac,
+                                             num_microbatches=a.microbatches)
+    print(json.dumps({"model": full.name, "layout": f"pp{a.pp}-dp{a.dp}-zero3", "micro_batch": a.micro_batch,
+                      "seq_len": a.seq_len, "ac": a.ac, "state_gb_per_layer": round(state_layer, 3),
+                      "act_gb_per_layer_per_microbatch": round(act_layer, 3), "edge_state_gb": round(edge_state, 2),
+                      "edge_act_gb": round(edge_act, 2), "stage0_gb_from_slice": round(stage0, 1),
+                      "last_stage_gb_from_slice": round(stage_last, 1), "planner_gb": round(est, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
