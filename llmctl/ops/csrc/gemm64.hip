@@ -857,6 +857,29 @@ __device__ __forceinline__ void g4w_row_dma(f32x4_t& c0, f32x4_t& c1, f32x4_t& c
                : "memory");
 }
 
+// two MFMAs (acc row i x n-tiles j, j+1, one K-slice) / the same with one LDS-DMA piece between
+// them (M0 written ahead of the first MFMA): variant 9's finer statements, so each fragment read
+// and each DMA piece gets an MFMA gap of its own
+__device__ __forceinline__ void g4w_pair(f32x4_t& c0, f32x4_t& c1, const bf16x8_t& a, const bf16x8_t& b0,
+                                         const bf16x8_t& b1) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %3, %2, %0\n\t"
+               "v_mfma_f32_16x16x32_bf16 %1, %4, %2, %1"
+               : "+a"(c0), "+a"(c1)
+               : "v"(a), "v"(b0), "v"(b1)
+               : "memory");
+}
+__device__ __forceinline__ void g4w_pair_dma(f32x4_t& c0, f32x4_t& c1, const bf16x8_t& a, const bf16x8_t& b0,
+                                             const bf16x8_t& b1, unsigned voff, i32x4_t rsrc, unsigned soff,
+                                             unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %8\n\t"
+               "v_mfma_f32_16x16x32_bf16 %0, %3, %2, %0\n\t"
+               "buffer_load_dwordx4 %5, %6, %7 offen lds\n\t"
+               "v_mfma_f32_16x16x32_bf16 %1, %4, %2, %1"
+               : "+a"(c0), "+a"(c1)
+               : "v"(a), "v"(b0), "v"(b1), "v"(voff), "s"(rsrc), "s"(soff), "s"(lds_byte)
+               : "memory");
+}
+
 __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
   asm volatile("s_nop 7\n\ts_nop 7"
                : "+a"(acc[4][0]), "+a"(acc[4][1]), "+a"(acc[4][2]), "+a"(acc[4][3]), "+a"(acc[5][0]), "+a"(acc[5][1]),
@@ -872,7 +895,8 @@ __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
 // wait of K-tile t+2, before W(t) at P3 of K-tile t+2.  The prologue issues out-of-range dummies
 // W/L(-2) and W/L(-1) at their stream positions so every count holds from the first phase.
 // IL: 0 = loads ahead of each phase's MFMAs (variant 6), 1 = loads interleaved between MFMA row
-// blocks (variant 7), 2 = as 1 with the DMA pieces inside the MFMA statements (variant 8)
+// blocks (variant 7), 2 = as 1 with the DMA pieces inside the MFMA statements (variant 8), 3 =
+// 2-MFMA statements, reads in the first half of the phase, DMA in the second (variant 9)
 template <bool AT, bool BT, int EPI, int GROUP, int IL, int SIDE = 0>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(G64Args args) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
@@ -1048,6 +1072,28 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
     const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
     const i32x4_t rr = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
+    if constexpr (IL == 3) {
+      // variant 9: 16 statements of 2 MFMAs; the 8 fragment reads go out after statements 0-7
+      // (they complete long before the phase's closing lgkmcnt wait), the 4 DMA pieces inside
+      // statements 9, 11, 13, 15
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ks = q >> 3, i = (q >> 1) & 3, j = (q & 1) * 2;
+        if (q >= 8 && (q & 1)) {
+          const int pc = (q - 9) >> 1;
+          g4w_pair_dma(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks],
+                       vo[kind][pc], rr, so, l + pc * 4096);
+        } else {
+          g4w_pair(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks]);
+        }
+        if (q < 8) {
+          const int f = q >> 1, fk = q & 1;
+          if constexpr (RDB) dst[f][fk] = frag<BT>(img, p0 + 16 * f, fk, lane);
+          else dst[f][fk] = frag<AT>(img, p0 + 16 * f, fk, lane);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int ks = r >> 2, i = r & 3;
@@ -1638,8 +1684,9 @@ void launch_g(const G64Args& g, int variant) {
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
   if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU ||
                 EPI == EPI_SWIGLU_FWD) {
-    if (variant >= 6 && variant <= 8) {  // 4-wave kernel: 128x128 per wave (7/8: loads interleaved)
-      if (variant == 8) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 2>), grid, dim3(NT4), 0, stream(), g);
+    if (variant >= 6 && variant <= 9) {  // 4-wave kernel: 128x128 per wave (7-9: loads interleaved)
+      if (variant == 9) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 3>), grid, dim3(NT4), 0, stream(), g);
+      else if (variant == 8) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 2>), grid, dim3(NT4), 0, stream(), g);
       else if (variant == 7) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 1>), grid, dim3(NT4), 0, stream(), g);
       else hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 0>), grid, dim3(NT4), 0, stream(), g);
       variant = -1;
@@ -1819,7 +1866,9 @@ at::Tensor gemm64_swiglu_dgrad(const at::Tensor& dy, const at::Tensor& w, const 
 template <int EPI, int SIDE>
 void launch_side(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
-  if (variant == 8)  // 4-wave kernel, loads interleaved (8: DMA inside the MFMA statements)
+  if (variant == 9)  // 4-wave kernel, loads interleaved (8/9: DMA inside the MFMA statements)
+    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 3, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
+  else if (variant == 8)
     hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 2, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
   else if (variant == 6 || variant == 7)
     hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
