@@ -235,6 +235,11 @@ MODEL_TEMPLATES: Dict[str, Dict[str, Dict[str, Any]]] = {
             "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
             "rope": {"base": 10000, "scaling": "linear"},
         },
+        "deep64": {  # 8 layers at head_dim 64: the deep pipeline layouts on the GPU kernels (D 64 / 128)
+            "name": "tiny-deep64", "arch": "decoder-only", "layers": 8, "hidden": 256, "ffn": 704,
+            "heads": 4, "kv_heads": 2, "vocab_size": 512, "max_position_embeddings": 512,
+            "rope": {"base": 10000, "scaling": "linear"},
+        },
         "wide": {  # 8 query / 8 KV heads: enough heads for TP=8 (BASELINE config #5's degree)
             "name": "tiny-wide", "arch": "decoder-only", "layers": 2, "hidden": 512, "ffn": 1024,
             "heads": 8, "kv_heads": 8, "vocab_size": 512, "max_position_embeddings": 512,
@@ -255,6 +260,7 @@ ALIASES = {
     "llama-70b": ("llama", "70b"), "tiny": ("tiny", "test"), "tiny-test": ("tiny", "test"),
     "mixtral-8x7b": ("mixtral", "8x7b"), "tiny-moe": ("tiny", "moe"),
     "tiny-tied": ("tiny", "tied"), "tiny-deep": ("tiny", "deep"), "tiny-wide": ("tiny", "wide"),
+    "tiny-deep64": ("tiny", "deep64"),
 }
 
 

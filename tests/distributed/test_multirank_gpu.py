@@ -86,8 +86,8 @@ def test_config4_pp4_dp2_zero3_eight_ranks_one_gpu():
     all-gathers + gradient reduce-scatters across the DP pair of every stage, and the 1F1B
     schedule's device-tensor p2p.  An 8-layer model (2 per stage); the losses follow one process
     accumulating both DP ranks' micro-batches."""
-    ref = _layout_losses(1, {}, "tiny-deep", ref_dp=2)[0]
-    out = _layout_losses(8, {"pp": 4, "zero": 3, "microbatches": 4}, "tiny-deep", timeout=240)
+    ref = _layout_losses(1, {}, "tiny-deep64", ref_dp=2)[0]
+    out = _layout_losses(8, {"pp": 4, "zero": 3, "microbatches": 4}, "tiny-deep64", timeout=240)
     assert all(o["native"] and o["zero3"] and o["pp"] == 4 and o["dp"] == 2 for o in out)
     assert out[0]["backend"] == "gloo"
     for a, b in zip(out[0]["losses"], ref["losses"]):
