@@ -887,6 +887,155 @@ __device__ __forceinline__ void g4w_fence(f32x4_t (&acc)[8][8]) {
                  "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]));
 }
 
+// 4-wave epilogues (lane holds C[wr*128 + 16 i + (l & 15)][wc*128 + 16 j + 4 (l >> 4) + r]): split
+// partial, fp32 store / accumulate, bf16 store / accumulate, fused RoPE-QKV / SwiGLU forward
+template <int EPI>
+__device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)[8][8], int tm, int tn, int wr, int wc,
+                                             int lane, int sp, int u) {
+  constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;
+  const int g = lane >> 4, i16 = lane & 15;
+  if constexpr (EPI == EPI_ROPE_QKV) {
+    // a 256-column tile = 2 heads of D = 128: wave wc owns head 2 tn + wc whole; n-tile j (< 4)
+    // holds dims d = 16 j + 4 g + r, n-tile j + 4 the rotation partners d + 64
+    const int h = 2 * tn + wc;
+    const int nrot = args.nq + args.nkv;  // heads [0, nrot) rotate
+    unsigned short* dst0;
+    long dst_ld;
+    if (h < args.nq) {
+      dst0 = args.c + (long)h * 128;
+      dst_ld = (long)args.nq * 128;
+    } else if (h < nrot) {
+      dst0 = args.out2 + (long)(h - args.nq) * 128;
+      dst_ld = (long)args.nkv * 128;
+    } else {
+      dst0 = args.out3 + (long)(h - nrot) * 128;
+      dst_ld = (long)args.nkv * 128;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = tm * TM + wr * 128 + 16 * i + i16;
+      unsigned short* drow = dst0 + (long)t * dst_ld;
+      const long p = args.pos ? (long)args.pos[t] : (long)(t % args.seq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = 16 * j + 4 * g;
+        float o1[4], o2[4];
+        if (h < nrot) {  // as rope_fwd_kernel on the bf16-stored projection
+          const f32x4_t cs = *reinterpret_cast<const f32x4_t*>(args.cosT + p * 64 + d);
+          const f32x4_t sn = *reinterpret_cast<const f32x4_t*>(args.sinT + p * 64 + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = bf2f(f2bf(acc[i][j][e])), b = bf2f(f2bf(acc[i][j + 4][e]));
+            o1[e] = a * cs[e] - b * sn[e];
+            o2[e] = b * cs[e] + a * sn[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o1[e] = acc[i][j][e];
+            o2[e] = acc[i][j + 4][e];
+          }
+        }
+        s2_t a1, a2;
+        a1[0] = (unsigned)f2bf(o1[0]) | ((unsigned)f2bf(o1[1]) << 16);
+        a1[1] = (unsigned)f2bf(o1[2]) | ((unsigned)f2bf(o1[3]) << 16);
+        a2[0] = (unsigned)f2bf(o2[0]) | ((unsigned)f2bf(o2[1]) << 16);
+        a2[1] = (unsigned)f2bf(o2[2]) | ((unsigned)f2bf(o2[3]) << 16);
+        *reinterpret_cast<s2_t*>(drow + d) = a1;
+        *reinterpret_cast<s2_t*>(drow + 64 + d) = a2;
+      }
+    }
+    return;
+  }
+  if constexpr (PAIRED_B) {
+    // n-tile j (< 4): gate cols 128 tn + wc * 64 + 16 j + 4 g + r; n-tile j + 4: the same up cols.
+    // EPI_UP_SWIGLU stores gu [T, 2F] and act [T, F]; EPI_SWIGLU_FWD only act (into C, ldc = F)
+    const long F = args.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long t = (long)tm * TM + wr * 128 + 16 * i + i16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = tn * 128 + wc * 64 + 16 * j + 4 * g;
+        float o[4];
+        unsigned short gb[4], ub[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // as swiglu_fwd_kernel on the bf16-stored g / u
+          gb[e] = f2bf(acc[i][j][e]);
+          ub[e] = f2bf(acc[i][j + 4][e]);
+          const float gg = bf2f(gb[e]), uu = bf2f(ub[e]);
+          o[e] = gg * (1.f / (1.f + __expf(-gg))) * uu;
+        }
+        s2_t pa;
+        pa[0] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+        pa[1] = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+        if constexpr (EPI == EPI_UP_SWIGLU) {
+          s2_t pg, pu;
+          pg[0] = (unsigned)gb[0] | ((unsigned)gb[1] << 16);
+          pg[1] = (unsigned)gb[2] | ((unsigned)gb[3] << 16);
+          pu[0] = (unsigned)ub[0] | ((unsigned)ub[1] << 16);
+          pu[1] = (unsigned)ub[2] | ((unsigned)ub[3] << 16);
+          unsigned short* gurow = args.c + t * args.ldc;
+          *reinterpret_cast<s2_t*>(gurow + col) = pg;
+          *reinterpret_cast<s2_t*>(gurow + F + col) = pu;
+          *reinterpret_cast<s2_t*>(args.out2 + t * F + col) = pa;
+        } else {
+          *reinterpret_cast<s2_t*>(args.c + t * args.ldc + col) = pa;
+        }
+      }
+    }
+    return;
+  }
+  if (sp >= 0) {
+    float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 128 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + 16 * j) = acc[i][j];
+    return;
+  }
+  if constexpr (epi_f32(EPI)) {
+    float* Cf = reinterpret_cast<float*>(args.c) + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (EPI == EPI_ACC_F32) {
+        f32x4_t old[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j) = old[j] + acc[i][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j) = acc[i][j];
+      }
+    }
+    return;
+  }
+  unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + 4 * g;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s2_t old[8];
+    if constexpr (EPI == EPI_ACC) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f32x4_t v = acc[i][j];
+      if constexpr (EPI == EPI_ACC) {
+        v[0] += bf2f(old[j][0] & 0xffff);
+        v[1] += bf2f(old[j][0] >> 16);
+        v[2] += bf2f(old[j][1] & 0xffff);
+        v[3] += bf2f(old[j][1] >> 16);
+      }
+      s2_t o;
+      o[0] = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+      o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      *reinterpret_cast<s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j) = o;
+    }
+  }
+}
+
 // Side job (SIDE > 0: the down projection's wgrad computing dgu = swiglu_bwd(dact, gu), as in the
 // 8-wave kernel above): SIDE chunks of 1024 elements per K-tile per work item, each thread two
 // element pairs per chunk (256 threads).  Phase P3 of K-tile t, after its DMA, stores W(t-2)
@@ -1202,148 +1351,153 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // other accumulator was last written >= 32 MFMAs earlier)
   g4w_fence(acc);
 
-  // ---- epilogue: lane holds C[wr*128 + 16 i + (l & 15)][wc*128 + 16 j + 4 (l >> 4) + r]
-  const int g = lane >> 4, i16 = lane & 15;
-  if constexpr (EPI == EPI_ROPE_QKV) {
-    // a 256-column tile = 2 heads of D = 128: wave wc owns head 2 tn + wc whole; n-tile j (< 4)
-    // holds dims d = 16 j + 4 g + r, n-tile j + 4 the rotation partners d + 64
-    const int h = 2 * tn + wc;
-    const int nrot = args.nq + args.nkv;  // heads [0, nrot) rotate
-    unsigned short* dst0;
-    long dst_ld;
-    if (h < args.nq) {
-      dst0 = args.c + (long)h * 128;
-      dst_ld = (long)args.nq * 128;
-    } else if (h < nrot) {
-      dst0 = args.out2 + (long)(h - args.nq) * 128;
-      dst_ld = (long)args.nkv * 128;
-    } else {
-      dst0 = args.out3 + (long)(h - nrot) * 128;
-      dst_ld = (long)args.nkv * 128;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int t = tm * TM + wr * 128 + 16 * i + i16;
-      unsigned short* drow = dst0 + (long)t * dst_ld;
-      const long p = args.pos ? (long)args.pos[t] : (long)(t % args.seq);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int d = 16 * j + 4 * g;
-        float o1[4], o2[4];
-        if (h < nrot) {  // as rope_fwd_kernel on the bf16-stored projection
-          const f32x4_t cs = *reinterpret_cast<const f32x4_t*>(args.cosT + p * 64 + d);
-          const f32x4_t sn = *reinterpret_cast<const f32x4_t*>(args.sinT + p * 64 + d);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float a = bf2f(f2bf(acc[i][j][e])), b = bf2f(f2bf(acc[i][j + 4][e]));
-            o1[e] = a * cs[e] - b * sn[e];
-            o2[e] = b * cs[e] + a * sn[e];
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            o1[e] = acc[i][j][e];
-            o2[e] = acc[i][j + 4][e];
-          }
-        }
-        s2_t a1, a2;
-        a1[0] = (unsigned)f2bf(o1[0]) | ((unsigned)f2bf(o1[1]) << 16);
-        a1[1] = (unsigned)f2bf(o1[2]) | ((unsigned)f2bf(o1[3]) << 16);
-        a2[0] = (unsigned)f2bf(o2[0]) | ((unsigned)f2bf(o2[1]) << 16);
-        a2[1] = (unsigned)f2bf(o2[2]) | ((unsigned)f2bf(o2[3]) << 16);
-        *reinterpret_cast<s2_t*>(drow + d) = a1;
-        *reinterpret_cast<s2_t*>(drow + 64 + d) = a2;
-      }
-    }
-    return;
+  g4w_epilogue<EPI>(args, acc, tm, tn, wr, wc, lane, sp, u);
+}
+
+
+// ---- 4-wave K-step-major kernel (config variant 4) -------------------------------------------
+// The phase kernel above ends every 32-MFMA phase on a workgroup barrier (4 per K-tile) and, with
+// one wave per SIMD, no partner wave covers the barrier.  This loop has hipBLASLt's shape instead:
+// per K-tile two K-steps (K = 32 each) of 64 MFMAs per wave (all 8 x 8 tiles of the wave's
+// 128 x 128 block), with the NEXT K-step's 8 A + 8 B fragments read under the current one (two
+// register sets) and ONE barrier per K-tile:
+//    A(t)  MFMA K-step 0 of tile t  |  read K-step 1 of tile t  (buffer t & 1)
+//          lgkmcnt(0), vmcnt(0), s_barrier     (RAW: tile t+1 landed; WAR: tile t fully read)
+//    B(t)  MFMA K-step 1 of tile t  |  read K-step 0 of tile t+1 (other buffer)  |  DMA tile t+2 -> buffer t & 1
+// Fragment reads go out after the first 16 of 32 two-MFMA statements (done well before the next
+// wait), DMA pieces ride inside the last 16.  Tile t+2's DMA has one K-tile (~128 MFMAs) to land.
+template <bool AT, bool BT, int EPI, int GROUP>
+__global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4k_kernel(G64Args args) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  const int bid = blockIdx.x;
+  int wg, sp = -1, u = 0;
+  if (bid < args.n_main) {
+    const int nwg = args.n_main;
+    const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
+    wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
+  } else {
+    const int i = bid - args.n_main;
+    u = i / args.splits;
+    sp = i - u * args.splits;
+    wg = args.n_main + u;
   }
-  if constexpr (PAIRED_B) {
-    // n-tile j (< 4): gate cols 128 tn + wc * 64 + 16 j + 4 g + r; n-tile j + 4: the same up cols.
-    // EPI_UP_SWIGLU stores gu [T, 2F] and act [T, F]; EPI_SWIGLU_FWD only act (into C, ldc = F)
-    const long F = args.N;
+  const int per_group = GROUP * args.tiles_n;
+  const int grp = wg / per_group;
+  const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
+  const int inner = wg - grp * per_group;
+  const int tm = grp * GROUP + inner % gsz;
+  const int tn = inner / gsz;
+
+  const long lda = args.lda, ldb = args.ldb;
+  const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
+  constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;
+  const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
+                             : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
+  const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
+  const i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
+  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
+  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
+  const int KT = sp < 0 ? args.K / TK : args.kt_part;
+  const unsigned kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
+
+  unsigned vo[4][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const long t = (long)tm * TM + wr * 128 + 16 * i + i16;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = tn * 128 + wc * 64 + 16 * j + 4 * g;
-        float o[4];
-        unsigned short gb[4], ub[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {  // as swiglu_fwd_kernel on the bf16-stored g / u
-          gb[e] = f2bf(acc[i][j][e]);
-          ub[e] = f2bf(acc[i][j + 4][e]);
-          const float gg = bf2f(gb[e]), uu = bf2f(ub[e]);
-          o[e] = gg * (1.f / (1.f + __expf(-gg))) * uu;
-        }
-        s2_t pa;
-        pa[0] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
-        pa[1] = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
-        if constexpr (EPI == EPI_UP_SWIGLU) {
-          s2_t pg, pu;
-          pg[0] = (unsigned)gb[0] | ((unsigned)gb[1] << 16);
-          pg[1] = (unsigned)gb[2] | ((unsigned)gb[3] << 16);
-          pu[0] = (unsigned)ub[0] | ((unsigned)ub[1] << 16);
-          pu[1] = (unsigned)ub[2] | ((unsigned)ub[3] << 16);
-          unsigned short* gurow = args.c + t * args.ldc;
-          *reinterpret_cast<s2_t*>(gurow + col) = pg;
-          *reinterpret_cast<s2_t*>(gurow + F + col) = pu;
-          *reinterpret_cast<s2_t*>(args.out2 + t * F + col) = pa;
-        } else {
-          *reinterpret_cast<s2_t*>(args.c + t * args.ldc + col) = pa;
-        }
-      }
-    }
-    return;
+  for (int i = 0; i < 4; ++i) {
+    vo[A_LO][i] = stage_voff<AT, A_LO, NT4>(i, tid, lda);
+    vo[A_HI][i] = stage_voff<AT, A_HI, NT4>(i, tid, lda);
+    vo[B_H0][i] = stage_voff<BT, B_H0, NT4>(i, tid, ldb);
+    vo[B_H1][i] = stage_voff<BT, B_H1, NT4>(i, tid, ldb);
   }
-  if (sp >= 0) {
-    float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 128 + 4 * g;
+  const unsigned lds0 = lds_addr(smem) + wave * 1024;
+  auto issue = [&](auto kind_c, int t) __attribute__((always_inline)) {
+    constexpr int kind = decltype(kind_c)::value;
+    const unsigned tc = kt0 + (unsigned)(t < KT ? t : KT - 1);
+    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
+    const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
+    const i32x4_t r = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 4; ++i) bdma16(r, vo[kind][i], so, l + i * 4096);
+  };
+
+  f32x4_t acc[8][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + 16 * j) = acc[i][j];
-    return;
-  }
-  if constexpr (epi_f32(EPI)) {
-    float* Cf = reinterpret_cast<float*>(args.c) + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + 4 * g;
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if constexpr (EPI == EPI_ACC_F32) {
-        f32x4_t old[8];
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ap = wr * 64;
+  const int bo03 = PAIRED_B ? B_H0 * HALF : (B_H0 + wc) * HALF, p03 = PAIRED_B ? wc * 64 : 0;
+  const int bo47 = PAIRED_B ? B_H1 * HALF : (B_H0 + wc) * HALF, p47 = PAIRED_B ? wc * 64 : 64;
+  bf16x8_t fa[2][8], fb[2][8];
+  auto frA = [&](int i, int ks, const unsigned char* buf) __attribute__((always_inline)) {
+    return frag<AT>(buf + (i < 4 ? A_LO : A_HI) * HALF, ap + 16 * (i & 3), ks, lane);
+  };
+  auto frB = [&](int j, int ks, const unsigned char* buf) __attribute__((always_inline)) {
+    return j < 4 ? frag<BT>(buf + bo03, p03 + 16 * j, ks, lane) : frag<BT>(buf + bo47, p47 + 16 * (j - 4), ks, lane);
+  };
+  // one K-step: 32 statements of 2 MFMAs on fragment set S; after statement q < 16 the q-th
+  // fragment of the next K-step (A 0-7, then B 0-7) into set S ^ 1; with DMA, piece q - 16
+  // (half-tile kind (q - 16) >> 2) of tile t_dma rides inside statement q >= 16
+  auto kstep = [&](auto s_c, auto dma_c, int nks, const unsigned char* nbuf, int t_dma) __attribute__((always_inline)) {
+    constexpr int S = decltype(s_c)::value;
+    constexpr bool DMA = decltype(dma_c)::value;
+    const unsigned tc = kt0 + (unsigned)(t_dma < KT ? t_dma : KT - 1);
+    const unsigned soA = __builtin_amdgcn_readfirstlane(tc * a_kstep);
+    const unsigned soB = __builtin_amdgcn_readfirstlane(tc * b_kstep);
+    const unsigned l0 = lds0 + (t_dma & 1) * BUF;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j) = old[j] + acc[i][j];
+    for (int q = 0; q < 32; ++q) {
+      const int i = q >> 2, j = (q & 3) * 2;
+      if (DMA && q >= 16) {
+        const int kind = (q - 16) >> 2, pc = (q - 16) & 3;
+        const i32x4_t r = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
+        g4w_pair_dma(acc[i][j], acc[i][j + 1], fa[S][i], fb[S][j], fb[S][j + 1], vo[kind][pc], r,
+                     kind <= A_HI ? soA : soB, l0 + kind * HALF + pc * 4096);
       } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(Cf + (long)(16 * i) * args.ldc + 16 * j) = acc[i][j];
+        g4w_pair(acc[i][j], acc[i][j + 1], fa[S][i], fb[S][j], fb[S][j + 1]);
       }
+      if (q < 8) fa[S ^ 1][q] = frA(q, nks, nbuf);
+      else if (q < 16) fb[S ^ 1][q - 8] = frB(q - 8, nks, nbuf);
     }
-    return;
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 retired, K-step 0 of tile 0 into set 0
+  issue(K_<A_LO>{}, 0);
+  issue(K_<A_HI>{}, 0);
+  issue(K_<B_H0>{}, 0);
+  issue(K_<B_H1>{}, 0);
+  issue(K_<A_LO>{}, 1);
+  issue(K_<A_HI>{}, 1);
+  issue(K_<B_H0>{}, 1);
+  issue(K_<B_H1>{}, 1);
+  wait_vm<16>();
+  bar();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[0][i] = frA(i, 0, smem);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb[0][j] = frB(j, 0, smem);
+
+  auto ktile = [&](int t, auto par_c) __attribute__((always_inline)) {
+    constexpr int P = decltype(par_c)::value;
+    const unsigned char* buf = smem + P * BUF;
+    const unsigned char* nbuf = smem + (P ^ 1) * BUF;
+    kstep(K_<0>{}, std::false_type{}, 1, buf, t);  // K-step 0 of t  |  reads K-step 1 of t
+    wait_vm<0>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) through the builtin (hipcc tracks it)
+    bar();
+    kstep(K_<1>{}, std::true_type{}, 0, nbuf, t + 2);  // K-step 1 of t  |  reads K-step 0 of t+1  |  DMA t+2
+  };
+  for (int t = 0; t < KT; t += 2) {
+    ktile(t, K_<0>{});
+    ktile(t + 1, K_<1>{});
   }
-  unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + 4 * g;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    s2_t old[8];
-    if constexpr (EPI == EPI_ACC) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      f32x4_t v = acc[i][j];
-      if constexpr (EPI == EPI_ACC) {
-        v[0] += bf2f(old[j][0] & 0xffff);
-        v[1] += bf2f(old[j][0] >> 16);
-        v[2] += bf2f(old[j][1] & 0xffff);
-        v[3] += bf2f(old[j][1] >> 16);
-      }
-      s2_t o;
-      o[0] = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-      o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-      *reinterpret_cast<s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j) = o;
-    }
-  }
+  wait_vm<0>();  // the clamped tail items are still landing
+  g4w_fence(acc);
+  g4w_epilogue<EPI>(args, acc, tm, tn, wr, wc, lane, sp, u);
 }
 
 // ---- persistent variant ------------------------------------------------------------------------
@@ -1684,6 +1838,10 @@ void launch_g(const G64Args& g, int variant) {
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
   if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU ||
                 EPI == EPI_SWIGLU_FWD) {
+    if (variant == 4) {  // 4-wave K-step-major kernel: one barrier per K-tile
+      hipLaunchKernelGGL((gemm4k_kernel<AT, BT, EPI, GROUP>), grid, dim3(NT4), 0, stream(), g);
+      variant = -1;
+    }
     if (variant >= 6 && variant <= 9) {  // 4-wave kernel: 128x128 per wave (7-9: loads interleaved)
       if (variant == 9) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 3>), grid, dim3(NT4), 0, stream(), g);
       else if (variant == 8) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 2>), grid, dim3(NT4), 0, stream(), g);
@@ -1808,7 +1966,7 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   const int grp = (int)(config % 1000);
   if (f32_out) {  // fp32 main gradients: the 4-wave, persistent or variant-1 schedule only
     const int v = (grp / 100) % 10;
-    const int c = (v >= 5 ? v * 100 : 100) + grp % 100;
+    const int c = (v >= 4 ? v * 100 : 100) + grp % 100;
     if (accumulate) launch<true, true, EPI_ACC_F32>(g, c);
     else launch<true, true, EPI_STORE_F32>(g, c);
     return;

@@ -645,41 +645,6 @@ def test_decode_linear_add_rmsnorm_fused(native_lib, M, N, K, bias):
     assert _row_err(res_out, s) < 1.5e-2 and _row_err(y, ref_y) < 2e-2
 
 
-@pytest.mark.parametrize("M,nq,nkv,D,K", [(16, 32, 32, 128, 4096), (5, 8, 2, 128, 1024), (3, 8, 2, 64, 512),
-                                          (1, 4, 1, 128, 2048)])
-def test_paged_attention_decode_qkv_fused(native_lib, M, nq, nkv, D, K):
-    """Decode attention that sums the QKV projection's K-chunk partials itself (q RoPE'd in the
-    prologue, the new token's K/V written by the workgroup that reads it) == decode_qkv_rope_cache
-    + paged_attention_decode, bit for bit, incl. split contexts, GQA, a 1-token context and a
-    padded row (slot -1); both caches identical afterwards."""
-    bs, maxb = 16, 20
-    nb = M * maxb  # disjoint blocks per sequence: no sequence reads another one's new token
-    N = (nq + 2 * nkv) * D
-    x = _bf(M, K, seed=201)
-    w = _bf(N, K, scale=0.05, seed=202)
-    cos, sin = ref.rope_tables(1024, D, base=10000.0, device=DEV)
-    kc = _bf(nb, bs, nkv, D, seed=203)
-    vc = _bf(nb, bs, nkv, D, seed=204)
-    g = torch.Generator().manual_seed(5)
-    ctx = [int(v) for v in torch.randint(1, 300, (M,), generator=g)]
-    ctx[0] = 1
-    bt = torch.randperm(nb, generator=g).to(torch.int32).view(M, maxb).to(DEV)
-    pos = torch.tensor([c - 1 for c in ctx], dtype=torch.int32, device=DEV)
-    slots = torch.tensor([int(bt[i, (ctx[i] - 1) // bs]) * bs + (ctx[i] - 1) % bs for i in range(M)], device=DEV)
-    if M > 2:
-        slots[2] = -1
-    ctx_t = torch.tensor(ctx, dtype=torch.int32, device=DEV)
-    kc2, vc2 = kc.clone(), vc.clone()
-    ws = native_lib.decode_linear_partials(x, w)
-    o = native_lib.paged_attention_decode_qkv(ws, None, cos, sin, pos, slots, kc, vc, bt, ctx_t, nq, nkv, D ** -0.5)
-    q = native_lib.decode_qkv_rope_cache(x, w, None, cos, sin, nq, nkv, pos, kc2, vc2, slots)
-    o2 = native_lib.paged_attention_decode(q, kc2, vc2, bt, ctx_t, D ** -0.5)
-    assert o.shape == (M, nq, D)
-    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
-    live = [i for i in range(M) if int(slots[i]) >= 0]
-    assert torch.equal(o[live], o2[live])
-
-
 @pytest.mark.parametrize("M,F,K", [(256, 128, 256), (2048, 11008, 4096), (512, 384, 1152)])
 def test_gemm64_swiglu_fwd(native_lib, M, F, K):
     """Gate/up projection with the SwiGLU in the gemm64 epilogue (gate rows and the matching up
