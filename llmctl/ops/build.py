@@ -91,10 +91,11 @@ def build(arch: str = "gfx950", jobs: int = 0, force: bool = False, save_temps: 
     def _one(so):
         s, o = so
         cmd = [hipcc()] + file_flags(s, flags) + ["-c", str(s), "-o", str(o)]
+        key = _digest(s, file_flags(s, flags))  # before compiling: a source edited mid-build stays stale
         r = subprocess.run(cmd, capture_output=True, text=True, cwd=str(BUILD))
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {s.name}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        o.with_suffix(o.suffix + ".key").write_text(_digest(s, file_flags(s, flags)))
+        o.with_suffix(o.suffix + ".key").write_text(key)
         return s.name
 
     jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))

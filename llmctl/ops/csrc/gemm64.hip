@@ -868,6 +868,16 @@ __device__ __forceinline__ void g4w_pair(f32x4_t& c0, f32x4_t& c1, const bf16x8_
                : "v"(a), "v"(b0), "v"(b1)
                : "memory");
 }
+// the same with C = 0 (an item's first K-slice): the accumulators are defined here, not carried
+// from a zeroing through the item loop's back-edge (persistent kernel)
+__device__ __forceinline__ void g4w_pair_z(f32x4_t& c0, f32x4_t& c1, const bf16x8_t& a, const bf16x8_t& b0,
+                                           const bf16x8_t& b1) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %3, %2, 0\n\t"
+               "v_mfma_f32_16x16x32_bf16 %1, %4, %2, 0"
+               : "=a"(c0), "=a"(c1)
+               : "v"(a), "v"(b0), "v"(b1)
+               : "memory");
+}
 __device__ __forceinline__ void g4w_pair_dma(f32x4_t& c0, f32x4_t& c1, const bf16x8_t& a, const bf16x8_t& b0,
                                              const bf16x8_t& b1, unsigned voff, i32x4_t rsrc, unsigned soff,
                                              unsigned lds_byte) {
@@ -1033,6 +1043,7 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
       o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
       *reinterpret_cast<s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j) = o;
     }
+    __builtin_amdgcn_sched_barrier(0);  // one row's conversions live at a time (no spills)
   }
 }
 
@@ -1354,6 +1365,218 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   g4w_epilogue<EPI>(args, acc, tm, tn, wr, wc, lane, sp, u);
 }
 
+
+
+// ---- persistent 4-wave kernel (config variant 3) ------------------------------------------------
+// At K = 4096 the one-shot kernels run ~8 % below hipBLASLt, at K >= 12288 2-3 % (profiles/
+// gemm4w_r4_b.txt): a fixed per-tile cost -- the pipeline fill (two K-tiles of DMA waited for with
+// nothing to overlap) and the store epilogue.  Here one workgroup per CU walks the work items
+// g = blockIdx.x, + gridDim.x, ... and the half-tile DMA stream does not stop at an item boundary:
+// the stream slots past the last K-tile of item i (the one-shot kernel's clamped re-loads) fetch
+// K-tiles 0 and 1 of item i+1 into the same buffers, in the prologue's order, and the last K-tile's
+// phases P2 / P3 already read item i+1's a_lo / b03 fragments.  Item i+1's loop therefore starts
+// with its operands in registers, and item i's epilogue stores run while item i+1's first K-tiles
+// land.  The waits stay correct (the epilogue's stores are younger than every half-tile a later
+// vmcnt(N) targets, so they only make those waits more conservative).  Variant-9 phase schedule.
+template <bool AT, bool BT, int EPI, int GROUP>
+__global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4wp_kernel(G64Args args,
+                                                                                                  int n_items) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // lane-constant addressing (DMA voffsets, fragment LDS offsets) is recomputed per item from a
+  // laundered thread id: hoisted to kernel entry it stays live across the epilogue, is spilled,
+  // and the reloads' compiler vmcnt(0) would wait for the next item's in-flight DMA
+  int lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;
+  const long lda = args.lda, ldb = args.ldb;
+  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
+  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
+
+  // work-item fields as plain scalars (a struct of them ended up on the stack)
+  auto decode = [&](int bid, int& tm, int& tn, int& sp, int& u, int& KT, unsigned& kt0, i32x4_t& ra, i32x4_t& rb,
+                    i32x4_t& rb_hi) __attribute__((always_inline)) {
+    int wg;
+    sp = -1;
+    u = 0;
+    if (bid < args.n_main) {
+      const int nwg = args.n_main;
+      const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
+      wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
+    } else {
+      const int i = bid - args.n_main;
+      u = i / args.splits;
+      sp = i - u * args.splits;
+      wg = args.n_main + u;
+    }
+    const int per_group = GROUP * args.tiles_n;
+    const int grp = wg / per_group;
+    const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
+    const int inner = wg - grp * per_group;
+    tm = grp * GROUP + inner % gsz;
+    tn = inner / gsz;
+    KT = sp < 0 ? args.K / TK : args.kt_part;
+    kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
+    const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
+    const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
+                               : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
+    ra = make_rsrc(Ab);
+    rb = make_rsrc(Bb);
+    rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
+  };
+
+  unsigned vo[4][4];
+  auto lane_consts = [&]() __attribute__((always_inline)) {
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    lane = t & 63;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      vo[A_LO][i] = stage_voff<AT, A_LO, NT4>(i, t, lda);
+      vo[A_HI][i] = stage_voff<AT, A_HI, NT4>(i, t, lda);
+      vo[B_H0][i] = stage_voff<BT, B_H0, NT4>(i, t, ldb);
+      vo[B_H1][i] = stage_voff<BT, B_H1, NT4>(i, t, ldb);
+    }
+  };
+  lane_consts();
+  const unsigned lds0 = lds_addr(smem) + wave * 1024;
+  const int ap = wr * 64;
+  const int bo03 = PAIRED_B ? B_H0 * HALF : (B_H0 + wc) * HALF, p03 = PAIRED_B ? wc * 64 : 0;
+  const int bo47 = PAIRED_B ? B_H1 * HALF : (B_H0 + wc) * HALF, p47 = PAIRED_B ? wc * 64 : 64;
+
+  int g = blockIdx.x;
+  int c_tm, c_tn, c_sp, c_u, c_KT, n_tm, n_tn, n_sp, n_u, n_KT;
+  unsigned c_kt0, n_kt0;
+  i32x4_t c_ra, c_rb, c_rbh, n_ra, n_rb, n_rbh;
+  decode(g, c_tm, c_tn, c_sp, c_u, c_KT, c_kt0, c_ra, c_rb, c_rbh);
+  bool has_next = g + (int)gridDim.x < n_items;
+  decode(has_next ? g + (int)gridDim.x : g, n_tm, n_tn, n_sp, n_u, n_KT, n_kt0, n_ra, n_rb, n_rbh);
+  // stream slot t of the current item: its K-tile t, else K-tile t - KT of the next item (else the
+  // current item's last K-tile again: a slot nobody reads)
+  auto src = [&](int kind, int t, unsigned& so, i32x4_t& r) __attribute__((always_inline)) {
+    const bool own = t < c_KT || !has_next;
+    const int tt = t < c_KT ? t : has_next ? t - c_KT : c_KT - 1;
+    const unsigned tc = (own ? c_kt0 : n_kt0) + (unsigned)tt;
+    so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
+    if (kind <= A_HI) r = own ? c_ra : n_ra;
+    else if (kind == B_H1) r = own ? c_rbh : n_rbh;
+    else r = own ? c_rb : n_rb;
+  };
+  auto issue = [&](auto kind_c, int t) __attribute__((always_inline)) {
+    constexpr int kind = decltype(kind_c)::value;
+    unsigned so;
+    i32x4_t r;
+    src(kind, t, so, r);
+    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bdma16(r, vo[kind][i], so, l + i * 4096);
+  };
+
+  f32x4_t acc[8][8];
+  bf16x8_t a_lo[4][2], a_hi[4][2], b47[4][2], b03[2][4][2];
+  auto sync = [&](auto n_c) __attribute__((always_inline)) {
+    constexpr int N = decltype(n_c)::value;
+    if constexpr (N >= 0) wait_vm<N>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    bar();
+  };
+  auto il_phase = [&](auto m0_c, auto n0_c, const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2], auto rd_b_c,
+                      bf16x8_t (&dst)[4][2], const unsigned char* img, int p0, auto kind_c, int t, auto zero_c)
+                      __attribute__((always_inline)) {
+    constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
+    constexpr bool ZERO = decltype(zero_c)::value;
+    constexpr bool RDB = decltype(rd_b_c)::value;
+    constexpr int kind = decltype(kind_c)::value;
+    unsigned so;
+    i32x4_t rr;
+    src(kind, t, so, rr);
+    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ks = q >> 3, i = (q >> 1) & 3, j = (q & 1) * 2;
+      if (q >= 8 && (q & 1)) {
+        const int pc = (q - 9) >> 1;
+        g4w_pair_dma(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks], vo[kind][pc],
+                     rr, so, l + pc * 4096);
+      } else if (ZERO && q < 8) {
+        g4w_pair_z(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks]);
+      } else {
+        g4w_pair(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks]);
+      }
+      if (q < 8) {
+        const int f = q >> 1, fk = q & 1;
+        if constexpr (RDB) dst[f][fk] = frag<BT>(img, p0 + 16 * f, fk, lane);
+        else dst[f][fk] = frag<AT>(img, p0 + 16 * f, fk, lane);
+      }
+    }
+  };
+  auto ktile = [&](int t, auto par_c, auto zero_c) __attribute__((always_inline)) {
+    constexpr int P = decltype(par_c)::value;
+    const unsigned char* buf = smem + P * BUF;
+    const unsigned char* nbuf = smem + (P ^ 1) * BUF;
+    il_phase(K_<0>{}, K_<0>{}, a_lo, b03[P], std::true_type{}, b47, buf + bo47, p47, K_<A_LO>{}, t + 2, zero_c);
+    sync(K_<20>{});
+    il_phase(K_<0>{}, K_<4>{}, a_lo, b47, std::false_type{}, a_hi, buf + A_HI * HALF, ap, K_<B_H0>{}, t + 2, zero_c);
+    sync(K_<20>{});
+    il_phase(K_<4>{}, K_<4>{}, a_hi, b47, std::false_type{}, a_lo, nbuf + A_LO * HALF, ap, K_<B_H1>{}, t + 2, zero_c);
+    sync(K_<16>{});
+    il_phase(K_<4>{}, K_<0>{}, a_hi, b03[P], std::true_type{}, b03[P ^ 1], nbuf + bo03, p03, K_<A_HI>{}, t + 2,
+             zero_c);
+    sync(K_<-1>{});
+  };
+
+  // K-step 0 fragments of an item's K-tile 0 (buffer 0): a_lo / b03[0]; then lgkmcnt(0) + barrier
+  // (WAR: the first phase restages this buffer's A_lo)
+  auto first_frags = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = frag<AT>(smem + A_LO * HALF, ap + 16 * i, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b03[0][j][ks] = frag<BT>(smem + bo03, p03 + 16 * j, ks, lane);
+    sync(K_<-1>{});
+  };
+  // prologue (first item only): K-tiles 0 and 1 in flight; retire A_lo(0) / B(0)
+  issue(K_<A_LO>{}, 0);
+  issue(K_<B_H0>{}, 0);
+  issue(K_<B_H1>{}, 0);
+  issue(K_<A_HI>{}, 0);
+  issue(K_<A_LO>{}, 1);
+  issue(K_<B_H0>{}, 1);
+  issue(K_<B_H1>{}, 1);
+  issue(K_<A_HI>{}, 1);
+  wait_vm<20>();
+  bar();
+
+  while (true) {
+    lane_consts();
+    // the item's K-tile 0 is in buffer 0 (the prologue's, or the previous item's stream tail behind
+    // its last waits and barrier): its first fragments are read here, so no fragment is carried
+    // through the loop's back-edge (nor live across the epilogue)
+    first_frags();
+    // K-tile 0 starts every accumulator from C = 0 (KT >= 2, even)
+    ktile(0, K_<0>{}, std::true_type{});
+    ktile(1, K_<1>{}, std::false_type{});
+    for (int t = 2; t < c_KT; t += 2) {
+      ktile(t, K_<0>{}, std::false_type{});
+      ktile(t + 1, K_<1>{}, std::false_type{});
+    }
+    g4w_fence(acc);
+    if (!has_next) wait_vm<0>();  // the clamped tail items are still landing
+    // one epilogue call site: two copies had the accumulators copied out (and spilled) ahead of
+    // the branch between them
+    g4w_epilogue<EPI>(args, acc, c_tm, c_tn, wr, wc, lane, c_sp, c_u);
+    if (!has_next) break;
+    g += (int)gridDim.x;
+    c_tm = n_tm, c_tn = n_tn, c_sp = n_sp, c_u = n_u, c_KT = n_KT, c_kt0 = n_kt0;
+    c_ra = n_ra, c_rb = n_rb, c_rbh = n_rbh;
+    has_next = g + (int)gridDim.x < n_items;
+    if (has_next) decode(g + (int)gridDim.x, n_tm, n_tn, n_sp, n_u, n_KT, n_kt0, n_ra, n_rb, n_rbh);
+  }
+}
 
 // ---- 4-wave K-step-major kernel (config variant 4) -------------------------------------------
 // The phase kernel above ends every 32-MFMA phase on a workgroup barrier (4 per K-tile) and, with
@@ -1838,6 +2061,12 @@ void launch_g(const G64Args& g, int variant) {
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
   if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU ||
                 EPI == EPI_SWIGLU_FWD) {
+    if (variant == 3 && (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV ||
+                         EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD)) {  // persistent 4-wave kernel
+      const dim3 pgrid(min(n_items, num_cus()));
+      hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP>), pgrid, dim3(NT4), 0, stream(), g, n_items);
+      variant = -1;
+    }
     if (variant == 4) {  // 4-wave K-step-major kernel: one barrier per K-tile
       hipLaunchKernelGGL((gemm4k_kernel<AT, BT, EPI, GROUP>), grid, dim3(NT4), 0, stream(), g);
       variant = -1;
@@ -1966,7 +2195,7 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   const int grp = (int)(config % 1000);
   if (f32_out) {  // fp32 main gradients: the 4-wave, persistent or variant-1 schedule only
     const int v = (grp / 100) % 10;
-    const int c = (v >= 4 ? v * 100 : 100) + grp % 100;
+    const int c = (v >= 3 ? v * 100 : 100) + grp % 100;
     if (accumulate) launch<true, true, EPI_ACC_F32>(g, c);
     else launch<true, true, EPI_STORE_F32>(g, c);
     return;
