@@ -119,6 +119,12 @@ struct G64Args {
   unsigned short* s_dgu = nullptr;
   unsigned s_E = 0;
   int s_F = 0;
+  // bottleneck probes (one-shot 4-wave kernel only; results are garbage): 1 = operand loads out of
+  // range (no memory traffic), 2 = no workgroup barriers, 4 = no epilogue
+  int probe = 0;
+  // persistent kernel: retire an item's epilogue stores before the next item's first DMA (the
+  // undrained form measured intermittent wrong rows; native knob gemm_p3_drain)
+  int p3_drain = 1;
 };
 
 // SwiGLU backward of one element: d = dL/dact, act = silu(g) * u
@@ -1021,27 +1027,49 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
     }
     return;
   }
-  unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + 4 * g;
+  // bf16: 16-byte stores.  v_permlane16_swap pairs n-tiles j, j + 1 (j even): lane row-group g
+  // then holds 8 consecutive columns 16 (j + (g & 1)) + 8 (g >> 1) + [0, 8) of its row, so a
+  // row's 4 lanes write 64 contiguous bytes per instruction and a thread issues 32 stores (not 64
+  // of 8 bytes) -- half the vector-memory operations the persistent kernel's counted waits after an
+  // epilogue must allow for
+  const int cs = 16 * (g & 1) + 8 * (g >> 1);
+  unsigned short* Cb = args.c + (long)(tm * TM + wr * 128 + i16) * args.ldc + tn * TN + wc * 128 + cs;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    s2_t old[8];
+    uint4 old[4];
     if constexpr (EPI == EPI_ACC) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j);
+      for (int jp = 0; jp < 4; ++jp) old[jp] = *reinterpret_cast<const uint4*>(Cb + (long)(16 * i) * args.ldc + 32 * jp);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      f32x4_t v = acc[i][j];
+    for (int jp = 0; jp < 4; ++jp) {
+      const int j = 2 * jp;
+      uint4 o;
       if constexpr (EPI == EPI_ACC) {
-        v[0] += bf2f(old[j][0] & 0xffff);
-        v[1] += bf2f(old[j][0] >> 16);
-        v[2] += bf2f(old[j][1] & 0xffff);
-        v[3] += bf2f(old[j][1] >> 16);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][e]), __float_as_uint(acc[i][j + 1][e]),
+                                                          false, false);
+          v[e] = __uint_as_float(r[0]);
+          v[4 + e] = __uint_as_float(r[1]);
+        }
+        const unsigned ow[4] = {old[jp].x, old[jp].y, old[jp].z, old[jp].w};
+        unsigned pk[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          pk[e] = (unsigned)f2bf(v[2 * e] + bf2f(ow[e] & 0xffff)) | ((unsigned)f2bf(v[2 * e + 1] + bf2f(ow[e] >> 16)) << 16);
+        o = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      } else {
+        const unsigned x0 = (unsigned)f2bf(acc[i][j][0]) | ((unsigned)f2bf(acc[i][j][1]) << 16);
+        const unsigned x1 = (unsigned)f2bf(acc[i][j][2]) | ((unsigned)f2bf(acc[i][j][3]) << 16);
+        const unsigned y0 = (unsigned)f2bf(acc[i][j + 1][0]) | ((unsigned)f2bf(acc[i][j + 1][1]) << 16);
+        const unsigned y1 = (unsigned)f2bf(acc[i][j + 1][2]) | ((unsigned)f2bf(acc[i][j + 1][3]) << 16);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        o = make_uint4(r0[0], r1[0], r0[1], r1[1]);
       }
-      s2_t o;
-      o[0] = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-      o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-      *reinterpret_cast<s2_t*>(Cb + (long)(16 * i) * args.ldc + 16 * j) = o;
+      *reinterpret_cast<uint4*>(Cb + (long)(16 * i) * args.ldc + 32 * jp) = o;
     }
     __builtin_amdgcn_sched_barrier(0);  // one row's conversions live at a time (no spills)
   }
@@ -1088,9 +1116,10 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;  // gate + up rows per tile
   const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
                              : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
-  const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
+  i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
   // paired: B_H1 image rows 128 + ip -> up row N + 128 tn + ip (N = F)
-  const i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
+  i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
+  if (args.probe & 1) ra[2] = rb[2] = rb_hi[2] = 0;
   const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
   const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
   const int KT = sp < 0 ? args.K / TK : args.kt_part;
@@ -1217,7 +1246,7 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     constexpr int N = decltype(n_c)::value;
     if constexpr (N >= 0) wait_vm<N>();
     __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
-    bar();
+    if (!(args.probe & 2)) bar();
   };
 
   // interleaved phase (IL): 8 row blocks of 4 MFMAs (K-slice ks = r >> 2, row i = r & 3); after
@@ -1361,7 +1390,7 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // the last phase's MFMA results -> the epilogue's accumulator reads: 16 wait states (every
   // other accumulator was last written >= 32 MFMAs earlier)
   g4w_fence(acc);
-
+  if (args.probe & 4) return;
   g4w_epilogue<EPI>(args, acc, tm, tn, wr, wc, lane, sp, u);
 }
 
@@ -1376,8 +1405,14 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 // K-tiles 0 and 1 of item i+1 into the same buffers, in the prologue's order, and the last K-tile's
 // phases P2 / P3 already read item i+1's a_lo / b03 fragments.  Item i+1's loop therefore starts
 // with its operands in registers, and item i's epilogue stores run while item i+1's first K-tiles
-// land.  The waits stay correct (the epilogue's stores are younger than every half-tile a later
-// vmcnt(N) targets, so they only make those waits more conservative).  Variant-9 phase schedule.
+// land.  vmcnt counts the stores too, but they complete out of order with the LDS-DMA loads, so a
+// wait may count only younger LOADS: the next item's first waits therefore also wait for the
+// epilogue's stores (16-byte stores halve them).  The last two K-tiles are peeled: only there do
+// the DMA sources belong to the next item, so its fields are decoded there and the current item's
+// buffer descriptors are dead -- holding both sets through the loop spilled SGPRs to VGPR lanes,
+// and a v_readlane reload (a VALU write of an SGPR) right before the inline-asm buffer_load that
+// reads it is the unpadded VALU-SGPR -> VMEM hazard (intermittent wrong rows).  K >= 256.
+// Variant-9 phase schedule.
 template <bool AT, bool BT, int EPI, int GROUP>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4wp_kernel(G64Args args,
                                                                                                   int n_items) {
@@ -1450,24 +1485,22 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   unsigned c_kt0, n_kt0;
   i32x4_t c_ra, c_rb, c_rbh, n_ra, n_rb, n_rbh;
   decode(g, c_tm, c_tn, c_sp, c_u, c_KT, c_kt0, c_ra, c_rb, c_rbh);
-  bool has_next = g + (int)gridDim.x < n_items;
-  decode(has_next ? g + (int)gridDim.x : g, n_tm, n_tn, n_sp, n_u, n_KT, n_kt0, n_ra, n_rb, n_rbh);
-  // stream slot t of the current item: its K-tile t, else K-tile t - KT of the next item (else the
-  // current item's last K-tile again: a slot nobody reads)
-  auto src = [&](int kind, int t, unsigned& so, i32x4_t& r) __attribute__((always_inline)) {
-    const bool own = t < c_KT || !has_next;
-    const int tt = t < c_KT ? t : has_next ? t - c_KT : c_KT - 1;
-    const unsigned tc = (own ? c_kt0 : n_kt0) + (unsigned)tt;
-    so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
-    if (kind <= A_HI) r = own ? c_ra : n_ra;
-    else if (kind == B_H1) r = own ? c_rbh : n_rbh;
-    else r = own ? c_rb : n_rb;
+  // DMA source of stream slot t: the current item's K-tile t, or (NEXT: an item's last two K-tiles)
+  // K-tile t - KT of the next item -- the current item's again after the last item (loads nobody
+  // reads, drained before its epilogue)
+  auto src = [&](auto next_c, int kind, int t, unsigned& so, i32x4_t& r) __attribute__((always_inline)) {
+    constexpr bool NEXT = decltype(next_c)::value;
+    const unsigned tc = NEXT ? n_kt0 + (unsigned)(t - c_KT) : c_kt0 + (unsigned)t;
+    so = tc * (kind <= A_HI ? a_kstep : b_kstep);
+    if (kind <= A_HI) r = NEXT ? n_ra : c_ra;
+    else if (kind == B_H1) r = NEXT ? n_rbh : c_rbh;
+    else r = NEXT ? n_rb : c_rb;
   };
   auto issue = [&](auto kind_c, int t) __attribute__((always_inline)) {
     constexpr int kind = decltype(kind_c)::value;
     unsigned so;
     i32x4_t r;
-    src(kind, t, so, r);
+    src(std::false_type{}, kind, t, so, r);
     const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
 #pragma unroll
     for (int i = 0; i < 4; ++i) bdma16(r, vo[kind][i], so, l + i * 4096);
@@ -1482,15 +1515,15 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     bar();
   };
   auto il_phase = [&](auto m0_c, auto n0_c, const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2], auto rd_b_c,
-                      bf16x8_t (&dst)[4][2], const unsigned char* img, int p0, auto kind_c, int t, auto zero_c)
-                      __attribute__((always_inline)) {
+                      bf16x8_t (&dst)[4][2], const unsigned char* img, int p0, auto kind_c, int t, auto zero_c,
+                      auto next_c) __attribute__((always_inline)) {
     constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
     constexpr bool ZERO = decltype(zero_c)::value;
     constexpr bool RDB = decltype(rd_b_c)::value;
     constexpr int kind = decltype(kind_c)::value;
     unsigned so;
     i32x4_t rr;
-    src(kind, t, so, rr);
+    src(next_c, kind, t, so, rr);
     const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -1511,18 +1544,20 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       }
     }
   };
-  auto ktile = [&](int t, auto par_c, auto zero_c) __attribute__((always_inline)) {
+  auto ktile = [&](int t, auto par_c, auto zero_c, auto next_c) __attribute__((always_inline)) {
     constexpr int P = decltype(par_c)::value;
     const unsigned char* buf = smem + P * BUF;
     const unsigned char* nbuf = smem + (P ^ 1) * BUF;
-    il_phase(K_<0>{}, K_<0>{}, a_lo, b03[P], std::true_type{}, b47, buf + bo47, p47, K_<A_LO>{}, t + 2, zero_c);
+    il_phase(K_<0>{}, K_<0>{}, a_lo, b03[P], std::true_type{}, b47, buf + bo47, p47, K_<A_LO>{}, t + 2, zero_c, next_c);
     sync(K_<20>{});
-    il_phase(K_<0>{}, K_<4>{}, a_lo, b47, std::false_type{}, a_hi, buf + A_HI * HALF, ap, K_<B_H0>{}, t + 2, zero_c);
+    il_phase(K_<0>{}, K_<4>{}, a_lo, b47, std::false_type{}, a_hi, buf + A_HI * HALF, ap, K_<B_H0>{}, t + 2, zero_c,
+             next_c);
     sync(K_<20>{});
-    il_phase(K_<4>{}, K_<4>{}, a_hi, b47, std::false_type{}, a_lo, nbuf + A_LO * HALF, ap, K_<B_H1>{}, t + 2, zero_c);
+    il_phase(K_<4>{}, K_<4>{}, a_hi, b47, std::false_type{}, a_lo, nbuf + A_LO * HALF, ap, K_<B_H1>{}, t + 2, zero_c,
+             next_c);
     sync(K_<16>{});
     il_phase(K_<4>{}, K_<0>{}, a_hi, b03[P], std::true_type{}, b03[P ^ 1], nbuf + bo03, p03, K_<A_HI>{}, t + 2,
-             zero_c);
+             zero_c, next_c);
     sync(K_<-1>{});
   };
 
@@ -1557,24 +1592,25 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     // its last waits and barrier): its first fragments are read here, so no fragment is carried
     // through the loop's back-edge (nor live across the epilogue)
     first_frags();
-    // K-tile 0 starts every accumulator from C = 0 (KT >= 2, even)
-    ktile(0, K_<0>{}, std::true_type{});
-    ktile(1, K_<1>{}, std::false_type{});
-    for (int t = 2; t < c_KT; t += 2) {
-      ktile(t, K_<0>{}, std::false_type{});
-      ktile(t + 1, K_<1>{}, std::false_type{});
+    // K-tile 0 starts every accumulator from C = 0 (KT >= 4, even)
+    ktile(0, K_<0>{}, std::true_type{}, std::false_type{});
+    ktile(1, K_<1>{}, std::false_type{}, std::false_type{});
+    for (int t = 2; t < c_KT - 2; t += 2) {
+      ktile(t, K_<0>{}, std::false_type{}, std::false_type{});
+      ktile(t + 1, K_<1>{}, std::false_type{}, std::false_type{});
     }
+    const bool has_next = g + (int)gridDim.x < n_items;
+    decode(has_next ? g + (int)gridDim.x : g, n_tm, n_tn, n_sp, n_u, n_KT, n_kt0, n_ra, n_rb, n_rbh);
+    ktile(c_KT - 2, K_<0>{}, std::false_type{}, std::true_type{});
+    ktile(c_KT - 1, K_<1>{}, std::false_type{}, std::true_type{});
     g4w_fence(acc);
-    if (!has_next) wait_vm<0>();  // the clamped tail items are still landing
-    // one epilogue call site: two copies had the accumulators copied out (and spilled) ahead of
-    // the branch between them
+    if (!has_next) wait_vm<0>();  // the re-loads of the last item's K-tiles 0 / 1 are still landing
     g4w_epilogue<EPI>(args, acc, c_tm, c_tn, wr, wc, lane, c_sp, c_u);
     if (!has_next) break;
+    if (args.p3_drain) wait_vm<0>();
     g += (int)gridDim.x;
     c_tm = n_tm, c_tn = n_tn, c_sp = n_sp, c_u = n_u, c_KT = n_KT, c_kt0 = n_kt0;
     c_ra = n_ra, c_rb = n_rb, c_rbh = n_rbh;
-    has_next = g + (int)gridDim.x < n_items;
-    if (has_next) decode(g + (int)gridDim.x, n_tm, n_tn, n_sp, n_u, n_KT, n_kt0, n_ra, n_rb, n_rbh);
   }
 }
 
@@ -2061,6 +2097,7 @@ void launch_g(const G64Args& g, int variant) {
   constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
   if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU ||
                 EPI == EPI_SWIGLU_FWD) {
+    if (variant == 3 && g.K < 4 * TK) variant = 9;  // the persistent kernel peels two K-tiles per item
     if (variant == 3 && (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV ||
                          EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD)) {  // persistent 4-wave kernel
       const dim3 pgrid(min(n_items, num_cus()));
@@ -2186,6 +2223,8 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
   G64Args g{reinterpret_cast<const unsigned short*>(a.data_ptr()), reinterpret_cast<const unsigned short*>(b.data_ptr()),
             reinterpret_cast<unsigned short*>(out.data_ptr()), a.stride(0), b.stride(0), out.stride(0),
             (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr, nullptr};
+  g.probe = (int)knob("gemm_probe", 0);
+  g.p3_drain = (int)knob("gemm_p3_drain", 1);
   plan_split(g, (int)(config / 1000));
   at::Tensor ws;
   if (g.splits > 1) {

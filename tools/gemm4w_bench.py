@@ -37,10 +37,14 @@ def main():
     ap.add_argument("--configs", type=int, nargs="+", default=[104, 604])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--layouts", nargs="+", default=["fwd", "dgrad", "wgrad"])
+    ap.add_argument("--knob", action="append", default=[], help="native knob name=value (repeatable)")
     a = ap.parse_args()
     assert _lib.load(), _lib._error
     print("tuned hipBLASLt solutions:", enable_tuned_gemms(), flush=True)
     ops = torch.ops.llmctl
+    for kv in a.knob:
+        k, v = kv.split("=")
+        ops.set_knob(k, int(v))
     T = a.tokens
     for name in a.shapes:
         out, inn = SHAPES[name]

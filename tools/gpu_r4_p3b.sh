@@ -1,0 +1,13 @@
+#!/bin/bash
+# gpurun: 16-byte epilogue stores + persistent waits: gemm64 / fused-forward tests, then the
+# training-shape bench (904 / 304 / hipBLASLt) and the probes
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONPATH=$PWD
+timeout -k 10 500 python -u -m pytest tests/kernels/test_gemm64.py tests/kernels/test_fused_fwd.py -x -q \
+  --timeout 120 --timeout-method thread > gpurun_out/p3_test.log 2>&1 || { tail -40 gpurun_out/p3_test.log; exit 1; }
+tail -2 gpurun_out/p3_test.log
+timeout -k 10 300 python -u tools/gemm4w_bench.py --configs 904 304 > gpurun_out/p3_bench.log 2>&1 || { tail -20 gpurun_out/p3_bench.log; exit 1; }
+cat gpurun_out/p3_bench.log
+timeout -k 10 300 python -u tools/gemm_probe.py --config 904 > gpurun_out/probe.log 2>&1 || { tail -20 gpurun_out/probe.log; exit 1; }
+cat gpurun_out/probe.log
