@@ -35,15 +35,22 @@ import torch.nn.functional as F
 from llmctl.config.knobs import knobs
 
 
-# gemm64_ex config: knob gemm64_config (default: tile-order group 4, schedule variant 1 — the
-# fastest 8-wave schedule of profiles/gemm64_variants_r2.jsonl).  A tuning cache
+# gemm64_ex config: knobs gemm64_config / gemm64_fd_config (see gemm64_config below).  A tuning cache
 # (llmctl.plugins.tuning_cache) can override it per layout or per exact shape.
 GEMM64_CONFIGS: dict = {}  # layout -> config
 GEMM64_SHAPE_CONFIGS: dict = {}  # (layout, M, N, K) -> config
 
 
 def gemm64_config(layout: str, M: int, N: int, K: int) -> int:
-    return GEMM64_SHAPE_CONFIGS.get((layout, M, N, K), GEMM64_CONFIGS.get(layout, knobs().gemm64_config))
+    """Config of one gemm64 call: a tuning-cache entry for the exact shape or the layout, else
+    knob ``gemm64_fd_config`` (forward / data gradient: the persistent 4-wave kernel, 304) or
+    ``gemm64_config`` (weight gradients: the one-shot 4-wave kernel, 904, which also carries the
+    SwiGLU backward as a side job)."""
+    c = GEMM64_SHAPE_CONFIGS.get((layout, M, N, K), GEMM64_CONFIGS.get(layout))
+    if c is not None:
+        return c
+    k = knobs()
+    return k.gemm64_fd_config if layout in ("fwd", "dgrad") and k.gemm64_fd_config else k.gemm64_config
 
 
 def _gemm64_enabled() -> bool:
