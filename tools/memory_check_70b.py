@@ -49,8 +49,10 @@ def measure(model, layers, mb, seq, ac):
     eng.train_step([data.batch(1)])
     torch.cuda.synchronize()
     peak = torch.cuda.max_memory_allocated()
+    wt = sum(getattr(p, "_llmctl_wt").numel() * 2 for p in eng.model.parameters()
+             if getattr(p, "_llmctl_wt", None) is not None)
     res = {"layers": layers, "state_gb": round(state / GiB, 2), "peak_gb": round(peak / GiB, 2),
-           "params": sum(p.numel() for p in eng.model.parameters())}
+           "weight_t_gb": round(wt / GiB, 2), "params": sum(p.numel() for p in eng.model.parameters())}
     eng.shutdown()
     del eng
     torch.cuda.empty_cache()
@@ -67,17 +69,32 @@ def main():
     ap.add_argument("--pp", type=int, default=4)
     ap.add_argument("--dp", type=int, default=2)
     ap.add_argument("--microbatches", type=int, default=8)
+    ap.add_argument("--one", type=int, default=0, help=argparse.SUPPRESS)
     a = ap.parse_args()
+    if a.one:  # child: one slice, one JSON line
+        r, _ = measure(a.model, a.one, a.micro_batch, a.seq_len, a.ac)
+        print("SLICE " + json.dumps(r), flush=True)
+        return
+    import subprocess
+
     rows = []
     for L in a.layers:
-        r, mc = measure(a.model, L, a.micro_batch, a.seq_len, a.ac)
+        # every slice in a fresh process: a second engine in the same process found ~15 GB of the
+        # first still allocated
+        cp = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", str(L), "--model", a.model,
+                             "--micro-batch", str(a.micro_batch), "--seq-len", str(a.seq_len), "--ac", a.ac],
+                            capture_output=True, text=True, check=True)
+        r = json.loads([ln for ln in cp.stdout.splitlines() if ln.startswith("SLICE ")][-1][6:])
         print(json.dumps(r), flush=True)
         rows.append(r)
     (r0, r1) = rows
     dl = r1["layers"] - r0["layers"]
-    state_layer = (r1["state_gb"] - r0["state_gb"]) / dl
+    # the slices (ZeRO-0, one rank) keep W^T copies for the data gradients (the grad-sink path);
+    # ZeRO-3 installs no grad sink, so the projection leaves them out
+    wt_layer = (r1["weight_t_gb"] - r0["weight_t_gb"]) / dl
+    state_layer = (r1["state_gb"] - r0["state_gb"]) / dl - wt_layer
     act_layer = ((r1["peak_gb"] - r1["state_gb"]) - (r0["peak_gb"] - r0["state_gb"])) / dl
-    edge_state = r0["state_gb"] - state_layer * r0["layers"]
+    edge_state = r0["state_gb"] - r0["weight_t_gb"] - state_layer * r0["layers"]
     edge_act = (r0["peak_gb"] - r0["state_gb"]) - act_layer * r0["layers"]
     from llmctl.models import get_model_config
     from llmctl.partition.planner import ParallelismPlanner
@@ -96,6 +113,7 @@ def main():
                                              num_microbatches=a.microbatches)
     print(json.dumps({"model": full.name, "layout": f"pp{a.pp}-dp{a.dp}-zero3", "micro_batch": a.micro_batch,
                       "seq_len": a.seq_len, "ac": a.ac, "state_gb_per_layer": round(state_layer, 3),
+                      "weight_t_gb_per_layer_zero0": round(wt_layer, 3),
                       "act_gb_per_layer_per_microbatch": round(act_layer, 3), "edge_state_gb": round(edge_state, 2),
                       "edge_act_gb": round(edge_act, 2), "stage0_gb_from_slice": round(stage0, 1),
                       "last_stage_gb_from_slice": round(stage_last, 1), "planner_gb": round(est, 1)}), flush=True)
