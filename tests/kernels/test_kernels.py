@@ -585,7 +585,8 @@ def test_rope_flash_attention_fused_backward(native_lib, B, S, nq, nkv, D, with_
 @pytest.mark.parametrize("M,K,bias", [(1, 4096, False), (5, 2048, True), (16, 4096, False), (16, 1024, True)])
 def test_decode_qkv_rope_cache_fused(native_lib, M, K, bias):
     """QKV projection + RoPE + paged-cache write in the GEMM's finalize pass == the unfused
-    v2 GEMM (config 23) followed by rope_qkv_cache_fwd, bit for bit (q and both caches)."""
+    decode GEMM (config 25: the same streaming / chunked product) followed by rope_qkv_cache_fwd
+    (q / k within one bf16 ulp, v bit for bit)."""
     nq, nkv, D, bs, nb = 8, 2, 128, 16, 8
     N = (nq + 2 * nkv) * D
     x = _bf(M, K, seed=91)
@@ -599,11 +600,16 @@ def test_decode_qkv_rope_cache_fused(native_lib, M, K, bias):
     kc = torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV)
     vc = torch.zeros_like(kc)
     q = native_lib.decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, pos, kc, vc, slots)
-    qkv = native_lib.skinny_linear_cfg(x, w, b, 23)
+    qkv = native_lib.skinny_linear_cfg(x, w, b, 25)
     kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(kc)
     q2, _, _ = native_lib.rope_qkv_cache_fwd(qkv, cos, sin, nq, nkv, 256, pos, kc2, vc2, slots)
     assert q.shape == (M, nq, D)
-    assert torch.equal(q, q2) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    # the projection is bit-identical; the two RoPE kernels may contract a*cos - b*sin differently
+    # (measured: one element in 12k off by one ulp), so q / k within one bf16 ulp, v exact
+    for got, want in ((q, q2), (kc, kc2)):
+        ulp = (want.float().abs() * 2.0 ** -7).clamp_min(2.0 ** -133)
+        assert ((got.float() - want.float()).abs() <= ulp).all()
+    assert torch.equal(vc, vc2)
     # and against the fp32 oracle of the whole chain
     qr, kr, vr = ref.rope_qkv_fwd((x.float() @ w.float().t() + (b.float() if bias else 0.0)), cos, sin, nq, nkv,
                                   256, pos)
@@ -617,7 +623,7 @@ def test_decode_up_swiglu_fused(native_lib, M, F, K, bias):
     w = _bf(2 * F, K, scale=0.05, seed=95)
     b = _bf(2 * F, seed=96) if bias else None
     act = native_lib.decode_up_swiglu(x, w, b)
-    act2 = native_lib.swiglu_fwd(native_lib.skinny_linear_cfg(x, w, b, 23))
+    act2 = native_lib.swiglu_fwd(native_lib.skinny_linear_cfg(x, w, b, 25))
     assert act.shape == (M, F) and torch.equal(act, act2)
     gu = x.float() @ w.float().t() + (b.float() if bias else 0.0)
     ref_act = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
@@ -636,7 +642,7 @@ def test_decode_linear_add_rmsnorm_fused(native_lib, M, N, K, bias):
     res = _bf(M, N, seed=100)
     nw = (1.0 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
     y, res_out = native_lib.decode_linear_add_rmsnorm(x, w, b, res, nw, 1e-5)
-    y2, res2, _ = native_lib.add_rmsnorm_fwd(native_lib.skinny_linear_cfg(x, w, b, 23), res, nw, 1e-5)
+    y2, res2, _ = native_lib.add_rmsnorm_fwd(native_lib.skinny_linear_cfg(x, w, b, 25), res, nw, 1e-5)
     assert torch.equal(res_out, res2)
     ulp = (y2.float().abs() * 2.0 ** -7).clamp_min(1e-30)
     assert ((y.float() - y2.float()).abs() <= ulp).all()
