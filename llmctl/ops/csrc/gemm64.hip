@@ -120,7 +120,8 @@ struct G64Args {
   unsigned s_E = 0;
   int s_F = 0;
   // bottleneck probes (one-shot 4-wave kernel only; results are garbage): 1 = operand loads out of
-  // range (no memory traffic), 2 = no workgroup barriers, 4 = no epilogue
+  // range (no memory traffic), 2 = no workgroup barriers, 4 = no epilogue, 8 = every tile loads
+  // tile (0, 0)'s operands (L2-resident), 16 = every K-tile loads K-tile 0
   int probe = 0;
   // persistent kernel: retire an item's epilogue stores before the next item's first DMA (the
   // undrained form measured intermittent wrong rows; native knob gemm_p3_drain)
@@ -1112,16 +1113,18 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const int tn = inner / gsz;
 
   const long lda = args.lda, ldb = args.ldb;
-  const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
+  const int tml = (args.probe & 8) ? 0 : tm, tnl = (args.probe & 8) ? 0 : tn;  // probe 8: one tile's operands
+  const unsigned short* Ab = AT ? args.a + (long)tml * TM : args.a + (long)tml * TM * lda;
   constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;  // gate + up rows per tile
-  const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
-                             : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
+  const unsigned short* Bb = PAIRED_B ? args.b + (long)tnl * (TN / 2) * ldb
+                             : BT ? args.b + (long)tnl * TN : args.b + (long)tnl * TN * ldb;
   i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
   // paired: B_H1 image rows 128 + ip -> up row N + 128 tn + ip (N = F)
-  i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
+  i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tnl * (TN / 2) - TN / 2) * ldb) : rb;
   if (args.probe & 1) ra[2] = rb[2] = rb_hi[2] = 0;
-  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
-  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
+  // probe 16: every K-tile re-reads K-tile 0 (a 64 KB working set per tile: L2-hit latency only)
+  const unsigned a_kstep = (args.probe & 16) ? 0u : AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
+  const unsigned b_kstep = (args.probe & 16) ? 0u : BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
   const int KT = sp < 0 ? args.K / TK : args.kt_part;
   const unsigned kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
 

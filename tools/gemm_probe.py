@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--config", type=int, default=904)
     ap.add_argument("--shapes", nargs="+", default=["up", "o"])
     ap.add_argument("--probes", type=int, nargs="+", default=[0, 1, 2, 4, 3, 5, 6, 7])
+    # 8: one tile's operands for every tile (L2-resident), 16: K-tile 0 for every K-tile
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     assert _lib.load(), _lib._error
