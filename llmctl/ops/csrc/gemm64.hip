@@ -1122,6 +1122,8 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // paired: B_H1 image rows 128 + ip -> up row N + 128 tn + ip (N = F)
   i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tnl * (TN / 2) - TN / 2) * ldb) : rb;
   if (args.probe & 1) ra[2] = rb[2] = rb_hi[2] = 0;
+  if (args.probe & 32) ra[2] = 0;            // probe 32: A loads out of range only
+  if (args.probe & 64) rb[2] = rb_hi[2] = 0;  // probe 64: B loads out of range only
   // probe 16: every K-tile re-reads K-tile 0 (a 64 KB working set per tile: L2-hit latency only)
   const unsigned a_kstep = (args.probe & 16) ? 0u : AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
   const unsigned b_kstep = (args.probe & 16) ? 0u : BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
