@@ -319,7 +319,7 @@ __device__ __forceinline__ void epi_acc_bf16(const f32x4_t (&acc)[8][4], unsigne
 // 3.60 (separate swiglu_bwd kernel).  Element ranges follow the global K-tile
 // order (item base + t); range-checked buffer resources turn the elements past E (and the
 // prologue's dummy ops) into zero loads and dropped stores, with no branch in the loop.
-// Pipelining (variant-1 schedule; P = t & 1 selects one of two register slots), all in phase
+// Pipelining (P = t & 1 selects one of two register slots), all in phase
 // j = 3, the one without LDS fragment reads (its wave group's read section has the most slack
 // under the other group's MFMA segment; the stores in phase 0 and the loads in phase 1 measured
 // 2.02 ms against 1.98 ms here):
@@ -336,9 +336,8 @@ constexpr unsigned SIDE_OOB = 0x80000000u;  // byte offset past every side buffe
 #endif
 //  // byte offset past every side buffer (E*4 < 2^31)
 
-template <bool AT, bool BT, int EPI, int GROUP, int V, int SIDE = 0>
+template <bool AT, bool BT, int EPI, int GROUP, int SIDE = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
-  static_assert(SIDE == 0 || (V & 1), "side job: variant-1 schedule only");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -509,26 +508,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
   };
   bf16x8_t af[4][2], bfr[4][2];
 
-  // V bits (A/B'd by tools/gemm64_bench.py): 1 = issue the phase's DMA in the read section
-  // (before the wait and the first barrier, where the wave otherwise idles at the barrier)
-  // instead of right before the MFMAs; 2 = no s_setprio around the MFMA cluster.  (A two-phase
-  // schedule with 32-MFMA segments measured neutral, +-1 %: profiles/gemm_ld_probe_r3.txt.)
-  constexpr bool EARLY = V & 1, PRIO = !(V & 2);
+  // Schedule (A/B'd by tools/gemm64_bench.py against the retired alternatives): each phase's DMA
+  // is issued in the read section (before the wait and the first barrier, where the wave would
+  // otherwise idle at the barrier), not right before the MFMAs, and the MFMA cluster runs under
+  // s_setprio 1.  (A two-phase schedule with 32-MFMA segments measured neutral, +-1 %:
+  // profiles/gemm_ld_probe_r3.txt.)
   auto mfma_quadrant = [&](auto m0_c, auto n0_c) {
     constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) acc[m0 + i][n0 + j] = mfma16(bfr[n0 + j][ks], af[i][ks], acc[m0 + i][n0 + j]);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   };
 
-  // EARLY moves each issue ahead of its phase's wait: the waits then count 2 more pieces
+  // each issue goes ahead of its phase's wait: the waits count 2 more pieces
   auto ktile = [&](int t, const unsigned char* buf, auto slot_c) {
     // j = 0
 #pragma unroll
@@ -539,9 +538,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bhalf(j), bpos(j), ks, lane);
-    if constexpr (EARLY) issue(K_<B_H1>{}, t + 1);
+    issue(K_<B_H1>{}, t + 1);
     bar();
-    if constexpr (!EARLY) issue(K_<B_H1>{}, t + 1);
     mfma_quadrant(K_<0>{}, K_<0>{});
     bar();
     // j = 1
@@ -549,15 +547,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     for (int j = 2; j < 4; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bhalf(j), bpos(j), ks, lane);
-    if constexpr (EARLY) {
-      issue(K_<A_HI>{}, t + 1);
-      wait_vm<8 + 5 * SIDE>();
-      bar();
-    } else {
-      wait_vm<6>();
-      bar();
-      issue(K_<A_HI>{}, t + 1);
-    }
+    issue(K_<A_HI>{}, t + 1);
+    wait_vm<8 + 5 * SIDE>();
+    bar();
     mfma_quadrant(K_<0>{}, K_<2>{});
     bar();
     // j = 2
@@ -565,25 +557,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_HI * HALF, ap + 16 * i, ks, lane);
-    if constexpr (EARLY) issue(K_<A_LO>{}, t + 2);
+    issue(K_<A_LO>{}, t + 2);
     bar();
-    if constexpr (!EARLY) issue(K_<A_LO>{}, t + 2);
     mfma_quadrant(K_<4>{}, K_<2>{});
     bar();
     // j = 3
-    if constexpr (EARLY) {
-      issue(K_<B_H0>{}, t + 2);
-      if constexpr (SIDE > 0) {
-        side_store(slot_c);                     // W(t-2)
-        side_load(slot_c, std::false_type{});  // L(t)
-      }
-      wait_vm<6 + 5 * SIDE>();
-      bar();
-    } else {
-      wait_vm<4>();
-      bar();
-      issue(K_<B_H0>{}, t + 2);
+    issue(K_<B_H0>{}, t + 2);
+    if constexpr (SIDE > 0) {
+      side_store(slot_c);                     // W(t-2)
+      side_load(slot_c, std::false_type{});  // L(t)
     }
+    wait_vm<6 + 5 * SIDE>();
+    bar();
     mfma_quadrant(K_<4>{}, K_<0>{});
     bar();
   };
@@ -776,7 +761,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 }
 
 
-// ---- 4-wave kernel (config variant 6): one 128x128 output block per wave ---------------------
+// ---- 4-wave kernel (config variants >= 4): one 128x128 output block per wave ---------------------
 // The 8-wave kernel above reads (128 + 64) x 64 operand elements from LDS per wave per K-tile for
 // a 128x64 block: 192 KB of ds_read per CU per K-tile, 75 % of the MFMA time of the tile at the
 // LDS's 256 B/clk.  hipBLASLt's MT256x256x64 kernel (rocprof: 256 threads, 130 KB LDS, 252 VGPRs)
@@ -800,73 +785,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
 //     least one phase earlier (so retired before that phase's closing barrier).  The waits keep 4-5
 //     half-tiles (16-20 DMA instructions per thread) in flight.
 constexpr int NT4 = 256;
-// one row of a 4x4 MFMA block: accumulators %(4i + j) += B frag %(20 + j) x A frag %(16 + i)
-#define G4W_MF(d, b, a) "v_mfma_f32_16x16x32_bf16 %" #d ", %" #b ", %" #a ", %" #d "\n\t"
-#define G4W_ROW_(d0, d1, d2, d3, a) G4W_MF(d0, 20, a) G4W_MF(d1, 21, a) G4W_MF(d2, 22, a) G4W_MF(d3, 23, a)
-#define G4W_ROW(i, a) G4W_ROW_I(i, a)
-#define G4W_ROW_I(i, a) G4W_ROW_##i(a)
-#define G4W_ROW_0(a) G4W_ROW_(0, 1, 2, 3, a)
-#define G4W_ROW_1(a) G4W_ROW_(4, 5, 6, 7, a)
-#define G4W_ROW_2(a) G4W_ROW_(8, 9, 10, 11, a)
-#define G4W_ROW_3(a) G4W_ROW_(12, 13, 14, 15, a)
-
-// a 64x64 quadrant x K = 64: two asm statements of 16 MFMAs with the accumulators pinned to the
-// accumulation registers ("+a"; hipcc's own MFMA selection moved them through VGPRs and spilled:
-// 256 accumulators + 160 fragment registers exceed the 256 VGPRs).  Hazards (guide §5.7 item 2):
-// s_nop 1 ahead for operands a compiler VALU / v_accvgpr_write just wrote; MFMA -> MFMA
-// accumulate chains need none; the epilogue's reads are fenced after the loop.
-template <int m0, int n0>
-__device__ __forceinline__ void g4w_mma(f32x4_t (&acc)[8][8], const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2]) {
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    asm volatile("s_nop 1\n\t"
-                 G4W_ROW(0, 16) G4W_ROW(1, 17) G4W_ROW(2, 18) G4W_ROW(3, 19)
-                 : "+a"(acc[m0][n0]), "+a"(acc[m0][n0 + 1]), "+a"(acc[m0][n0 + 2]), "+a"(acc[m0][n0 + 3]),
-                   "+a"(acc[m0 + 1][n0]), "+a"(acc[m0 + 1][n0 + 1]), "+a"(acc[m0 + 1][n0 + 2]), "+a"(acc[m0 + 1][n0 + 3]),
-                   "+a"(acc[m0 + 2][n0]), "+a"(acc[m0 + 2][n0 + 1]), "+a"(acc[m0 + 2][n0 + 2]), "+a"(acc[m0 + 2][n0 + 3]),
-                   "+a"(acc[m0 + 3][n0]), "+a"(acc[m0 + 3][n0 + 1]), "+a"(acc[m0 + 3][n0 + 2]), "+a"(acc[m0 + 3][n0 + 3])
-                 : "v"(A[0][ks]), "v"(A[1][ks]), "v"(A[2][ks]), "v"(A[3][ks]),
-                   "v"(B[0][ks]), "v"(B[1][ks]), "v"(B[2][ks]), "v"(B[3][ks]));
-  }
-}
-
-// one row block (4 MFMAs: acc row i x n-tiles n0..n0+3, one K-slice).  The "memory" clobber pins
-// the LDS fragment reads and DMA issues placed between two such statements to their gap: the
-// K-loop interleaves its loads with the MFMA stream instead of issuing them all ahead of it
-// (one wave per SIMD: an instruction waiting behind a busy MFMA pipe stalls the wave's issue).
-__device__ __forceinline__ void g4w_row(f32x4_t& c0, f32x4_t& c1, f32x4_t& c2, f32x4_t& c3, const bf16x8_t& a,
-                                        const bf16x8_t& b0, const bf16x8_t& b1, const bf16x8_t& b2, const bf16x8_t& b3) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %5, %4, %0\n\t"
-               "v_mfma_f32_16x16x32_bf16 %1, %6, %4, %1\n\t"
-               "v_mfma_f32_16x16x32_bf16 %2, %7, %4, %2\n\t"
-               "v_mfma_f32_16x16x32_bf16 %3, %8, %4, %3"
-               : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
-               : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
-               : "memory");
-}
-
-// g4w_row with one LDS-DMA piece issued between its second and third MFMA (variant 8): M0 is
-// written ahead of the first MFMA, so the two MFMAs cover the M0 -> LDS-DMA wait state that the
-// stand-alone bdma16 pays with an s_nop (4 issue cycles), and the DMA issue shares a gap with no
-// other filler (an MFMA gap leaves 8 of its 16 cycles to other instructions).
-__device__ __forceinline__ void g4w_row_dma(f32x4_t& c0, f32x4_t& c1, f32x4_t& c2, f32x4_t& c3, const bf16x8_t& a,
-                                            const bf16x8_t& b0, const bf16x8_t& b1, const bf16x8_t& b2,
-                                            const bf16x8_t& b3, unsigned voff, i32x4_t rsrc, unsigned soff,
-                                            unsigned lds_byte) {
-  asm volatile("s_mov_b32 m0, %12\n\t"
-               "v_mfma_f32_16x16x32_bf16 %0, %5, %4, %0\n\t"
-               "v_mfma_f32_16x16x32_bf16 %1, %6, %4, %1\n\t"
-               "buffer_load_dwordx4 %9, %10, %11 offen lds\n\t"
-               "v_mfma_f32_16x16x32_bf16 %2, %7, %4, %2\n\t"
-               "v_mfma_f32_16x16x32_bf16 %3, %8, %4, %3"
-               : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
-               : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(voff), "s"(rsrc), "s"(soff), "s"(lds_byte)
-               : "memory");
-}
-
 // two MFMAs (acc row i x n-tiles j, j+1, one K-slice) / the same with one LDS-DMA piece between
-// them (M0 written ahead of the first MFMA): variant 9's finer statements, so each fragment read
-// and each DMA piece gets an MFMA gap of its own
+// them (M0 written ahead of the first MFMA, so the MFMA covers the M0 -> LDS-DMA wait state): the
+// K-loop's statements, so each fragment read and each DMA piece gets an MFMA gap of its own.
+// Accumulators are pinned to the accumulation registers ("+a"; hipcc's own MFMA selection moved
+// them through VGPRs and spilled: 256 accumulators + 160 fragment registers exceed the 256
+// VGPRs); the "memory" clobber pins the reads / DMA issues placed between two statements to their
+// gap.  Hazards (guide §5.7 item 2): MFMA -> MFMA accumulate chains need no wait states; the
+// epilogue's reads are fenced after the loop (g4w_fence).
 __device__ __forceinline__ void g4w_pair(f32x4_t& c0, f32x4_t& c1, const bf16x8_t& a, const bf16x8_t& b0,
                                          const bf16x8_t& b1) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %3, %2, %0\n\t"
@@ -1083,10 +1009,9 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
 // waits count past (P0: 20 + 2 S_OPS, P1: 20 + S_OPS, P2: 16 + S_OPS); L(t) is retired by the P1
 // wait of K-tile t+2, before W(t) at P3 of K-tile t+2.  The prologue issues out-of-range dummies
 // W/L(-2) and W/L(-1) at their stream positions so every count holds from the first phase.
-// IL: 0 = loads ahead of each phase's MFMAs (variant 6), 1 = loads interleaved between MFMA row
-// blocks (variant 7), 2 = as 1 with the DMA pieces inside the MFMA statements (variant 8), 3 =
-// 2-MFMA statements, reads in the first half of the phase, DMA in the second (variant 9)
-template <bool AT, bool BT, int EPI, int GROUP, int IL, int SIDE = 0>
+// Each phase: 16 statements of 2 MFMAs, the next phase's fragment reads in the first half, the
+// phase's 4 DMA pieces inside the second (retired orderings: profiles/ab_gemm64_config_r4.log)
+template <bool AT, bool BT, int EPI, int GROUP, int SIDE = 0>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(G64Args args) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1241,9 +1166,6 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) d[j][ks] = frag<BT>(img, p0 + 16 * j, ks, lane);
   };
-  auto mma = [&](auto m0_c, auto n0_c, const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2]) {
-    g4w_mma<decltype(m0_c)::value, decltype(n0_c)::value>(acc, A, B);
-  };
   // lgkmcnt(0) through the builtin: hipcc's waitcnt pass then knows the fragment reads are done
   // (an asm wait is opaque to it, and it re-waited lgkmcnt(0) ahead of the next MFMA block --
   // after the NEXT phase's reads had been issued, serialising them)
@@ -1254,9 +1176,10 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     if (!(args.probe & 2)) bar();
   };
 
-  // interleaved phase (IL): 8 row blocks of 4 MFMAs (K-slice ks = r >> 2, row i = r & 3); after
-  // block r the r-th fragment read of the next phase's set (A: m-tile f >> 1 / K-slice f & 1; B:
-  // n-tile / K-slice) and, after even r, one quarter of the phase's DMA half-tile
+  // one phase: 16 statements of 2 MFMAs (K-slice q >> 3, row (q >> 1) & 3, n-tiles 2 (q & 1) + 0/1);
+  // the 8 fragment reads of the next phase's set (A: m-tile f / K-slice fk; B: n-tile / K-slice) go
+  // out after statements 0-7 (they complete long before the phase's closing lgkmcnt wait), the 4
+  // DMA pieces of the phase's half-tile inside statements 9, 11, 13, 15
   auto il_phase = [&](auto m0_c, auto n0_c, const bf16x8_t (&A)[4][2], const bf16x8_t (&B)[4][2], auto rd_b_c,
                       bf16x8_t (&dst)[4][2], const unsigned char* img, int p0, auto kind_c, int t) {
     constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
@@ -1266,42 +1189,21 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
     const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
     const i32x4_t rr = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
-    if constexpr (IL == 3) {
-      // variant 9: 16 statements of 2 MFMAs; the 8 fragment reads go out after statements 0-7
-      // (they complete long before the phase's closing lgkmcnt wait), the 4 DMA pieces inside
-      // statements 9, 11, 13, 15
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int ks = q >> 3, i = (q >> 1) & 3, j = (q & 1) * 2;
-        if (q >= 8 && (q & 1)) {
-          const int pc = (q - 9) >> 1;
-          g4w_pair_dma(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks],
-                       vo[kind][pc], rr, so, l + pc * 4096);
-        } else {
-          g4w_pair(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks]);
-        }
-        if (q < 8) {
-          const int f = q >> 1, fk = q & 1;
-          if constexpr (RDB) dst[f][fk] = frag<BT>(img, p0 + 16 * f, fk, lane);
-          else dst[f][fk] = frag<AT>(img, p0 + 16 * f, fk, lane);
-        }
-      }
-      return;
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int ks = r >> 2, i = r & 3;
-      if (IL == 2 && (r & 1) == 0) {
-        g4w_row_dma(acc[m0 + i][n0], acc[m0 + i][n0 + 1], acc[m0 + i][n0 + 2], acc[m0 + i][n0 + 3], A[i][ks],
-                    B[0][ks], B[1][ks], B[2][ks], B[3][ks], vo[kind][r >> 1], rr, so, l + (r >> 1) * 4096);
+    for (int q = 0; q < 16; ++q) {
+      const int ks = q >> 3, i = (q >> 1) & 3, j = (q & 1) * 2;
+      if (q >= 8 && (q & 1)) {
+        const int pc = (q - 9) >> 1;
+        g4w_pair_dma(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks],
+                     vo[kind][pc], rr, so, l + pc * 4096);
       } else {
-        g4w_row(acc[m0 + i][n0], acc[m0 + i][n0 + 1], acc[m0 + i][n0 + 2], acc[m0 + i][n0 + 3], A[i][ks], B[0][ks],
-                B[1][ks], B[2][ks], B[3][ks]);
+        g4w_pair(acc[m0 + i][n0 + j], acc[m0 + i][n0 + j + 1], A[i][ks], B[j][ks], B[j + 1][ks]);
       }
-      const int f = r >> 1, fk = r & 1;
-      if constexpr (RDB) dst[f][fk] = frag<BT>(img, p0 + 16 * f, fk, lane);
-      else dst[f][fk] = frag<AT>(img, p0 + 16 * f, fk, lane);
-      if (IL != 2 && (r & 1) == 0) bdma16(rr, vo[kind][r >> 1], so, l + (r >> 1) * 4096);
+      if (q < 8) {
+        const int f = q >> 1, fk = q & 1;
+        if constexpr (RDB) dst[f][fk] = frag<BT>(img, p0 + 16 * f, fk, lane);
+        else dst[f][fk] = frag<AT>(img, p0 + 16 * f, fk, lane);
+      }
     }
   };
 
@@ -1328,39 +1230,6 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   rdB(b03[0], smem + bo03, p03);
   sync(K_<-1>{});  // WAR: P0 restages A_lo of this buffer
 
-  auto ktile = [&](int t, auto par_c) {
-    constexpr int P = decltype(par_c)::value;
-    const unsigned char* buf = smem + P * BUF;
-    const unsigned char* nbuf = smem + (P ^ 1) * BUF;
-    // P0
-    rdB(b47, buf + bo47, p47);
-    issue(K_<A_LO>{}, t + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(K_<0>{}, K_<0>{}, a_lo, b03[P]);
-    sync(K_<20 + 2 * S_OPS>{});
-    // P1
-    rdA(a_hi, buf + A_HI * HALF);
-    issue(K_<B_H0>{}, t + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(K_<0>{}, K_<4>{}, a_lo, b47);
-    sync(K_<20 + S_OPS>{});
-    // P2
-    rdA(a_lo, nbuf + A_LO * HALF);
-    issue(K_<B_H1>{}, t + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(K_<4>{}, K_<4>{}, a_hi, b47);
-    sync(K_<16 + S_OPS>{});
-    // P3
-    rdB(b03[P ^ 1], nbuf + bo03, p03);
-    issue(K_<A_HI>{}, t + 2);
-    if constexpr (SIDE > 0) {
-      side_store(K_<P>{});                   // W(t-2)
-      side_load(K_<P>{}, std::false_type{});  // L(t)
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mma(K_<4>{}, K_<0>{}, a_hi, b03[P]);
-    sync(K_<-1>{});
-  };
   auto ktile_il = [&](int t, auto par_c) {
     constexpr int P = decltype(par_c)::value;
     const unsigned char* buf = smem + P * BUF;
@@ -1379,13 +1248,8 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     sync(K_<-1>{});
   };
   for (int t = 0; t < KT; t += 2) {
-    if constexpr (IL > 0) {
-      ktile_il(t, K_<0>{});
-      ktile_il(t + 1, K_<1>{});
-    } else {
-      ktile(t, K_<0>{});
-      ktile(t + 1, K_<1>{});
-    }
+    ktile_il(t, K_<0>{});
+    ktile_il(t + 1, K_<1>{});
   }
   wait_vm<0>();  // the clamped tail items are still landing
   if constexpr (SIDE > 0) {  // W(KT-2), W(KT-1)
@@ -1414,10 +1278,12 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 // wait may count only younger LOADS: the next item's first waits therefore also wait for the
 // epilogue's stores (16-byte stores halve them).  The last two K-tiles are peeled: only there do
 // the DMA sources belong to the next item, so its fields are decoded there and the current item's
-// buffer descriptors are dead -- holding both sets through the loop spilled SGPRs to VGPR lanes,
-// and a v_readlane reload (a VALU write of an SGPR) right before the inline-asm buffer_load that
-// reads it is the unpadded VALU-SGPR -> VMEM hazard (intermittent wrong rows).  K >= 256.
-// Variant-9 phase schedule.
+// buffer descriptors are dead.  The earlier, unpeeled form held both descriptor sets through the
+// loop (SGPRs spilled to VGPR lanes) and gave intermittent wrong rows; the peeled form fixed that
+// empirically (every test since), but the root cause is NOT pinned down: the suspected VALU write
+// of an SGPR (v_readlane reload) ahead of an inline-asm buffer_load was not confirmed --
+// tools/sgpr_hazard_check.py found only SALU writers ahead of those loads.  K >= 256.
+// Phase schedule: the one-shot 4-wave kernel's.
 template <bool AT, bool BT, int EPI, int GROUP>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4wp_kernel(G64Args args,
                                                                                                   int n_items) {
@@ -1619,426 +1485,6 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   }
 }
 
-// ---- 4-wave K-step-major kernel (config variant 4) -------------------------------------------
-// The phase kernel above ends every 32-MFMA phase on a workgroup barrier (4 per K-tile) and, with
-// one wave per SIMD, no partner wave covers the barrier.  This loop has hipBLASLt's shape instead:
-// per K-tile two K-steps (K = 32 each) of 64 MFMAs per wave (all 8 x 8 tiles of the wave's
-// 128 x 128 block), with the NEXT K-step's 8 A + 8 B fragments read under the current one (two
-// register sets) and ONE barrier per K-tile:
-//    A(t)  MFMA K-step 0 of tile t  |  read K-step 1 of tile t  (buffer t & 1)
-//          lgkmcnt(0), vmcnt(0), s_barrier     (RAW: tile t+1 landed; WAR: tile t fully read)
-//    B(t)  MFMA K-step 1 of tile t  |  read K-step 0 of tile t+1 (other buffer)  |  DMA tile t+2 -> buffer t & 1
-// Fragment reads go out after the first 16 of 32 two-MFMA statements (done well before the next
-// wait), DMA pieces ride inside the last 16.  Tile t+2's DMA has one K-tile (~128 MFMAs) to land.
-template <bool AT, bool BT, int EPI, int GROUP>
-__global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4k_kernel(G64Args args) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-
-  const int bid = blockIdx.x;
-  int wg, sp = -1, u = 0;
-  if (bid < args.n_main) {
-    const int nwg = args.n_main;
-    const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
-    wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
-  } else {
-    const int i = bid - args.n_main;
-    u = i / args.splits;
-    sp = i - u * args.splits;
-    wg = args.n_main + u;
-  }
-  const int per_group = GROUP * args.tiles_n;
-  const int grp = wg / per_group;
-  const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
-  const int inner = wg - grp * per_group;
-  const int tm = grp * GROUP + inner % gsz;
-  const int tn = inner / gsz;
-
-  const long lda = args.lda, ldb = args.ldb;
-  const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
-  constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;
-  const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
-                             : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
-  const i32x4_t ra = make_rsrc(Ab), rb = make_rsrc(Bb);
-  const i32x4_t rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
-  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
-  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
-  const int KT = sp < 0 ? args.K / TK : args.kt_part;
-  const unsigned kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
-
-  unsigned vo[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    vo[A_LO][i] = stage_voff<AT, A_LO, NT4>(i, tid, lda);
-    vo[A_HI][i] = stage_voff<AT, A_HI, NT4>(i, tid, lda);
-    vo[B_H0][i] = stage_voff<BT, B_H0, NT4>(i, tid, ldb);
-    vo[B_H1][i] = stage_voff<BT, B_H1, NT4>(i, tid, ldb);
-  }
-  const unsigned lds0 = lds_addr(smem) + wave * 1024;
-  auto issue = [&](auto kind_c, int t) __attribute__((always_inline)) {
-    constexpr int kind = decltype(kind_c)::value;
-    const unsigned tc = kt0 + (unsigned)(t < KT ? t : KT - 1);
-    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
-    const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
-    const i32x4_t r = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bdma16(r, vo[kind][i], so, l + i * 4096);
-  };
-
-  f32x4_t acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int ap = wr * 64;
-  const int bo03 = PAIRED_B ? B_H0 * HALF : (B_H0 + wc) * HALF, p03 = PAIRED_B ? wc * 64 : 0;
-  const int bo47 = PAIRED_B ? B_H1 * HALF : (B_H0 + wc) * HALF, p47 = PAIRED_B ? wc * 64 : 64;
-  bf16x8_t fa[2][8], fb[2][8];
-  auto frA = [&](int i, int ks, const unsigned char* buf) __attribute__((always_inline)) {
-    return frag<AT>(buf + (i < 4 ? A_LO : A_HI) * HALF, ap + 16 * (i & 3), ks, lane);
-  };
-  auto frB = [&](int j, int ks, const unsigned char* buf) __attribute__((always_inline)) {
-    return j < 4 ? frag<BT>(buf + bo03, p03 + 16 * j, ks, lane) : frag<BT>(buf + bo47, p47 + 16 * (j - 4), ks, lane);
-  };
-  // one K-step: 32 statements of 2 MFMAs on fragment set S; after statement q < 16 the q-th
-  // fragment of the next K-step (A 0-7, then B 0-7) into set S ^ 1; with DMA, piece q - 16
-  // (half-tile kind (q - 16) >> 2) of tile t_dma rides inside statement q >= 16
-  auto kstep = [&](auto s_c, auto dma_c, int nks, const unsigned char* nbuf, int t_dma) __attribute__((always_inline)) {
-    constexpr int S = decltype(s_c)::value;
-    constexpr bool DMA = decltype(dma_c)::value;
-    const unsigned tc = kt0 + (unsigned)(t_dma < KT ? t_dma : KT - 1);
-    const unsigned soA = __builtin_amdgcn_readfirstlane(tc * a_kstep);
-    const unsigned soB = __builtin_amdgcn_readfirstlane(tc * b_kstep);
-    const unsigned l0 = lds0 + (t_dma & 1) * BUF;
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int i = q >> 2, j = (q & 3) * 2;
-      if (DMA && q >= 16) {
-        const int kind = (q - 16) >> 2, pc = (q - 16) & 3;
-        const i32x4_t r = kind <= A_HI ? ra : kind == B_H1 ? rb_hi : rb;
-        g4w_pair_dma(acc[i][j], acc[i][j + 1], fa[S][i], fb[S][j], fb[S][j + 1], vo[kind][pc], r,
-                     kind <= A_HI ? soA : soB, l0 + kind * HALF + pc * 4096);
-      } else {
-        g4w_pair(acc[i][j], acc[i][j + 1], fa[S][i], fb[S][j], fb[S][j + 1]);
-      }
-      if (q < 8) fa[S ^ 1][q] = frA(q, nks, nbuf);
-      else if (q < 16) fb[S ^ 1][q - 8] = frB(q - 8, nks, nbuf);
-    }
-  };
-
-  // prologue: tiles 0 and 1 in flight, tile 0 retired, K-step 0 of tile 0 into set 0
-  issue(K_<A_LO>{}, 0);
-  issue(K_<A_HI>{}, 0);
-  issue(K_<B_H0>{}, 0);
-  issue(K_<B_H1>{}, 0);
-  issue(K_<A_LO>{}, 1);
-  issue(K_<A_HI>{}, 1);
-  issue(K_<B_H0>{}, 1);
-  issue(K_<B_H1>{}, 1);
-  wait_vm<16>();
-  bar();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) fa[0][i] = frA(i, 0, smem);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) fb[0][j] = frB(j, 0, smem);
-
-  auto ktile = [&](int t, auto par_c) __attribute__((always_inline)) {
-    constexpr int P = decltype(par_c)::value;
-    const unsigned char* buf = smem + P * BUF;
-    const unsigned char* nbuf = smem + (P ^ 1) * BUF;
-    kstep(K_<0>{}, std::false_type{}, 1, buf, t);  // K-step 0 of t  |  reads K-step 1 of t
-    wait_vm<0>();
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) through the builtin (hipcc tracks it)
-    bar();
-    kstep(K_<1>{}, std::true_type{}, 0, nbuf, t + 2);  // K-step 1 of t  |  reads K-step 0 of t+1  |  DMA t+2
-  };
-  for (int t = 0; t < KT; t += 2) {
-    ktile(t, K_<0>{});
-    ktile(t + 1, K_<1>{});
-  }
-  wait_vm<0>();  // the clamped tail items are still landing
-  g4w_fence(acc);
-  g4w_epilogue<EPI>(args, acc, tm, tn, wr, wc, lane, sp, u);
-}
-
-// ---- persistent variant ------------------------------------------------------------------------
-// Measured (profiles/gemm_ld_probe_r3.txt): the same kernel runs ~1450 TF at K = 4096 and
-// ~1525 TF at K = 11008-32000 — a fixed per-tile cost (workgroup launch, the prologue's pipeline
-// fill with nothing to overlap it, the epilogue's store tail) of ~5 % of a 92-us K = 4096 tile.
-// gemm64p_kernel keeps one workgroup per CU resident and walks the work items g = blockIdx.x,
-// + gridDim.x, ...: the K-tile DMA stream does not stop at a tile boundary — the items past the
-// last K-tile of tile i (which the one-shot kernel re-loads and discards) ARE the first K-tiles
-// of tile i+1, in exactly the prologue's order, so tile i+1 starts with its first operands
-// already in LDS.  The epilogue of tile i runs between the two K-loops with no barrier; as the
-// two wave groups run one barrier apart, each group's epilogue overlaps the other group's MFMA
-// segment.  Epilogue stores are inline-asm global_store (exactly EPI_OPS vector-memory ops per
-// thread, which the first wait of the next tile counts past); epilogues that load (accumulate,
-// SwiGLU backward) end with vmcnt(0) instead.
-struct Item {
-  int tm, tn, sp, u, KT;
-  unsigned kt0;
-};
-
-template <int GROUP>
-__device__ __forceinline__ Item decode_item(const G64Args& args, int bid) {
-  int wg, sp = -1, u = 0;
-  if (bid < args.n_main) {
-    const int nwg = args.n_main;
-    const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
-    wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
-  } else {
-    const int i = bid - args.n_main;
-    u = i / args.splits;
-    sp = i - u * args.splits;
-    wg = args.n_main + u;
-  }
-  const int per_group = GROUP * args.tiles_n;
-  const int grp = wg / per_group;
-  const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
-  const int inner = wg - grp * per_group;
-  Item it;
-  it.tm = grp * GROUP + inner % gsz;
-  it.tn = inner / gsz;
-  it.sp = sp;
-  it.u = u;
-  it.KT = sp < 0 ? args.K / TK : args.kt_part;
-  it.kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
-  return it;
-}
-
-constexpr int EPI_OPS = 32;  // vector-memory ops per thread of a store-only epilogue (8 x 4 tiles)
-
-__device__ __forceinline__ void st_x2(unsigned short* p, s2_t v) {
-  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
-// a store of more than 64 bits of data needs wait states before a VALU write of its data VGPRs
-// (hipcc pads only its own stores): the trailing s_nop covers the accumulator re-zeroing that
-// follows the epilogue
-__device__ __forceinline__ void st_x4(float* p, f32x4_t v) {
-  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-
-template <bool AT, bool BT, int EPI, int GROUP>
-__global__ __launch_bounds__(NTHR, 1) void gemm64p_kernel(G64Args args, int n_items) {
-  static_assert(EPI != EPI_SWIGLU_FWD && EPI != EPI_ROPE_QKV && EPI != EPI_UP_SWIGLU,
-                "paired-column epilogues: one-shot kernel only");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  int g = blockIdx.x;
-  if (g >= n_items) return;
-  const long lda = args.lda, ldb = args.ldb;
-  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
-  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
-  auto base_a = [&](const Item& it) {
-    return AT ? args.a + (long)it.tm * TM : args.a + (long)it.tm * TM * lda;
-  };
-  auto base_b = [&](const Item& it) {
-    return BT ? args.b + (long)it.tn * TN : args.b + (long)it.tn * TN * ldb;
-  };
-  // only what the DMA stream needs stays live through the K-loop (SGPR budget): the current and
-  // next item's operand bases and K-tile ranges; the epilogue re-decodes its item
-  Item cur = decode_item<GROUP>(args, g);
-  const unsigned short *pa = base_a(cur), *pb = base_b(cur);
-  unsigned kt0 = cur.kt0;
-  int KT = cur.KT;
-  int gn = g + (int)gridDim.x;
-  bool has_next = gn < n_items;
-  const unsigned short *pa_x = pa, *pb_x = pb;
-  unsigned kx = kt0 + (unsigned)(KT - 1);
-  int kx_step = 0;
-  if (has_next) {
-    const Item nx = decode_item<GROUP>(args, gn);
-    pa_x = base_a(nx);
-    pb_x = base_b(nx);
-    kx = nx.kt0;
-    kx_step = 1;
-  }
-
-  unsigned vo[4][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    vo[A_LO][i] = stage_voff<AT, A_LO>(i, tid, lda);
-    vo[A_HI][i] = stage_voff<AT, A_HI>(i, tid, lda);
-    vo[B_H0][i] = stage_voff<BT, B_H0>(i, tid, ldb);
-    vo[B_H1][i] = stage_voff<BT, B_H1>(i, tid, ldb);
-  }
-  const unsigned lds0 = lds_addr(smem) + wave * 1024;
-
-  // stream item: half-tile KIND of K-tile t of the current item; t >= KT continues into the next
-  // item's K-tiles 0, 1 (KT is even, so the LDS buffer parity carries over); with no next item the
-  // last K-tile is re-loaded into slots nobody reads again
-  // stream item: half-tile KIND of K-tile t; t >= KT continues into the next item (pa_x / pb_x /
-  // kx: the next item's bases and first K-tile, or — with no next item — the current bases and
-  // its last K-tile with step 0, i.e. a discarded re-load).  Branch-free scalar selects: a
-  // branch per issue cost ~3 s_cbranch per DMA piece in the inner loop
-  auto issue = [&](auto kind_c, int t) {
-    constexpr int kind = decltype(kind_c)::value;
-    const int over = t - KT;
-    const unsigned long m = (unsigned long)(long)(over >> 31);  // all ones while t < KT
-    const unsigned long pc = (unsigned long)(kind <= A_HI ? pa : pb), px = (unsigned long)(kind <= A_HI ? pa_x : pb_x);
-    const unsigned long base = px ^ ((pc ^ px) & m);
-    const unsigned tx = kx + (unsigned)(over * kx_step);
-    const unsigned tc = tx ^ ((tx ^ (kt0 + (unsigned)t)) & (unsigned)m);
-    const i32x4_t r = make_rsrc(reinterpret_cast<const void*>(base));
-    const unsigned l = lds0 + (t & 1) * BUF + kind * HALF;
-    const unsigned so = __builtin_amdgcn_readfirstlane(tc * (kind <= A_HI ? a_kstep : b_kstep));
-    bdma16(r, vo[kind][0], so, l);
-    bdma16(r, vo[kind][1], so, l + 8192);
-  };
-
-  f32x4_t acc[8][4];
-  const int ap = wr * 64, bh = (wc >> 1) * HALF, bp = (wc & 1) * 64;
-  bf16x8_t af[4][2], bfr[4][2];
-  auto mfma_quadrant = [&](auto m0_c, auto n0_c) {
-    constexpr int m0 = decltype(m0_c)::value, n0 = decltype(n0_c)::value;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) acc[m0 + i][n0 + j] = mfma16(bfr[n0 + j][ks], af[i][ks], acc[m0 + i][n0 + j]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  // gemm64_kernel's variant-1 schedule (DMA issued in the read section); AFTER_EPI: the first
-  // K-tile after an epilogue, whose j = 1 wait also counts the EPI_OPS stores issued between
-  auto ktile = [&](int t, const unsigned char* buf, bool after_epi) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_LO * HALF, ap + 16 * i, ks, lane);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
-    issue(K_<B_H1>{}, t + 1);
-    bar();
-    mfma_quadrant(K_<0>{}, K_<0>{});
-    bar();
-#pragma unroll
-    for (int j = 2; j < 4; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag<BT>(buf + B_H0 * HALF + bh, bp + 16 * j, ks, lane);
-    issue(K_<A_HI>{}, t + 1);
-    if (after_epi) wait_vm<8 + EPI_OPS>();  // wave-uniform scalar branch
-    else wait_vm<8>();
-    bar();
-    mfma_quadrant(K_<0>{}, K_<2>{});
-    bar();
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag<AT>(buf + A_HI * HALF, ap + 16 * i, ks, lane);
-    issue(K_<A_LO>{}, t + 2);
-    bar();
-    mfma_quadrant(K_<4>{}, K_<2>{});
-    bar();
-    issue(K_<B_H0>{}, t + 2);
-    wait_vm<6>();
-    bar();
-    mfma_quadrant(K_<4>{}, K_<0>{});
-    bar();
-  };
-
-  // prologue (first item only): the stream up to B_h0(1) in flight; A_lo/B_h0/B_h1 of K-tile 0 retired
-  issue(K_<A_LO>{}, 0);
-  issue(K_<B_H0>{}, 0);
-  issue(K_<B_H1>{}, 0);
-  issue(K_<A_HI>{}, 0);
-  issue(K_<A_LO>{}, 1);
-  issue(K_<B_H0>{}, 1);
-  wait_vm<6>();
-  bar();
-  if (wr == 1) bar();  // wave group 1 runs one barrier behind group 0 (for the whole launch)
-
-  bool first = true;
-  for (;;) {
-    // this item's epilogue coordinates (the current item only; decoded before its K-loop)
-    const Item ep = first ? cur : decode_item<GROUP>(args, g);
-    const bool ep_split = ep.sp >= 0;
-    const long ep_off = ep_split ? ((long)ep.u * args.splits + ep.sp) * (TM * TN)
-                                 : (long)(ep.tm * TM) * args.ldc + ep.tn * TN;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma nounroll
-    for (int t = 0; t < KT; t += 2) {
-      ktile(t, smem, t == 0 && !first);
-      ktile(t + 1, smem + BUF, false);
-    }
-    // ---- epilogue of the current item (lane: C[m = .. + (l&15)][n = .. + 4(l>>4) + r])
-    const int gq = lane >> 4, i16 = lane & 15;
-    if (ep_split) {  // split item: fp32 partial tile, row-major 256 x 256
-      float* W = args.ws + ep_off + (wr * 128 + i16) * TN + wc * 64 + 4 * gq;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) st_x4(W + (16 * i) * TN + 16 * j, acc[i][j]);
-    } else if constexpr (epi_f32(EPI)) {
-      float* Cf = reinterpret_cast<float*>(args.c) + ep_off + (long)(wr * 128 + i16) * args.ldc + wc * 64 + 4 * gq;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float* p = Cf + (long)(16 * i) * args.ldc + 16 * j;
-          if constexpr (EPI == EPI_ACC_F32) st_x4(p, *reinterpret_cast<const f32x4_t*>(p) + acc[i][j]);
-          else st_x4(p, acc[i][j]);
-        }
-      if constexpr (EPI == EPI_ACC_F32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      unsigned short* Cb = args.c + ep_off + (long)(wr * 128 + i16) * args.ldc + wc * 64 + 4 * gq;
-      if constexpr (EPI == EPI_SWIGLU_BWD) {
-        epi_swiglu_bwd(acc, Cb, args.aux + (Cb - args.c), args.ldc, args.N);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if constexpr (EPI == EPI_ACC) {
-        epi_acc_bf16(acc, Cb, args.ldc, true);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            unsigned short* p = Cb + (long)(16 * i) * args.ldc + 16 * j;
-            f32x4_t v = acc[i][j];
-            s2_t o;
-            o[0] = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-            o[1] = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-            st_x2(p, o);
-          }
-      }
-    }
-    if (!has_next) break;
-    // advance: the next item's first K-tiles are already in flight / landed
-    g = gn;
-    pa = pa_x;
-    pb = pb_x;
-    kt0 = kx;
-    KT = g < args.n_main ? args.K / TK : args.kt_part;
-    gn += (int)gridDim.x;
-    has_next = gn < n_items;
-    kx = kt0 + (unsigned)(KT - 1);
-    kx_step = 0;
-    if (has_next) {
-      const Item nx = decode_item<GROUP>(args, gn);
-      pa_x = base_a(nx);
-      pb_x = base_b(nx);
-      kx = nx.kt0;
-      kx_step = 1;
-    }
-    first = false;
-  }
-  if (wr == 0) bar();  // re-align the barrier count of the two groups
-  wait_vm<0>();        // the clamped tail items are still landing
-}
-
 // sum of the split partials of tail tile u (grouped-order position n_main + u) + epilogue;
 // thread = 8 consecutive columns of one row
 template <int EPI, int GROUP>
@@ -2095,51 +1541,27 @@ __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
   store8(p, v);
 }
 
+// schedule variant (config / 100 % 10): 3 = the persistent 4-wave kernel, >= 4 = the one-shot 4-wave
+// kernel, 0-2 = the 8-wave kernel (the SwiGLU-backward epilogue: always the 8-wave kernel).  Retired
+// (measured slower, aliased here): the 8-wave schedules 0 / 2 / 3 and persistent 8-wave kernel (5;
+// profiles/gemm_persistent_r3.txt), the 4-wave K-step-major kernel (4) and the 4-wave phase
+// orderings 6-8 (profiles/ab_gemm64_config_r4.log), register-staged B (profiles/gemm_regstage_ab_r4.txt)
 template <bool AT, bool BT, int EPI, int GROUP>
 void launch_g(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
-  const dim3 grid(n_items), block(NTHR);
-  constexpr bool fused_fwd = EPI == EPI_SWIGLU_FWD || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU;
-  if constexpr (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU ||
-                EPI == EPI_SWIGLU_FWD) {
-    if (variant == 3 && g.K < 4 * TK) variant = 9;  // the persistent kernel peels two K-tiles per item
-    if (variant == 3 && (EPI == EPI_STORE || EPI == EPI_ACC || epi_f32(EPI) || EPI == EPI_ROPE_QKV ||
-                         EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD)) {  // persistent 4-wave kernel
-      const dim3 pgrid(min(n_items, num_cus()));
-      hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP>), pgrid, dim3(NT4), 0, stream(), g, n_items);
-      variant = -1;
-    }
-    if (variant == 4) {  // 4-wave K-step-major kernel: one barrier per K-tile
-      hipLaunchKernelGGL((gemm4k_kernel<AT, BT, EPI, GROUP>), grid, dim3(NT4), 0, stream(), g);
-      variant = -1;
-    }
-    if (variant >= 6 && variant <= 9) {  // 4-wave kernel: 128x128 per wave (7-9: loads interleaved)
-      if (variant == 9) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 3>), grid, dim3(NT4), 0, stream(), g);
-      else if (variant == 8) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 2>), grid, dim3(NT4), 0, stream(), g);
-      else if (variant == 7) hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 1>), grid, dim3(NT4), 0, stream(), g);
-      else hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP, 0>), grid, dim3(NT4), 0, stream(), g);
-      variant = -1;
+  const dim3 grid(n_items);
+  bool launched = false;
+  if constexpr (EPI != EPI_SWIGLU_BWD) {
+    if (variant == 3 && g.K >= 4 * TK) {  // the persistent kernel peels two K-tiles per item
+      hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP>), dim3(min(n_items, num_cus())), dim3(NT4), 0, stream(), g,
+                         n_items);
+      launched = true;
+    } else if (variant >= 3) {
+      hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP>), grid, dim3(NT4), 0, stream(), g);
+      launched = true;
     }
   }
-  if constexpr (!fused_fwd) {
-    if (variant == 5) {  // persistent: one workgroup per CU walks the items
-      const dim3 pgrid(min(n_items, num_cus()));
-      hipLaunchKernelGGL((gemm64p_kernel<AT, BT, EPI, GROUP>), pgrid, block, 0, stream(), g, n_items);
-      variant = -1;
-    }
-  }
-  if constexpr (epi_f32(EPI) || EPI == EPI_ROPE_QKV || EPI == EPI_UP_SWIGLU) {
-    // fp32 outputs / fused training epilogues: variant 1 (or persistent) only (fewer instantiations)
-    if (variant != -1) hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g);
-  } else {
-    switch (variant) {
-      case -1: break;
-      case 1: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 1>), grid, block, 0, stream(), g); break;
-      case 2: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 2>), grid, block, 0, stream(), g); break;
-      case 3: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 3>), grid, block, 0, stream(), g); break;
-      default: hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP, 0>), grid, block, 0, stream(), g); break;
-    }
-  }
+  if (!launched) hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP>), grid, dim3(NTHR), 0, stream(), g);
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
   if (n_tail > 0)
     hipLaunchKernelGGL((gemm64_split_reduce<EPI, GROUP>), dim3(n_tail * (TM * TN / 8 / 256)), dim3(256), 0, stream(),
@@ -2237,11 +1659,9 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
     g.ws = ws.data_ptr<float>();
   }
   const int grp = (int)(config % 1000);
-  if (f32_out) {  // fp32 main gradients: the 4-wave, persistent or variant-1 schedule only
-    const int v = (grp / 100) % 10;
-    const int c = (v >= 3 ? v * 100 : 100) + grp % 100;
-    if (accumulate) launch<true, true, EPI_ACC_F32>(g, c);
-    else launch<true, true, EPI_STORE_F32>(g, c);
+  if (f32_out) {  // fp32 main gradients
+    if (accumulate) launch<true, true, EPI_ACC_F32>(g, grp);
+    else launch<true, true, EPI_STORE_F32>(g, grp);
     return;
   }
   const int sel = (at_ ? 4 : 0) | (bt_ ? 2 : 0) | (accumulate ? 1 : 0);
@@ -2297,14 +1717,10 @@ at::Tensor gemm64_swiglu_dgrad(const at::Tensor& dy, const at::Tensor& w, const 
 template <int EPI, int SIDE>
 void launch_side(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
-  if (variant == 9)  // 4-wave kernel, loads interleaved (8/9: DMA inside the MFMA statements)
-    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 3, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
-  else if (variant == 8)
-    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 2, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
-  else if (variant == 6 || variant == 7)
-    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
+  if (variant >= 3)  // the one-shot 4-wave kernel (launch_g's variant map; no persistent side-job kernel)
+    hipLaunchKernelGGL((gemm4w_kernel<true, true, EPI, 4, SIDE>), dim3(n_items), dim3(NT4), 0, stream(), g);
   else
-    hipLaunchKernelGGL((gemm64_kernel<true, true, EPI, 4, 1, SIDE>), dim3(n_items), dim3(NTHR), 0, stream(), g);
+    hipLaunchKernelGGL((gemm64_kernel<true, true, EPI, 4, SIDE>), dim3(n_items), dim3(NTHR), 0, stream(), g);
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
   if (n_tail > 0)
     hipLaunchKernelGGL((gemm64_split_reduce<EPI, 4>), dim3(n_tail * (TM * TN / 8 / 256)), dim3(256), 0, stream(), g);

@@ -235,7 +235,9 @@ def _knob(name: str, value: int):
 
 class Gemm64Tuner(Tunable):
     """gemm64_ex configuration (tile-order group + 100 * schedule variant) for one GEMM of a
-    linear layer: ``layout`` fwd (x W^T), dgrad (dy W) or wgrad (dy^T x) with M tokens."""
+    linear layer: ``layout`` fwd (x W^T), dgrad (dy W) or wgrad (dy^T x) with M tokens.  The
+    schedules: 1xx the 8-wave kernel, 3xx the persistent 4-wave kernel, 9xx the one-shot 4-wave
+    kernel; group 4 or 8 tile-rows per tile-order group."""
 
     LAYOUTS = {"fwd": (False, False), "dgrad": (False, True), "wgrad": (True, True)}
 
@@ -244,7 +246,7 @@ class Gemm64Tuner(Tunable):
         self.dev = _dev(device)
 
     def get_parameter_space(self):
-        return {"config": [4, 8, 104, 108, 204, 304]}
+        return {"config": [104, 108, 304, 308, 904, 908]}
 
     def validate_parameters(self, p):
         return self.dev.type == "cuda" and self.M % 256 == 0 and self.N % 256 == 0 and self.K % 128 == 0

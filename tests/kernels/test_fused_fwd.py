@@ -23,7 +23,7 @@ def _bf(*shape, seed=0, scale=1.0):
 
 @pytest.mark.parametrize("T,K,nq,nkv", [(512, 256, 4, 2), (1024, 384, 2, 2), (2048, 512, 8, 4)])
 @pytest.mark.parametrize("with_pos", [False, True])
-@pytest.mark.parametrize("config", [104, 304, 404, 704, 804, 904])
+@pytest.mark.parametrize("config", [104, 304, 904])
 def test_gemm64_qkv_rope_matches_fp32(native_lib, T, K, nq, nkv, with_pos, config):
     D = 128
     x = _bf(T, K, seed=1)
@@ -47,7 +47,7 @@ def test_gemm64_qkv_rope_matches_fp32(native_lib, T, K, nq, nkv, with_pos, confi
 
 
 @pytest.mark.parametrize("T,K,F", [(256, 256, 128), (512, 384, 384), (1024, 512, 1024)])
-@pytest.mark.parametrize("config", [104, 304, 404, 704, 804, 904])
+@pytest.mark.parametrize("config", [104, 304, 904])
 def test_gemm64_up_swiglu_matches_fp32(native_lib, T, K, F, config):
     x = _bf(T, K, seed=3)
     w = _bf(2 * F, K, seed=4, scale=K ** -0.5)
@@ -111,7 +111,7 @@ def test_decoder_layer_fused_forward_matches_unfused(native_lib, monkeypatch, si
         assert row_err(a2, b2) < 3e-2, n
 
 
-@pytest.mark.parametrize("config", [104, 304, 404, 704, 804, 904])
+@pytest.mark.parametrize("config", [104, 304, 904])
 def test_decoder_layer_all_gemm64_matches_hipblaslt(native_lib, monkeypatch, config):
     """Every projection of the layer on gemm64 (fused RoPE-QKV / up-SwiGLU forward epilogues,
     forward + data gradients with W read K-major, weight gradients, the SwiGLU backward as the

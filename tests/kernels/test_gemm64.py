@@ -27,7 +27,7 @@ TOL = 1.2e-2  # bf16 output rounding is <= 2^-8 of the row max; fp32 accumulatio
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
 @pytest.mark.parametrize("acc", [False, True])
 @pytest.mark.parametrize("split", [0, 1, 2])
-@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [1, 3, 9])
 def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split, variant):
     A = _bf(M, K, seed=71)
     B = _bf(N, K, seed=72)
@@ -41,13 +41,13 @@ def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split, variant):
     assert row_err(out, want) < TOL
 
 
-@pytest.mark.parametrize("config", [4, 8, 104, 108, 204, 304, 504, 508, 1104, 2104, 4008, 8104, 1504, 2504, 8504,
-                                    604, 608, 1604, 2604, 8604, 704, 708, 1704, 2704, 8704,
-                                    804, 808, 1804, 2804, 8804, 904, 908, 1904, 2904, 8904,
-                                    404, 408, 1404, 2404, 8404, 308, 1304, 2304, 8304])
+@pytest.mark.parametrize("config", [4, 8, 104, 108, 1104, 2104, 4008, 8104, 904, 908, 1904, 2904, 8904,
+                                    304, 308, 1304, 2304, 8304, 504])
 def test_gemm64_configs(native_lib, config):
     """Every tile-order group / schedule variant / tail split computes the same product (fwd
-    and wgrad); 1xxx = no split, Sxxx = S K-ranges (24 tiles < one round: all of them split)."""
+    and wgrad); 1xxx = no split, Sxxx = S K-ranges (24 tiles < one round: all of them split).
+    x0xx-x2xx: 8-wave kernel, x3xx: persistent 4-wave, x4xx-x9xx: one-shot 4-wave (504: a
+    retired variant number, aliased)."""
     M, N, K = 1536, 1024, 2048  # 24 tiles: more tiles than one group, several K-tile pairs
     A, B = _bf(M, K, seed=3), _bf(N, K, seed=4)
     want = A.float() @ B.float().t()
@@ -66,8 +66,8 @@ def test_gemm64_split_tail_multi_round(native_lib):
     A, B = _bf(K, M, seed=91), _bf(K, N, seed=92)
     c0 = _bf(M, N, seed=93)
     want = A.float().t() @ B.float()
-    for cfg in (104, 8104, 504, 1504, 8504, 604, 8604, 704, 8704, 804, 8804, 904, 8904, 404, 8404, 304, 1304, 8304):
-        # x5xx: 8-wave persistent; x3xx: 4-wave persistent; x4xx, x6xx-x9xx: 4-wave
+    for cfg in (104, 8104, 904, 8904, 304, 1304, 8304):
+        # x1xx: 8-wave; x3xx: 4-wave persistent; x9xx: 4-wave
         out = c0.clone()
         native_lib.gemm64_ex(A, B, out, True, True, True, cfg)
         assert row_err(out, want + c0.float()) < TOL, cfg
@@ -88,7 +88,7 @@ def test_gemm64_persistent_many_rounds(native_lib, at, bt):
     a = A.t().contiguous() if at else A
     b = B.t().contiguous() if bt else B
     want = A.float() @ B.float().t()
-    for cfg in (504, 1504, 304, 1304, 308):
+    for cfg in (304, 1304, 308):
         out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
         native_lib.gemm64_ex(a, b, out, at, bt, False, cfg)
         assert torch.isfinite(out.float()).all(), cfg
@@ -144,7 +144,7 @@ def test_linear_backward_on_gemm64(native_lib, mode):
 
 
 @pytest.mark.parametrize("M,H,F", [(256, 256, 256), (512, 384, 768), (2304, 1024, 1280)])
-@pytest.mark.parametrize("config", [104, 1104, 2104, 504, 2504])
+@pytest.mark.parametrize("config", [104, 1104, 2104, 904])
 def test_gemm64_swiglu_dgrad(native_lib, M, H, F, config):
     """Down-projection data gradient with the SwiGLU backward in the store epilogue (and in the
     tail-split reduction, config 2104): dgu vs fp32 swiglu_bwd(dy @ W, gu)."""
@@ -179,8 +179,7 @@ def test_swiglu_down_autograd_fused_matches_unfused(native_lib):
         assert row_err(gu.grad, g32.grad) < 2e-2 and row_err(w.grad, w32.grad) < 2e-2
 
 
-@pytest.mark.parametrize("cfg", [104, 504, 2104, 2504, 1504, 604, 2604, 704, 2704, 804, 2804, 904, 2904, 404, 2404,
-                                 304, 1304, 2304])
+@pytest.mark.parametrize("cfg", [104, 2104, 904, 2904, 1904, 304, 1304, 2304])
 def test_gemm64_wgrad_fp32_output(native_lib, cfg):
     """fp32 main gradients: the wgrad layout stores / accumulates an fp32 C (no bf16 rounding of
     the running sum); one-shot and persistent schedules, with and without the split tail."""
@@ -209,12 +208,10 @@ def _swiglu_bwd_ref(dact, gu):
                                        (512, 3072, 2304, 104),   # elements past E (range-checked)
                                        (2048, 4096, 1024, 4104),  # every tile split into 4 K-ranges
                                        (2048, 4096, 1024, 1104),
-                                       (512, 4096, 1024, 704),    # 4-wave kernel: one chunk per K-tile
-                                       (512, 2048, 2048, 704),    # two chunks
-                                       (512, 3072, 2304, 704),    # range-checked tail
-                                       (2048, 4096, 1024, 4704),
-                                       (512, 2048, 2048, 804),
-                                       (512, 2048, 2048, 904),
+                                       (512, 4096, 1024, 904),    # 4-wave kernel: one chunk per K-tile
+                                       (512, 2048, 2048, 904),    # two chunks
+                                       (512, 3072, 2304, 904),    # range-checked tail
+                                       (512, 2048, 2048, 304),    # persistent number: one-shot side kernel
                                        (2048, 4096, 1024, 4904)])
 @pytest.mark.parametrize("gdt,acc", [(torch.bfloat16, False), (torch.bfloat16, True), (torch.float32, False),
                                      (torch.float32, True)])

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""4-wave GEMM (gemm64 config variant 6) vs the 8-wave kernel (104) vs hipBLASLt (TunableOp
+"""4-wave GEMM (gemm64 config variant 9) vs the 8-wave kernel (104) vs hipBLASLt (TunableOp
 solutions) on the GPT-7B training shapes: forward / dgrad / wgrad layouts, random data, TF/s
 (median of interleaved rounds), plus a row-error check of every variant against fp32.
 
-    python tools/gemm4w_bench.py [--tokens 32768] [--configs 104 604]
+    python tools/gemm4w_bench.py [--tokens 32768] [--configs 104 904]
 """
 import argparse
 import json
@@ -34,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=32768)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--configs", type=int, nargs="+", default=[104, 604])
+    ap.add_argument("--configs", type=int, nargs="+", default=[104, 904])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--layouts", nargs="+", default=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--knob", action="append", default=[], help="native knob name=value (repeatable)")
