@@ -35,8 +35,7 @@ ENV = "LLMCTL_KNOBS"
 class PerfKnobs:
     # ---- training GEMM routing (llmctl/exec/linear.py, llmctl/models/transformer.py)
     gemm64: bool = True            # in-house MFMA GEMMs (False: hipBLASLt everywhere -- A/B only)
-    gemm64_config: int = 904       # gemm64 config: tile-order group + 100 * schedule variant + 1000 * split
-    gemm64_fd_config: int = 304    # the same for the forward / data-gradient layouts (0: gemm64_config)
+    gemm64_config: int = 304       # gemm64 config: tile-order group + 100 * schedule variant + 1000 * split
     fwd64: str = "auto"            # forward x W^T on gemm64: auto (small-M / wide shapes) | all | off
     dgrad64: str = "fused"         # data gradients on gemm64: fused (down projection) | all | off
     wgrad_kernel: bool = True      # weight gradients on the MFMA kernels (False: hipBLASLt)

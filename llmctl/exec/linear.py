@@ -35,7 +35,7 @@ import torch.nn.functional as F
 from llmctl.config.knobs import knobs
 
 
-# gemm64_ex config: knobs gemm64_config / gemm64_fd_config (see gemm64_config below).  A tuning cache
+# gemm64_ex config: knob gemm64_config (see gemm64_config below).  A tuning cache
 # (llmctl.plugins.tuning_cache) can override it per layout or per exact shape.
 GEMM64_CONFIGS: dict = {}  # layout -> config
 GEMM64_SHAPE_CONFIGS: dict = {}  # (layout, M, N, K) -> config
@@ -43,14 +43,14 @@ GEMM64_SHAPE_CONFIGS: dict = {}  # (layout, M, N, K) -> config
 
 def gemm64_config(layout: str, M: int, N: int, K: int) -> int:
     """Config of one gemm64 call: a tuning-cache entry for the exact shape or the layout, else
-    knob ``gemm64_fd_config`` (forward / data gradient: the persistent 4-wave kernel, 304) or
-    ``gemm64_config`` (weight gradients: the one-shot 4-wave kernel, 904, which also carries the
-    SwiGLU backward as a side job)."""
+    knob ``gemm64_config`` (default 304: the persistent 4-wave kernel; the down projection's
+    weight gradient with the SwiGLU backward as a side job runs the one-shot 4-wave kernel --
+    3 rounds of bench.py: 1051.9 vs 1053.3 ms/step for 904 on every wgrad,
+    profiles/ab_wgrad_persistent_r4.txt)."""
     c = GEMM64_SHAPE_CONFIGS.get((layout, M, N, K), GEMM64_CONFIGS.get(layout))
     if c is not None:
         return c
-    k = knobs()
-    return k.gemm64_fd_config if layout in ("fwd", "dgrad") and k.gemm64_fd_config else k.gemm64_config
+    return knobs().gemm64_config
 
 
 def _gemm64_enabled() -> bool:

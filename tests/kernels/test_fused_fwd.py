@@ -117,7 +117,7 @@ def test_decoder_layer_all_gemm64_matches_hipblaslt(native_lib, monkeypatch, con
     forward + data gradients with W read K-major, weight gradients, the SwiGLU backward as the
     down wgrad's side job at hidden 4096 / ffn 1024) against the library path (hipBLASLt
     forward / data gradients, unfused RoPE / SwiGLU), forward and every gradient."""
-    knobs = {"gemm64_config": config, "gemm64_fd_config": config, "fwd64": "all", "dgrad64": "all"}
+    knobs = {"gemm64_config": config, "fwd64": "all", "dgrad64": "all"}
     dims = (4096, 32, 8, 1024)
     out_f, g_f = _layer_grads(True, monkeypatch, True, knobs, dims)
     out_u, g_u = _layer_grads(False, monkeypatch, True, {"gemm64": False, "wgrad_kernel": False}, dims)
