@@ -12,7 +12,7 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE"; do
   for kind in ${KINDS:-fwd dkv dq}; do
     i=$((i+1))
-    timeout -k 10 -s KILL 90 rocprofv3 --pmc $set -d $R/gpurun_out/pmcattn2/$kind.$i -o run --output-format csv -- python3 $R/tools/attn_one.py $kind 5 12 2048 32 128 > $R/gpurun_out/pmcattn2/$kind.$i.log 2>&1 || { echo "fail $kind $set"; tail -5 $R/gpurun_out/pmcattn2/$kind.$i.log; exit 1; }
+    timeout -k 10 -s KILL 90 rocprofv3 --pmc $set -d $R/gpurun_out/pmcattn2/$kind.$i -o run --output-format csv -- python3 $R/tools/attn_one.py $kind 5 ${ABL_B:-16} 2048 32 128 > $R/gpurun_out/pmcattn2/$kind.$i.log 2>&1 || { echo "fail $kind $set"; tail -5 $R/gpurun_out/pmcattn2/$kind.$i.log; exit 1; }
   done
 done
 cd $R && python tools/pmc_summary.py gpurun_out/pmcattn2 fa_ > gpurun_out/pmcattn2_summary.txt 2>&1; cat gpurun_out/pmcattn2_summary.txt
