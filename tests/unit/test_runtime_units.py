@@ -375,3 +375,20 @@ def test_hw_network_benchmark_gloo_rehearsal():
     r = _bench_network(ranks=2, backend="gloo", sizes=(4096,), patterns=("allreduce", "all_gather"), iters=2)
     assert r["status"] == "ok" and len(r["results"]) == 2
     assert all(x["busbw_gbps"] is not None and x["time_ms"] > 0 for x in r["results"])
+
+
+def test_gemm64_default_config_single_knob(monkeypatch):
+    """Without a tuning cache every layout uses knob gemm64_config (default 304, the persistent
+    4-wave kernel); an override moves all layouts together."""
+    import importlib
+
+    linear = importlib.import_module("llmctl.exec.linear")
+    from llmctl.config.knobs import PerfKnobs, override
+
+    monkeypatch.setattr(linear, "GEMM64_CONFIGS", {})
+    monkeypatch.setattr(linear, "GEMM64_SHAPE_CONFIGS", {})
+    assert PerfKnobs().gemm64_config == 304
+    with override(gemm64_config=304):
+        assert {linear.gemm64_config(l, 4096, 4096, 4096) for l in ("fwd", "dgrad", "wgrad")} == {304}
+    with override(gemm64_config=904):
+        assert {linear.gemm64_config(l, 4096, 4096, 4096) for l in ("fwd", "dgrad", "wgrad")} == {904}
