@@ -10,7 +10,10 @@ one could not be reproduced from its manifest.  Here every *performance* choice 
 :func:`apply` makes a resolved record the process-wide active one (``knobs()``), pushes the
 native ones into the HIP library's knob table (``torch.ops.llmctl.set_knob``, read by the
 launchers in ``llmctl/ops/csrc``) and is called by the training and serving engines at init;
-the run manifest and checkpoints record ``asdict(knobs())`` so ``llmctl replay`` restores them.
+the run manifest (``run_manifest.json: perf_knobs``) and every checkpoint's
+``training_state.json`` record ``asdict`` of the engine's resolved knobs, so ``llmctl replay``
+restores them.  Each engine keeps its own resolved record (``engine.knobs``) and re-activates it
+(:func:`use`) on entry to its hot paths.
 
 The remaining environment variables are debugging aids only (``LLMCTL_DEBUG``,
 ``LLMCTL_HANG_DUMP``, ``LLMCTL_FAULT``, ``LLMCTL_STREAM_CHECK``, ``LLMCTL_SANITIZE``,
@@ -107,8 +110,25 @@ def parse_env(spec: Optional[str]) -> Dict[str, Any]:
     return out
 
 
+# per-feature variables of rounds 1-3 that are now knobs (LLMCTL_<NAME> for a knob NAME, plus these)
+_RETIRED_ENV = ("LLMCTL_SIDE_DGRAD", "LLMCTL_DECODE_ATTN_QKV", "LLMCTL_GEMM64_CONFIG", "LLMCTL_SKINNY")
+_warned: set = set()
+
+
+def _warn_retired_env() -> None:
+    import warnings
+
+    names = [f"LLMCTL_{n.upper()}" for n in _FIELDS] + list(_RETIRED_ENV)
+    for n in names:
+        if n in os.environ and n not in _warned:
+            _warned.add(n)
+            warnings.warn(f"{n} is no longer read (performance switches are knobs now): set "
+                          f"{ENV}=\"{n[7:].lower()}=<value>\" or the [perf] config table instead", stacklevel=3)
+
+
 def resolve(overrides: Optional[Dict[str, Any]] = None, env: bool = True) -> PerfKnobs:
     """Defaults < ``overrides`` (config) < ``LLMCTL_KNOBS`` (when ``env``)."""
+    _warn_retired_env()
     kw = {k: _coerce(k, v) for k, v in (overrides or {}).items()}
     if env:
         kw.update(parse_env(os.environ.get(ENV)))
@@ -145,6 +165,23 @@ def apply(k: PerfKnobs) -> PerfKnobs:
     _ACTIVE = k
     push_native(k)
     return k
+
+
+def use(k: PerfKnobs) -> PerfKnobs:
+    """Make an engine's own resolved knobs the active ones (no-op when they already are).  Engines
+    call this on entry to their step / prefill / decode paths, so a second engine built in the
+    same process (with other ``perf_knobs``) does not change the first one's kernel routing or
+    the knob state its hipGraphs are captured under."""
+    if k is not _ACTIVE:
+        apply(k)
+    return k
+
+
+def with_env(k: PerfKnobs) -> PerfKnobs:
+    """Re-apply the ``LLMCTL_KNOBS`` overrides on top of ``k`` (they stay highest in precedence
+    when a tuning cache refines the config-resolved knobs)."""
+    env = parse_env(os.environ.get(ENV))
+    return dataclasses.replace(k, **env) if env else k
 
 
 def configure(overrides: Optional[Dict[str, Any]] = None) -> PerfKnobs:

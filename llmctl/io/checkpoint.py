@@ -130,8 +130,16 @@ class CheckpointManager:
         pg = e.pg
         rank = pg.rank
         world = pg.layout.world_size
+        # save id: markers from an earlier, interrupted save of the same checkpoint (a rank killed
+        # mid-write, then an elastic restart that saves this step again) carry another id and are
+        # never counted toward this save's commit
+        save_id = f"{e.global_step}:{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}:{os.environ.get('TORCHELASTIC_RUN_ID', '')}"
         if e.is_main:
             path.mkdir(parents=True, exist_ok=True)
+            # before the barrier, so no rank of this save has written a marker yet: a stale
+            # marker set and a stale commit record must not survive into this save
+            shutil.rmtree(path / ".done", ignore_errors=True)
+            (path / "training_state.json").unlink(missing_ok=True)
         if dist.is_initialized():
             dist.barrier()
         path.mkdir(parents=True, exist_ok=True)
@@ -158,6 +166,8 @@ class CheckpointManager:
             "scheduler": e.scheduler.state_dict(), "consumed_samples": e.consumed_samples,
             "world_size": world, "layout": {"tp": pg.layout.tp, "pp": pg.layout.pp, "dp": pg.layout.dp, "cp": pg.layout.cp},
             "zero_stage": c.zero_stage,
+            # the resolved performance knobs this run trained under (replay restores them)
+            "perf_knobs": e.knobs.as_dict() if getattr(e, "knobs", None) is not None else None,
         }
 
         timeout = float(getattr(c, "collective_timeout_s", 1800) or 1800)
@@ -178,9 +188,9 @@ class CheckpointManager:
                 (path / "rng").mkdir(exist_ok=True)
                 torch.save(rng, path / "rng" / f"rank_{rank:05d}.pt")
                 (path / ".done").mkdir(exist_ok=True)
-                (path / ".done" / f"rank_{rank:05d}").write_text("")
+                (path / ".done" / f"rank_{rank:05d}").write_text(save_id)
                 if e.is_main:
-                    self._commit(path, state, n_shards, world, timeout)
+                    self._commit(path, state, n_shards, world, timeout, save_id)
             except BaseException as ex:  # surfaced by wait()
                 self._error = ex
 
@@ -192,7 +202,8 @@ class CheckpointManager:
             self.wait()
         return path
 
-    def _commit(self, path: Path, state: Dict[str, Any], n_shards: int, world: int, timeout: float) -> None:
+    def _commit(self, path: Path, state: Dict[str, Any], n_shards: int, world: int, timeout: float,
+                save_id: str = "") -> None:
         """Rank 0, off the training thread: once every rank's done-marker exists (each rank
         writes its marker after its own shards), write the metadata and move ``latest``.
 
@@ -203,7 +214,16 @@ class CheckpointManager:
         e = self.engine
         done = path / ".done"
         deadline = time.time() + timeout
-        while len(list(done.glob("rank_*"))) < world:
+        def _ready() -> int:
+            n = 0
+            for m in done.glob("rank_*"):
+                try:
+                    n += m.read_text() == save_id
+                except OSError:  # being written
+                    pass
+            return n
+
+        while _ready() < world:
             if time.time() > deadline:
                 raise TimeoutError(f"checkpoint {path}: not every rank finished writing within {timeout:.0f} s")
             time.sleep(0.05)
@@ -254,7 +274,15 @@ class CheckpointManager:
         e = self.engine
         p = Path(path)
         if p.is_dir() and (p / "latest").exists() and not (p / "training_state.json").exists():
+            root = p
             p = p / (p / "latest").read_text().strip()
+            if not (p / "training_state.json").exists():
+                # ``latest`` names a checkpoint whose re-save was interrupted (its commit record is
+                # removed before the rewrite): fall back to the newest complete one
+                done = [d for d in root.iterdir() if d.is_dir() and (d / "training_state.json").exists()]
+                if not done:
+                    raise FileNotFoundError(f"{root}: no complete checkpoint")
+                p = max(done, key=lambda d: json.loads((d / "training_state.json").read_text()).get("global_step", -1))
         state = json.loads((p / "training_state.json").read_text())
         e.optimizer.wait_params()
         full = load_full_state_dict(p, e.model_config)

@@ -123,9 +123,6 @@ struct G64Args {
   // range (no memory traffic), 2 = no workgroup barriers, 4 = no epilogue, 8 = every tile loads
   // tile (0, 0)'s operands (L2-resident), 16 = every K-tile loads K-tile 0
   int probe = 0;
-  // persistent kernel: retire an item's epilogue stores before the next item's first DMA (the
-  // undrained form measured intermittent wrong rows; native knob gemm_p3_drain)
-  int p3_drain = 1;
 };
 
 // SwiGLU backward of one element: d = dL/dact, act = silu(g) * u
@@ -1478,7 +1475,15 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     if (!has_next) wait_vm<0>();  // the re-loads of the last item's K-tiles 0 / 1 are still landing
     g4w_epilogue<EPI>(args, acc, c_tm, c_tn, wr, wc, lane, c_sp, c_u);
     if (!has_next) break;
-    if (args.p3_drain) wait_vm<0>();
+    // vmcnt accounting at an item boundary: the stream slots of the last two K-tiles already hold
+    // the next item's K-tiles 0 / 1 (16 DMA pieces), and the epilogue adds its 32 stores behind
+    // them.  vmcnt counts loads and stores together but they RETIRE out of order, so a counted
+    // wait (the next item's first wait_vm<20>, which assumes only DMA pieces are younger) could
+    // pass while the K-tile 0 pieces have not landed.  Draining here makes every later count
+    // exact again: the first fragment reads of the next item then see landed data (this wait
+    // costs one DMA latency per item, ~0.3 % at K = 4096).  Unconditional: the undrained form
+    // gave intermittent wrong rows.
+    wait_vm<0>();
     g += (int)gridDim.x;
     c_tm = n_tm, c_tn = n_tn, c_sp = n_sp, c_u = n_u, c_KT = n_KT, c_kt0 = n_kt0;
     c_ra = n_ra, c_rb = n_rb, c_rbh = n_rbh;
@@ -1651,7 +1656,6 @@ void gemm64_ex(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, bool a
             reinterpret_cast<unsigned short*>(out.data_ptr()), a.stride(0), b.stride(0), out.stride(0),
             (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr, nullptr};
   g.probe = (int)knob("gemm_probe", 0);
-  g.p3_drain = (int)knob("gemm_p3_drain", 1);
   plan_split(g, (int)(config / 1000));
   at::Tensor ws;
   if (g.splits > 1) {

@@ -110,7 +110,8 @@ def _set_knobs(**kw) -> None:
 
     from llmctl.config import knobs as K
 
-    K.apply(dataclasses.replace(K.knobs(), **kw))
+    # LLMCTL_KNOBS stays highest in precedence: re-applied over the tuned values
+    K.apply(K.with_env(dataclasses.replace(K.knobs(), **kw)))
 
 
 def apply_serving(path) -> Dict[str, Any]:

@@ -23,7 +23,6 @@ import torch
 import torch.distributed as dist
 
 from llmctl.comms.overlap import GradSyncEngine
-from llmctl.config.knobs import knobs
 from llmctl.models import ModelConfig, ParallelContext, build_model, get_model_config
 from llmctl.parallel.groups import ProcessGroups, build_process_groups
 from llmctl.runtime.faults import FaultInjector
@@ -133,6 +132,7 @@ class TrainingEngine:
         self.tuned = tuning_cache.apply_training(tc, c) if tc is not None else {}
         if self.tuned:
             log.info("tuning cache %s applied: %s", tc, self.tuned)
+        self.knobs = perf.knobs()  # config + tuning cache + LLMCTL_KNOBS
         self.global_step = 0
         self.epoch = 0
         self.consumed_samples = 0
@@ -288,7 +288,7 @@ class TrainingEngine:
         if self.zero3 is None and self.optimizer.zero_stage >= 1 and dp > 1:
             self._install_param_gather_hooks()
         elif (self.zero3 is None and self.optimizer.zero_stage == 0 and self.device.type == "cuda" and pp == 1
-              and knobs().overlap_optimizer):
+              and self.knobs.overlap_optimizer):
             # opt-in: measured neutral on GPT-7B mb 12 (27.7k vs 27.9k tok/s in one A/B,
             # profiles/bench_r1_overlap_opt_ab.jsonl) — the concurrent AdamW slows the GEMMs
             # about as much as it hides
@@ -395,6 +395,9 @@ class TrainingEngine:
     def train_step(self, batches: List[Tuple[torch.Tensor, torch.Tensor]]) -> Dict[str, torch.Tensor]:
         """One optimizer step over ``len(batches)`` micro-batches (grad accumulation).  Returns
         device tensors (no host sync): mean loss and grad norm."""
+        from llmctl.config.knobs import use
+
+        use(self.knobs)
         self.model.train()
         c = self.config
         # with the side-stream update the previous step may still be reading the gradients:
@@ -497,6 +500,9 @@ class TrainingEngine:
         from llmctl.io.checkpoint import CheckpointManager
         from llmctl.runtime.replay import write_manifest
 
+        from llmctl.config.knobs import use
+
+        use(self.knobs)
         c = self.config
         ckpt = CheckpointManager(self, c.output_dir)
         resume = c.resume_from_checkpoint

@@ -1,0 +1,305 @@
+"""TP serving control plane: rank 0's per-step plan to the other TP ranks without pickling.
+
+Every engine step of :class:`llmctl.serve.tp.TPInferenceEngine` ships a plan (token ids,
+positions, KV slots, block tables, ...) from rank 0 to the other ranks.  Round 4 sent it with
+``dist.broadcast_object_list`` over gloo: a pickle on rank 0, a size broadcast plus a payload
+broadcast through TCP, an unpickle on every rank -- per decode step, on every rank.
+
+Here a plan is packed into a fixed-layout byte record (:func:`pack` / :func:`unpack`: a small
+header per field -- key, kind, dtype, shape -- and the raw array bytes; nested dicts are
+flattened to ``a/b`` keys) and moved through one of two channels:
+
+* :class:`ShmChannel` (one node, the TP serving case): a ring of slots in a ``/dev/shm`` file
+  mapped by every rank.  Rank 0 writes the record into slot ``seq % SLOTS`` and publishes
+  ``seq`` in the slot header last; readers poll that word (spin, then back off to short
+  sleeps when idle) and acknowledge ``seq`` in their own header word, which rank 0 checks
+  before it reuses a slot.  No syscall or socket on the hot path: a decode step's plan costs a
+  few microseconds per rank (``tools/tp_control_bench.py``, ``profiles/tp_control_r5.txt``).
+* :class:`TensorChannel` (fallback: multi-node groups, or a plan larger than a slot): two gloo
+  broadcasts of uint8 tensors (length, then bytes) -- still no pickle.
+
+Reference: the reference server runs one process and has no TP control plane
+(``/root/reference/llmctl/serve/server.py:372-386``).
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import struct
+import time
+import uuid
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+# ---------------------------------------------------------------------------- record codec
+_KIND_NONE, _KIND_ARRAY, _KIND_LIST, _KIND_INT, _KIND_STR, _KIND_BOOL, _KIND_FLOAT, _KIND_DICT = range(8)
+_DTYPES = [np.dtype(t) for t in ("int64", "int32", "int16", "int8", "uint8", "bool", "float32", "float64", "uint32")]
+_DT_CODE = {d: i for i, d in enumerate(_DTYPES)}
+_HDR = struct.Struct("<HBBBxxx")  # key length, kind, dtype code, ndim
+
+
+def _flatten(d: Dict[str, Any], prefix: str, out: List[Tuple[str, Any]]) -> None:
+    for k, v in d.items():
+        key = prefix + k
+        if isinstance(v, dict):
+            out.append((key, _KIND_DICT))
+            _flatten(v, key + "/", out)
+        else:
+            out.append((key, v))
+
+
+# decode steps (the per-token hot path) have a fixed layout: [magic, n, mb] then ids / positions /
+# slots / ctx as int64 rows and the [n, mb] int32 block table -- one conversion, one copy
+_DECODE_MAGIC = 0x0DEC0DE1
+_DECODE_KEYS = {"op", "ids", "positions", "slots", "ctx", "bt"}
+_DECODE_KEYS_STAMPED = _DECODE_KEYS | {"stamp"}  # + a float timestamp (tools/tp_control_bench.py)
+
+
+def _pack_decode(plan: Dict[str, Any]) -> bytes:
+    bt = np.ascontiguousarray(plan["bt"], dtype=np.int32)
+    n = len(plan["ids"])
+    head = np.empty(4 + 4 * n, dtype=np.int64)
+    head[0], head[1], head[2] = _DECODE_MAGIC, n, bt.shape[1] if bt.ndim == 2 else 0
+    head[3:4].view(np.float64)[0] = plan.get("stamp", float("nan"))
+    for i, k in enumerate(("ids", "positions", "slots", "ctx")):
+        head[4 + i * n: 4 + (i + 1) * n] = plan[k]
+    return head.tobytes() + bt.tobytes()
+
+
+def _unpack_decode(buf) -> Dict[str, Any]:
+    a = np.frombuffer(buf, dtype=np.int64, count=4)
+    n, mb = int(a[1]), int(a[2])
+    rows = np.frombuffer(buf, dtype=np.int64, count=4 * n, offset=32).reshape(4, n).copy()
+    bt = np.frombuffer(buf, dtype=np.int32, count=n * mb, offset=32 + 32 * n).reshape(n, mb).copy()
+    out = {"op": "decode", "ids": rows[0], "positions": rows[1], "slots": rows[2], "ctx": rows[3], "bt": bt}
+    stamp = float(a[3:4].view(np.float64)[0])
+    if stamp == stamp:
+        out["stamp"] = stamp
+    return out
+
+
+def pack(plan: Dict[str, Any]) -> bytes:
+    """Plan dict -> bytes.  Values: None, bool, int, float, str, list of ints (round-trips as a
+    list), numpy arrays (int / bool / float dtypes, any shape), nested dicts.  Decode plans use a
+    fixed layout (their lists come back as int64 arrays)."""
+    if plan.get("op") == "decode" and (plan.keys() == _DECODE_KEYS or plan.keys() == _DECODE_KEYS_STAMPED):
+        return _pack_decode(plan)
+    items: List[Tuple[str, Any]] = []
+    _flatten(plan, "", items)
+    parts: List[bytes] = [struct.pack("<I", len(items))]
+    for key, v in items:
+        kb = key.encode()
+        if v is _KIND_DICT:
+            parts += [_HDR.pack(len(kb), _KIND_DICT, 0, 0), kb]
+            continue
+        if v is None:
+            parts += [_HDR.pack(len(kb), _KIND_NONE, 0, 0), kb]
+        elif isinstance(v, (bool, np.bool_)):
+            parts += [_HDR.pack(len(kb), _KIND_BOOL, 0, 0), kb, struct.pack("<q", int(v))]
+        elif isinstance(v, (int, np.integer)):
+            parts += [_HDR.pack(len(kb), _KIND_INT, 0, 0), kb, struct.pack("<q", int(v))]
+        elif isinstance(v, (float, np.floating)):
+            parts += [_HDR.pack(len(kb), _KIND_FLOAT, 0, 0), kb, struct.pack("<d", float(v))]
+        elif isinstance(v, str):
+            sb = v.encode()
+            parts += [_HDR.pack(len(kb), _KIND_STR, 0, 0), kb, struct.pack("<q", len(sb)), sb]
+        else:
+            kind = _KIND_ARRAY if isinstance(v, np.ndarray) else _KIND_LIST
+            a = np.ascontiguousarray(v if kind == _KIND_ARRAY else np.asarray(v, dtype=np.int64))
+            if a.dtype not in _DT_CODE:
+                raise TypeError(f"plan field {key!r}: unsupported dtype {a.dtype}")
+            parts += [_HDR.pack(len(kb), kind, _DT_CODE[a.dtype], a.ndim), kb,
+                      struct.pack(f"<{a.ndim}q", *a.shape), a.tobytes()]
+    return b"".join(parts)
+
+
+def unpack(buf) -> Dict[str, Any]:
+    """bytes / uint8 view -> plan dict (arrays are copies, safe after the slot is reused)."""
+    mv = memoryview(buf)
+    if len(mv) >= 24 and struct.unpack_from("<q", mv, 0)[0] == _DECODE_MAGIC:
+        return _unpack_decode(mv)
+    (n,) = struct.unpack_from("<I", mv, 0)
+    off = 4
+    out: Dict[str, Any] = {}
+    for _ in range(n):
+        klen, kind, dt, ndim = _HDR.unpack_from(mv, off)
+        off += _HDR.size
+        key = bytes(mv[off:off + klen]).decode()
+        off += klen
+        *path, leaf = key.split("/")
+        d = out
+        for p in path:
+            d = d[p]
+        if kind == _KIND_DICT:
+            d[leaf] = {}
+        elif kind == _KIND_NONE:
+            d[leaf] = None
+        elif kind in (_KIND_INT, _KIND_BOOL):
+            (x,) = struct.unpack_from("<q", mv, off)
+            off += 8
+            d[leaf] = bool(x) if kind == _KIND_BOOL else x
+        elif kind == _KIND_FLOAT:
+            (x,) = struct.unpack_from("<d", mv, off)
+            off += 8
+            d[leaf] = x
+        elif kind == _KIND_STR:
+            (ln,) = struct.unpack_from("<q", mv, off)
+            off += 8
+            d[leaf] = bytes(mv[off:off + ln]).decode()
+            off += ln
+        else:
+            shape = struct.unpack_from(f"<{ndim}q", mv, off)
+            off += 8 * ndim
+            dtype = _DTYPES[dt]
+            nb = math.prod(shape) * dtype.itemsize
+            a = np.frombuffer(mv[off:off + nb], dtype=dtype).reshape(shape).copy()
+            off += nb
+            d[leaf] = a.tolist() if kind == _KIND_LIST else a
+    return out
+
+
+# ---------------------------------------------------------------------------- channels
+class TensorChannel:
+    """Packed plans over two gloo broadcasts (length, bytes); any group, any node count."""
+
+    def __init__(self, group, src_rank: int = 0):
+        self.group = group
+        self.src = dist.get_global_rank(group, src_rank) if group is not None else src_rank
+        self.rank = dist.get_rank(group)
+
+    def publish(self, plan: Dict[str, Any]) -> None:
+        b = pack(plan)
+        n = torch.tensor([len(b)], dtype=torch.int64)
+        dist.broadcast(n, self.src, group=self.group)
+        dist.broadcast(torch.frombuffer(bytearray(b), dtype=torch.uint8), self.src, group=self.group)
+
+    def publish_bytes(self, b: bytes) -> None:
+        n = torch.tensor([len(b)], dtype=torch.int64)
+        dist.broadcast(n, self.src, group=self.group)
+        dist.broadcast(torch.frombuffer(bytearray(b), dtype=torch.uint8), self.src, group=self.group)
+
+    def receive(self) -> Dict[str, Any]:
+        n = torch.zeros(1, dtype=torch.int64)
+        dist.broadcast(n, self.src, group=self.group)
+        buf = torch.empty(int(n.item()), dtype=torch.uint8)
+        dist.broadcast(buf, self.src, group=self.group)
+        return unpack(buf.numpy().tobytes())
+
+    def close(self) -> None:
+        pass
+
+
+class ShmChannel:
+    """Single-writer ring in a ``/dev/shm`` file (one node).  Layout (bytes):
+
+    ``[0, 64 * 32)``        per-reader ack words (u64, one 64-B line each; index = group rank)
+    ``[2048, ...)``         SLOTS slots of ``slot_bytes``: [u64 seq][u64 nbytes][u64 spill][pad
+                            to 64][record]
+
+    A plan that does not fit a slot is published with ``spill = 1`` and its bytes follow through
+    the gloo :class:`TensorChannel` (same order on every rank)."""
+
+    SLOTS = 4
+    HDR = 2048
+    SLOT_HDR = 64
+
+    def __init__(self, group, slot_bytes: int = 8 << 20, path: Optional[str] = None, poll_spin_s: float = 2e-3):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > 32:
+            raise ValueError("ShmChannel: at most 32 ranks")
+        self.slot_bytes = slot_bytes
+        self.poll_spin_s = poll_spin_s
+        self.fallback = TensorChannel(group)
+        box = [None]
+        if self.rank == 0:
+            path = path or f"/dev/shm/llmctl-tp-{uuid.uuid4().hex[:16]}"
+            size = self.HDR + self.SLOTS * slot_bytes
+            with open(path, "wb") as f:
+                f.truncate(size)
+            box[0] = path
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        self.path = box[0]
+        import mmap
+
+        with open(self.path, "r+b") as f:
+            self._mmap = mmap.mmap(f.fileno(), self.HDR + self.SLOTS * slot_bytes)
+        self.mm = np.frombuffer(self._mmap, dtype=np.uint8)  # plain ndarray views: no memmap overhead
+        self.u64 = self.mm.view(np.uint64)
+        self._ack_idx = np.arange(1, self.world, dtype=np.int64) * 8
+        self.seq = 0
+        dist.barrier(group=group)  # every rank mapped the file before rank 0 may unlink it
+        if self.rank == 0:
+            os.unlink(self.path)  # the mappings keep it alive; nothing leaks if a rank dies
+        self.stats = {"published": 0, "spilled": 0}
+
+    def _slot(self, seq: int) -> int:
+        return self.HDR + (seq % self.SLOTS) * self.slot_bytes
+
+    def _ack_min(self) -> int:
+        return int(self.u64[self._ack_idx].min()) if self.world > 1 else self.seq
+
+    def publish(self, plan: Dict[str, Any]) -> None:
+        b = pack(plan)
+        self.seq += 1
+        s = self.seq
+        base = self._slot(s)
+        t0 = time.perf_counter()
+        while s - self._ack_min() > self.SLOTS:  # slot still unread by some rank
+            if time.perf_counter() - t0 > self.poll_spin_s:
+                time.sleep(1e-5)
+        spill = len(b) > self.slot_bytes - self.SLOT_HDR
+        w = base // 8
+        if not spill:
+            self.mm[base + self.SLOT_HDR: base + self.SLOT_HDR + len(b)] = np.frombuffer(b, dtype=np.uint8)
+        self.u64[w + 1] = len(b)
+        self.u64[w + 2] = 1 if spill else 0
+        self.u64[w] = s  # published last (x86-64 keeps store order)
+        self.stats["published"] += 1
+        if spill:
+            self.stats["spilled"] += 1
+            self.fallback.publish_bytes(b)
+
+    def receive(self) -> Dict[str, Any]:
+        self.seq += 1
+        s = self.seq
+        base = self._slot(s)
+        w = base // 8
+        t0 = time.perf_counter()
+        idle = 0
+        while int(self.u64[w]) != s:
+            el = time.perf_counter() - t0
+            if el > self.poll_spin_s:  # idle server: back off (50 us, then 1 ms sleeps)
+                idle += 1
+                time.sleep(1e-3 if el > 0.5 else 5e-5)
+            else:
+                os.sched_yield()  # spinning, but never starve the ranks that share this CPU
+        n = int(self.u64[w + 1])
+        if int(self.u64[w + 2]):
+            plan = self.fallback.receive()
+        else:
+            plan = unpack(self.mm[base + self.SLOT_HDR: base + self.SLOT_HDR + n].tobytes())
+        self.u64[8 * self.rank] = s  # ack: the slot may be reused
+        return plan
+
+    def close(self) -> None:
+        if self.mm is not None:
+            del self.u64
+            self.mm = None
+            try:
+                self._mmap.close()
+            except BufferError:  # an unpacked view still alive somewhere: the mapping dies with it
+                pass
+
+
+def make_channel(group, kind: str = "auto"):
+    """``shm`` when every rank of ``group`` is on this node (TP serving), else gloo tensors."""
+    if kind == "auto":
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+        kind = "shm" if dist.get_world_size(group) <= local and os.path.isdir("/dev/shm") else "tensor"
+    return ShmChannel(group) if kind == "shm" else TensorChannel(group)

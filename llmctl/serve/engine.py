@@ -33,7 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from llmctl import ops
-from llmctl.config.knobs import knobs
+from llmctl.config.knobs import use as use_knobs
 from llmctl.io.artifact import load_model
 from llmctl.models import DecoderLM
 
@@ -69,6 +69,7 @@ class InferenceEngine:
 
         tc = _tc.resolve(tuning_cache)
         self.tuned = _tc.apply_serving(tc) if tc is not None else {}
+        self.knobs = perf.knobs()  # perf_knobs + tuning cache + LLMCTL_KNOBS: this engine's routing
         self.dtype = dtype
         self.model_path = model_path
         self.model: DecoderLM
@@ -224,6 +225,7 @@ class InferenceEngine:
 
     @torch.inference_mode()
     def prefill_exec(self, plan: Dict) -> torch.Tensor:
+        use_knobs(self.knobs)
         d = self.device
         T = len(plan["ids"])
         ids = torch.from_numpy(plan["ids"]).to(d, non_blocking=True)
@@ -237,7 +239,7 @@ class InferenceEngine:
         # from the RoPE pass (16 x 2k burst TTFT p50 224.6 -> 218.6 ms, single 2k prompt 27.5 ->
         # 26.2 ms, profiles/serve_r2_session6.txt); knob prefill_fa off keeps the paged kernel
         doc = None
-        fa = plan.get("doc") is not None and d.type == "cuda" and knobs().prefill_fa
+        fa = plan.get("doc") is not None and d.type == "cuda" and self.knobs.prefill_fa
         if fa and len(plan["cu"]) > 2:  # several prompts packed: document boundaries
             doc = torch.from_numpy(plan["doc"]).to(d, non_blocking=True).view(1, T)
         # (one prompt: plain causal attention, which also lets the kernel split the K/V range of
@@ -284,6 +286,7 @@ class InferenceEngine:
         kernel.  Returns logits [n_final_chunks + n_decode, V]: the final chunks' rows first, in
         chunk order, then the decode rows (eager: the graph-captured decode step is for
         decode-only steps).  Reference batching: ``llmctl/serve/server.py:89-125, 372-386``."""
+        use_knobs(self.knobs)
         d = self.device
         pp, dp = plan["prefill"], plan["decode"]
         Tp, Td = len(pp["ids"]), len(dp["ids"])
@@ -296,7 +299,7 @@ class InferenceEngine:
         work = torch.tensor(pp["work"], dtype=torch.int32).to(d, non_blocking=True)
         bt_d = torch.from_numpy(dp["bt"]).to(d, non_blocking=True)
         ctx_d = torch.tensor(dp["ctx"], dtype=torch.int32).to(d, non_blocking=True)
-        fa = pp.get("doc") is not None and d.type == "cuda" and knobs().prefill_fa
+        fa = pp.get("doc") is not None and d.type == "cuda" and self.knobs.prefill_fa
         doc = torch.from_numpy(pp["doc"]).to(d, non_blocking=True).view(1, Tp) if fa and len(pp["cu"]) > 2 else None
         x = self._embed(ids, pos.long())
         res = None
@@ -327,7 +330,7 @@ class InferenceEngine:
 
     def _mixed_ok(self) -> bool:
         """Knob ``mixed_steps`` off runs a step's decode and prefill as two forwards (A/B)."""
-        return knobs().mixed_steps
+        return self.knobs.mixed_steps
 
     # ------------------------------------------------------------------ decode
     def _fused_decode(self) -> bool:
@@ -342,7 +345,7 @@ class InferenceEngine:
                 and cfg.gated_mlp
                 and not cfg.is_moe and m.final_norm_b is None
                 and all(l.attn_norm_b is None and l.mlp_norm_b is None for l in m.layers)
-                and knobs().decode_fused)
+                and self.knobs.decode_fused)
 
     def _decode_body(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
         if self._fused_decode():
@@ -444,6 +447,7 @@ class InferenceEngine:
 
     @torch.inference_mode()
     def decode_exec(self, plan: Dict) -> torch.Tensor:
+        use_knobs(self.knobs)
         ids, positions, slots, ctx, bt = plan["ids"], plan["positions"], plan["slots"], plan["ctx"], plan["bt"]
         n = len(ids)
         self.stats["decode_tokens"] += n
@@ -520,6 +524,7 @@ class InferenceEngine:
 
     def step(self) -> int:
         """One scheduling iteration; returns the number of tokens produced."""
+        use_knobs(self.knobs)
         out = self.scheduler.schedule()
         produced = 0
         if out.decode and out.prefill and self._mixed_ok():

@@ -26,7 +26,6 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
-from llmctl.config.knobs import knobs
 from llmctl.models import ParallelContext
 from llmctl.utils.env import dist_env
 
@@ -47,15 +46,22 @@ class TPInferenceEngine(InferenceEngine):
         self.control = control_group if control_group is not None else dist.new_group(backend="gloo")
         self._closed = False
         self._car_checks = 0
+        # plan channel (created on first use by every rank in the same order): "auto" = shm ring
+        # on one node, gloo tensors otherwise; "tensor" / "shm" force one
+        self.control_kind = kw.pop("control", "auto")
+        self.channel = None
         pc = ParallelContext(tp_group=tp_group, tp_size=self.tp_size, tp_rank=self.tp_rank)
-        if kw.get("use_graphs", True) and not knobs().tp_graphs:
+        # this engine's own knobs (perf_knobs + LLMCTL_KNOBS) decide, not whatever is active
+        from llmctl.config.knobs import resolve
+
+        if kw.get("use_graphs", True) and not resolve(kw.get("perf_knobs")).tp_graphs:
             kw["use_graphs"] = False
         self.car = None
         super().__init__(model_path, pc=pc, **kw)
         # decode-sized all-reduces go through the one-shot xGMI kernel (llmctl.comms.custom_ar);
         # prefill-sized ones and CPU runs stay on RCCL / gloo
         if (self.device.type == "cuda" and self.tp_size > 1
-                and knobs().custom_ar):
+                and self.knobs.custom_ar):
             from llmctl.comms.custom_ar import CustomAllReduce
 
             # one-shot up to 4 MB (decode), two-shot up to 32 MB (2k-token prefill chunks at d = 8192)
@@ -96,7 +102,7 @@ class TPInferenceEngine(InferenceEngine):
         return x
 
     def _fused_reduce_ok(self) -> bool:
-        return self.car is not None and knobs().tp_fused_decode
+        return self.car is not None and self.knobs.tp_fused_decode
 
     def _reduce_add_rmsnorm(self, part, bias, res, norm_w, eps):
         """One kernel (``car_allreduce_add_rmsnorm``): the row-parallel partials' all-reduce, the
@@ -127,9 +133,16 @@ class TPInferenceEngine(InferenceEngine):
 
     # ------------------------------------------------------------------ control plane
     def _bcast(self, plan: Optional[Dict]) -> Dict:
-        box = [plan]
-        dist.broadcast_object_list(box, src=dist.get_global_rank(self.control, 0), group=self.control)
-        return box[0]
+        """Rank 0's plan to every TP rank: packed record through the shared-memory ring
+        (``llmctl.serve.control``; gloo tensors across nodes), no pickle on the hot path."""
+        if self.channel is None:
+            from llmctl.serve.control import make_channel
+
+            self.channel = make_channel(self.control, self.control_kind)
+        if self.tp_rank == 0:
+            self.channel.publish(plan)
+            return plan
+        return self.channel.receive()
 
     @torch.inference_mode()
     def prefill(self, chunks) -> torch.Tensor:
@@ -178,6 +191,9 @@ class TPInferenceEngine(InferenceEngine):
             dist.barrier(group=self.control)
             self.car.close()
             self.car = None
+        if self.channel is not None:
+            self.channel.close()
+            self.channel = None
         if self._own_control and self.control is not None:
             dist.destroy_process_group(self.control)
         self.control = None

@@ -535,3 +535,37 @@ def _serve_forced_gpu(rank, world, max_tokens, model, forced, engine_kw) -> dict
         eng.stop_workers()
         eng.close()
     return res
+
+
+def control_channel_worker(rank, world, kind, slot_bytes=8 << 20):
+    """TP plan channel (llmctl.serve.control): rank 0 publishes a stream of decode / prefill /
+    mixed (nested) plans -- more than the ring has slots, and with a small ``slot_bytes`` some
+    spill to the gloo fallback -- and every rank returns a digest of what it holds."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from llmctl.serve.control import ShmChannel, TensorChannel
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ch = ShmChannel(None, slot_bytes=slot_bytes) if kind == "shm" else TensorChannel(None)
+    rng = np.random.default_rng(1)
+    digests = []
+    for it in range(11):
+        n = 1 + it
+        dec = {"op": "decode", "ids": rng.integers(0, 1000, n).tolist(), "positions": list(range(n)),
+               "slots": rng.integers(0, 1 << 20, n).tolist(), "ctx": [7] * n,
+               "bt": rng.integers(0, 99, (n, 5)).astype(np.int32)}
+        T = 64 * (it + 1)
+        pre = {"op": "prefill", "ids": rng.integers(0, 1000, T), "pos": np.arange(T, dtype=np.int32),
+               "cu": [0, T], "doc": None if it % 2 else np.zeros(T, dtype=np.int32), "last": [T - 1], "x": 1.5,
+               "flag": True}
+        plan = [dec, pre, {"op": "mixed", "prefill": pre, "decode": dec}][it % 3]
+        got = (ch.publish(plan), plan)[1] if rank == 0 else ch.receive()
+        d = got["decode"] if got["op"] == "mixed" else got
+        digests.append(torch.tensor([len(d["ids"]), int(np.asarray(d["ids"]).sum()),
+                                     int(np.asarray(d.get("bt", d.get("pos"))).sum())], dtype=torch.int64))
+        if got["op"] != "decode":
+            p = got["prefill"] if got["op"] == "mixed" else got
+            assert p["x"] == 1.5 and p["flag"] is True and (p["doc"] is None) == bool(it % 2)
+    ch.close()
+    return {"digest": torch.stack(digests), "spilled": torch.tensor(getattr(ch, "stats", {}).get("spilled", 0))}

@@ -77,12 +77,14 @@ def test_gemm64_split_tail_multi_round(native_lib):
 
 
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True)])
-def test_gemm64_persistent_many_rounds(native_lib, at, bt):
-    """Persistent kernel over ~3.4 rounds of items per CU with a split tail: every workgroup
-    streams several tiles back to back (the next tile's first K-tiles ride on the previous
-    tile's DMA stream); fwd / dgrad / wgrad layouts vs fp32."""
+@pytest.mark.parametrize("rounds", [3, 8])
+def test_gemm64_persistent_many_rounds(native_lib, at, bt, rounds):
+    """Persistent kernel over ~3.4 / ~8.3 rounds of items per CU with a split tail: every
+    workgroup streams several tiles back to back (the next tile's first K-tiles ride on the
+    previous tile's DMA stream, the item-boundary drain is taken repeatedly); fwd / dgrad /
+    wgrad layouts vs fp32, NaN-prefilled outputs."""
     n_cu = torch.cuda.get_device_properties(0).multi_processor_count
-    tiles = n_cu * 3 + n_cu // 3
+    tiles = n_cu * rounds + n_cu // 3
     M, N, K = 256 * (tiles // 4 + 1), 256 * 4, 512
     A, B = _bf(M, K, seed=11), _bf(N, K, seed=12)
     a = A.t().contiguous() if at else A

@@ -1,0 +1,33 @@
+"""TP control plane (llmctl.serve.control): packed plan records and the shm / gloo channels."""
+
+import numpy as np
+import pytest
+import torch
+
+from llmctl.serve.control import pack, unpack
+from llmctl.testing.harness import run_ranks
+from llmctl.testing.workers import control_channel_worker
+
+
+def test_pack_roundtrip_generic_and_decode():
+    pre = {"op": "prefill", "ids": np.arange(9, dtype=np.int64), "pos": np.arange(9, dtype=np.int32),
+           "bt": np.ones((2, 3), dtype=np.int32), "cu": [0, 4, 9], "doc": None, "x": 2.5, "ok": False, "n": -3,
+           "name": "abc"}
+    got = unpack(pack({"op": "mixed", "prefill": pre, "decode": {"op": "decode", "ids": [1, 2]}}))
+    p = got["prefill"]
+    assert got["op"] == "mixed" and got["decode"] == {"op": "decode", "ids": [1, 2]}
+    assert p["cu"] == [0, 4, 9] and p["doc"] is None and p["x"] == 2.5 and p["ok"] is False and p["n"] == -3
+    assert p["name"] == "abc" and p["pos"].dtype == np.int32 and (p["bt"] == 1).all() and p["bt"].shape == (2, 3)
+    dec = {"op": "decode", "ids": [5, 6, 7], "positions": [1, 2, 3], "slots": [9, 8, 7], "ctx": [2, 3, 4],
+           "bt": np.arange(6, dtype=np.int32).reshape(3, 2)}
+    d = unpack(pack(dec))  # fixed-layout fast path
+    assert d.keys() == dec.keys() and all((np.asarray(d[k]) == np.asarray(dec[k])).all() for k in dec if k != "op")
+
+
+@pytest.mark.parametrize("kind,slot", [("shm", 8 << 20), ("shm", 4096), ("tensor", 0)])
+def test_control_channel_multirank(kind, slot):
+    out = run_ranks(control_channel_worker, 3, kind, slot)
+    for r in (1, 2):
+        assert torch.equal(out[r]["digest"], out[0]["digest"])
+    if kind == "shm" and slot == 4096:
+        assert int(out[0]["spilled"]) > 0  # big prefill plans went through the gloo fallback

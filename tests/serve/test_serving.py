@@ -371,3 +371,21 @@ def test_mixed_prefill_decode_steps_match_separate(monkeypatch, prefix):
     b = [s.output_ids for s in e2.generate(prompts, p)]
     assert e2.stats.get("mixed_steps", 0) == 0
     assert a == b
+
+
+def test_engines_keep_their_own_knobs():
+    """A second engine in the same process (other perf_knobs) must not change the first one's
+    routing: each engine re-activates its own resolved knobs on every step."""
+    from llmctl.config.knobs import knobs
+    from llmctl.serve.scheduler import SamplingParams
+
+    kw = dict(device="cpu", max_batch_size=2, num_kv_blocks=32, block_size=8, max_model_len=128)
+    a = InferenceEngine("tiny", perf_knobs={"mixed_steps": False}, **kw)
+    b = InferenceEngine("tiny", perf_knobs={"mixed_steps": True}, **kw)
+    assert knobs().mixed_steps  # b's
+    a.add_request([1, 2, 3], SamplingParams(max_tokens=2, temperature=0.0))
+    a.step()
+    assert not knobs().mixed_steps and not a._mixed_ok()
+    b.add_request([1, 2, 3], SamplingParams(max_tokens=2, temperature=0.0))
+    b.step()
+    assert knobs().mixed_steps

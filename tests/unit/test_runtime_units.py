@@ -392,3 +392,33 @@ def test_gemm64_default_config_single_knob(monkeypatch):
         assert {linear.gemm64_config(l, 4096, 4096, 4096) for l in ("fwd", "dgrad", "wgrad")} == {304}
     with override(gemm64_config=904):
         assert {linear.gemm64_config(l, 4096, 4096, 4096) for l in ("fwd", "dgrad", "wgrad")} == {904}
+
+
+def test_checkpoint_commit_ignores_stale_done_markers(tmp_path):
+    """A re-save of the same checkpoint (elastic restart after a rank died mid-write) must not
+    count the earlier attempt's done-markers: rank 0 clears them (and the old commit record)
+    before the pre-write barrier, and only markers carrying this save's id count."""
+    from llmctl.io.checkpoint import CheckpointManager
+    from llmctl.runtime.engine import TrainingEngine
+    from llmctl.testing.workers import _config
+
+    eng = TrainingEngine(_config(output_dir=str(tmp_path)))
+    g = torch.Generator().manual_seed(0)
+    eng.train_step([(torch.randint(1, 500, (2, 32), generator=g), torch.randint(1, 500, (2, 32), generator=g))])
+    mgr = CheckpointManager(eng, str(tmp_path))
+    ck = tmp_path / "checkpoint-1"
+    (ck / ".done").mkdir(parents=True)
+    for r in range(4):  # an interrupted earlier attempt of a 4-rank job
+        (ck / ".done" / f"rank_{r:05d}").write_text("stale")
+    (ck / "training_state.json").write_text('{"global_step": -1}')
+    mgr.save("checkpoint-1", final=True)
+    st = json.loads((ck / "training_state.json").read_text())
+    assert st["global_step"] == eng.global_step
+    assert not (ck / ".done").exists()
+    assert (tmp_path / "latest").read_text() == "checkpoint-1"
+    # the commit counts only markers of this save: one fresh marker + stale ones of "other ranks"
+    (ck / ".done").mkdir()
+    (ck / ".done" / "rank_00000").write_text("this-save")
+    (ck / ".done" / "rank_00001").write_text("stale")
+    with pytest.raises(TimeoutError):
+        mgr._commit(ck, st, 1, 2, 0.2, "this-save")
