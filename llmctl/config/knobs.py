@@ -70,6 +70,8 @@ class PerfKnobs:
     mixed_steps: bool = True       # decode rows ride on prefill chunk steps
     custom_ar: bool = True         # TP all-reduces through the xGMI peer-memory kernel
     tp_graphs: bool = True         # TP decode steps captured in hipGraphs
+    async_decode: bool = True      # pure decode steps pipelined: step N+1 launched (ids fed on the
+                                   # device from step N's in-graph sampling) before step N's tokens are read
     tp_fused_decode: bool = True   # TP decode: all-reduce + residual + RMSNorm in one kernel
 
     def as_dict(self) -> Dict[str, Any]:

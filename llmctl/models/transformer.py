@@ -233,9 +233,13 @@ class _UpSwiGLUDown(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             _prep_weight_t(w_up, T)
         # the SwiGLU backward as the down projection wgrad's side job (swiglu_bwd = side), as
-        # _SwiGLUDown; the down data gradient then runs plain (gemm64 or hipBLASLt through W^T)
-        ctx.side = gu.requires_grad and wgrad_swiglu_ok(w_down, T, w_down.shape[1])
-        if ctx.side:
+        # _SwiGLUDown; the down data gradient then runs plain (gemm64 or hipBLASLt through W^T).
+        # (gu is made inside this Function, so gu.requires_grad is always False here: whether dgu
+        # is needed comes from the inputs -- round 4 read gu.requires_grad and never took the side
+        # path, running the down dgrad on the slower fused-epilogue kernel instead)
+        ctx.side = (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) and wgrad_swiglu_ok(w_down, T, w_down.shape[1])
+        ctx.dgrad_g64 = ctx.side and knobs().dgrad64 == "all"
+        if ctx.side and not ctx.dgrad_g64:
             _prep_weight_t(w_down, T)
         ctx.save_for_backward(x2, gu, act)
         ctx.w_up, ctx.w_down, ctx.xshape = w_up, w_down, x.shape
@@ -247,7 +251,10 @@ class _UpSwiGLUDown(torch.autograd.Function):
         dout2 = dout.reshape(-1, dout.shape[-1])
         dgu = None
         if ctx.side:
-            dact = data_grad(dout2, ctx.w_down)
+            if ctx.dgrad_g64 and _gemm64_dgrad_ok(dout2, ctx.w_down):
+                dact = dgrad64(dout2, ctx.w_down)
+            else:
+                dact = data_grad(dout2, ctx.w_down)
             dgu = ctx.w_down._llmctl_grad_sink.write_swiglu(ctx.w_down, dout2, act, dact, gu)
             dw_down = None
             if dgu is None:  # operands the side kernel cannot take: weight gradient + elementwise pass

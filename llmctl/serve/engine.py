@@ -105,8 +105,10 @@ class InferenceEngine:
         # MoE routing sizes the expert segments on the host: decode runs eagerly
         self.use_graphs = use_graphs and self.device.type == "cuda" and not cfg.is_moe
         self._graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, Dict[str, torch.Tensor]]] = {}
-        self._rng = torch.Generator(device=self.device)
-        self._rng.manual_seed(seed)
+        # sampling uniforms come from the host (one H2D copy with the step's other inputs), so
+        # in-graph sampling and the eager path draw the same stream
+        self._np_rng = np.random.default_rng(seed)
+        self._pending: Optional[Dict] = None  # an in-flight asynchronous decode step
         self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "graph_replays": 0}
         log.info("engine: %s on %s, %d KV blocks x %d tokens (%.1f GB)", cfg.name, self.device, num_kv_blocks,
                  block_size, self.kv_cache.nbytes / 1e9)
@@ -395,22 +397,45 @@ class InferenceEngine:
             b *= 2
         return min(b, max(self.max_batch_size, n))
 
-    def _static(self, nb: int) -> Dict[str, torch.Tensor]:
+    _STAGED = ("ids", "positions", "slots", "block_tables", "ctx_lens", "u")
+
+    def _static(self, nb: int) -> Dict:
         d = self.device
         bufs = {"ids": torch.zeros(nb, dtype=torch.long, device=d),
                 "positions": torch.zeros(nb, dtype=torch.int32, device=d),
                 "slots": torch.full((nb,), -1, dtype=torch.long, device=d),
                 "block_tables": torch.zeros(nb, self.max_blocks_per_seq, dtype=torch.int32, device=d),
-                "ctx_lens": torch.ones(nb, dtype=torch.int32, device=d)}
-        # pinned host staging of the same inputs: one truly asynchronous H2D copy each per step
-        # (a non_blocking copy from pageable memory is synchronous)
+                "ctx_lens": torch.ones(nb, dtype=torch.int32, device=d),
+                # in-graph sampling: per-row parameters (rewritten when the batch's change) and uniforms
+                "u": torch.zeros(nb, dtype=torch.float32, device=d),
+                "temp": torch.zeros(nb, dtype=torch.float32, device=d),
+                "topk": torch.zeros(nb, dtype=torch.int32, device=d),
+                "topp": torch.ones(nb, dtype=torch.float32, device=d)}
+        # pinned host staging of the step inputs, two sets: an asynchronous step refills one while
+        # the other's H2D copies may still be queued behind the step in flight (a non_blocking
+        # copy from pageable memory would be synchronous)
         pin = self.device.type == "cuda"
-        for k in ("ids", "positions", "slots", "block_tables", "ctx_lens"):
+        stage = []
+        for _ in range(2):
             # initialised from the device defaults: rows past the live batch are copied too and
             # must stay valid (block id 0, context 1) for the padded graph rows
-            h = bufs[k].to("cpu")
-            bufs["host_" + k] = h.pin_memory() if pin else h
+            h = {k: bufs[k].to("cpu") for k in self._STAGED}
+            stage.append({k: (v.pin_memory() if pin else v) for k, v in h.items()})
+        bufs["stage"] = stage
+        bufs["flip"] = 0
+        toks = torch.zeros(nb, dtype=torch.long)
+        bufs["host_toks"] = [toks.pin_memory() if pin else toks, toks.clone().pin_memory() if pin else toks.clone()]
+        bufs["tflip"] = 0
+        bufs["params_key"] = None
         return bufs
+
+    def _graph_body(self, bufs: Dict) -> None:
+        """Decode step + sampling; the sampled ids also become the next step's input ids (the
+        asynchronous path launches step N + 1 without reading step N's tokens first)."""
+        bufs["logits"] = self._decode_body(bufs["ids"], bufs["positions"], bufs["slots"], bufs["block_tables"],
+                                           bufs["ctx_lens"])
+        bufs["toks"] = ops.sample(bufs["logits"].contiguous(), bufs["temp"], bufs["topk"], bufs["topp"], bufs["u"])
+        bufs["ids"].copy_(bufs["toks"])
 
     def _capture(self, nb: int):
         bufs = self._static(nb)
@@ -418,13 +443,11 @@ class InferenceEngine:
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up (allocator / lazy init) outside the graph
-                self._decode_body(bufs["ids"], bufs["positions"], bufs["slots"], bufs["block_tables"],
-                                  bufs["ctx_lens"])
+                self._graph_body(bufs)
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            bufs["logits"] = self._decode_body(bufs["ids"], bufs["positions"], bufs["slots"], bufs["block_tables"],
-                                               bufs["ctx_lens"])
+            self._graph_body(bufs)
         self._graphs[nb] = (g, bufs)
 
     def release_graphs(self) -> None:
@@ -452,29 +475,110 @@ class InferenceEngine:
         n = len(ids)
         self.stats["decode_tokens"] += n
         if self.use_graphs:
-            nb = self._bucket(n)
-            if nb not in self._graphs:
-                self._capture(nb)
-            g, b = self._graphs[nb]
-            # the previous step's copies out of these pinned buffers completed before its
-            # sampled ids were read back (host sync per step), so they can be refilled here
-            h = {k: b["host_" + k].numpy() for k in ("ids", "positions", "slots", "block_tables", "ctx_lens")}
-            h["ids"][:n] = ids
-            h["positions"][:n] = positions
-            h["slots"][:] = -1
-            h["slots"][:n] = slots
-            h["block_tables"][:n] = bt
-            h["ctx_lens"][:] = 1
-            h["ctx_lens"][:n] = ctx
-            for k in ("ids", "positions", "slots", "block_tables", "ctx_lens"):
-                b[k].copy_(b["host_" + k], non_blocking=True)
-            g.replay()
-            self.stats["graph_replays"] += 1
+            g, b = self._stage_and_replay(plan, None, cont=False)
             return b["logits"][:n]
         d = self.device
         return self._decode_body(torch.tensor(ids, device=d), torch.tensor(positions, dtype=torch.int32, device=d),
                                  torch.tensor(slots, device=d), torch.from_numpy(bt).to(d),
                                  torch.tensor(ctx, dtype=torch.int32, device=d))
+
+    def _stage_and_replay(self, plan: Dict, seqs: Optional[List[Sequence]], cont: bool):
+        """Fill one host staging set with the step's inputs, copy them (asynchronously) into the
+        graph's static buffers and replay it.  ``cont``: the input ids are already on the device
+        (the previous replay of this graph sampled them), only positions / slots / block tables /
+        context lengths / uniforms are copied.  ``seqs``: rows whose sampling parameters to load."""
+        n = len(plan["positions"])
+        nb = self._bucket(n)
+        if nb not in self._graphs:
+            self._capture(nb)
+        g, b = self._graphs[nb]
+        h = b["stage"][b["flip"]]
+        b["flip"] ^= 1
+        hn = {k: v.numpy() for k, v in h.items()}
+        if not cont:
+            hn["ids"][:n] = plan["ids"]
+        hn["positions"][:n] = plan["positions"]
+        hn["slots"][:] = -1
+        hn["slots"][:n] = plan["slots"]
+        hn["block_tables"][:n] = plan["bt"]
+        hn["ctx_lens"][:] = 1
+        hn["ctx_lens"][:n] = plan["ctx"]
+        hn["u"][:n] = plan["u"] if "u" in plan else self._np_rng.random(n, dtype=np.float32)
+        if seqs is not None:
+            key = tuple((s.params.temperature, s.params.top_k if s.params.top_k and s.params.top_k > 0 else 0,
+                         s.params.top_p) for s in seqs)
+            if b["params_key"] != key:
+                d = self.device
+                b["temp"].zero_()
+                b["topk"].zero_()
+                b["topp"].fill_(1.0)
+                b["temp"][:n].copy_(torch.tensor([k[0] for k in key], dtype=torch.float32, device=d))
+                b["topk"][:n].copy_(torch.tensor([k[1] for k in key], dtype=torch.int32, device=d))
+                b["topp"][:n].copy_(torch.tensor([k[2] for k in key], dtype=torch.float32, device=d))
+                b["params_key"] = key
+        for k in self._STAGED:
+            if cont and k == "ids":
+                continue
+            b[k].copy_(h[k], non_blocking=True)
+        g.replay()
+        self.stats["graph_replays"] += 1
+        return g, b
+
+    # ------------------------------------------------------------------ asynchronous decode
+    def _launch_decode(self, seqs: List[Sequence], plan: Dict, cont: bool) -> Dict:
+        """Replay the decode graph (sampling inside) and queue the D2H copy of its tokens; the
+        tokens are read by :meth:`_finalize`."""
+        self.stats["decode_tokens"] += len(seqs)
+        g, b = self._stage_and_replay(plan, seqs, cont)
+        out = b["host_toks"][b["tflip"]]
+        b["tflip"] ^= 1
+        out.copy_(b["toks"], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return {"seqs": list(seqs), "host": out, "event": ev, "n": len(seqs)}
+
+    def _finalize(self, p: Dict) -> int:
+        """Read an in-flight step's tokens (the one host sync of the pipeline) and append them."""
+        p["event"].synchronize()
+        toks = p["host"][: p["n"]].tolist()
+        produced = 0
+        for seq, tok in zip(p["seqs"], toks):
+            if seq.status != "running":  # finished by the previous step's tokens: speculative row
+                continue
+            self.scheduler.computed(seq, 1)
+            self._append(seq, tok)
+            produced += 1
+        return produced
+
+    def _continue_decode(self, p: Dict) -> Optional[Dict]:
+        """Launch step N + 1 for the same batch before step N's tokens are known, when nothing
+        else can change the batch: no request waiting for admission, every sequence of the batch
+        still running and able to take two more tokens (length limits), and free KV blocks for
+        one more token each (no preemption).  Its input ids are step N's sampled tokens, already
+        on the device; positions / slots / context lengths advance by one."""
+        seqs = p["seqs"]
+        run = self.scheduler.running
+        if (not self.knobs.async_decode or self.scheduler.waiting or len(run) != len(seqs)
+                or any(a is not b for a, b in zip(run, seqs)) or self.kv.num_free_blocks() < len(seqs)):
+            return None
+        for s in seqs:
+            if (s.status != "running" or len(s.output_ids) + 2 > s.params.max_tokens
+                    or s.num_tokens + 2 > self.max_model_len):
+                return None
+        for s in seqs:
+            slot = self.kv.append_token(s.seq_id)
+            if slot < 0:  # cannot happen with the free-block check; never launch half a batch
+                raise RuntimeError("KV append failed despite free blocks")
+            s._decode_slot = slot
+            s.kv_len += 1
+        plan = {"positions": [s.num_tokens for s in seqs], "slots": [s._decode_slot for s in seqs],
+                "ctx": [self.kv.num_tokens(s.seq_id) for s in seqs],
+                "bt": np.asarray(self.kv.block_tables([s.seq_id for s in seqs], self.max_blocks_per_seq))}
+        self.stats["async_continued"] = self.stats.get("async_continued", 0) + 1
+        return self._launch_decode(seqs, plan, cont=True)
+
+    def _async_ok(self) -> bool:
+        return self.use_graphs and self.knobs.async_decode and self.tp == 1
 
     # ------------------------------------------------------------------ sampling
     def sample(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[int]:
@@ -491,7 +595,7 @@ class InferenceEngine:
             topp = torch.tensor([k[2] for k in key], dtype=torch.float32, device=d)
             self._sample_params = cached = (key, temp, topk, topp)
         _, temp, topk, topp = cached
-        u = torch.rand(n, generator=self._rng, device=d)
+        u = torch.from_numpy(self._np_rng.random(n, dtype=np.float32)).to(d)
         toks = ops.sample(logits.contiguous(), temp, topk, topp, u)
         return toks.tolist()
 
@@ -523,10 +627,22 @@ class InferenceEngine:
                 self.scheduler.finish(seq, "stop")
 
     def step(self) -> int:
-        """One scheduling iteration; returns the number of tokens produced."""
+        """One scheduling iteration; returns the number of tokens produced.  Pure decode steps
+        run asynchronously (knob ``async_decode``): the step is launched and its tokens are read
+        by the NEXT call, which first launches the following step when the batch cannot change."""
         use_knobs(self.knobs)
-        out = self.scheduler.schedule()
         produced = 0
+        if self._pending is not None:
+            p, self._pending = self._pending, None
+            nxt = self._continue_decode(p)
+            produced = self._finalize(p)
+            if nxt is not None:
+                self._pending = nxt
+                self.stats["steps"] += 1
+                return produced
+            if not self.scheduler.has_work():
+                return produced
+        out = self.scheduler.schedule()
         if out.decode and out.prefill and self._mixed_ok():
             logits = self.mixed(out.prefill, out.decode)
             final = [c.seq for c in out.prefill if c.final]
@@ -542,6 +658,14 @@ class InferenceEngine:
                 produced += 1
             self.stats["steps"] += 1
             return produced
+        if out.decode and not out.prefill and self.use_graphs and self.tp == 1:
+            # sampling inside the decode graph; asynchronous: the tokens are read next call
+            pend = self._launch_decode(out.decode, self.decode_plan(out.decode), cont=False)
+            self.stats["steps"] += 1
+            if self._async_ok():
+                self._pending = pend
+                return produced
+            return produced + self._finalize(pend)
         if out.decode:
             logits = self.decode(out.decode)
             for seq, tok in zip(out.decode, self.sample(logits, out.decode)):

@@ -268,3 +268,26 @@ def test_fresh_prefill_flash_attention_matches_paged(native_lib, monkeypatch):
     assert torch.equal(kc_a[0], e.kv_cache.k[0])  # layer 0: the same RoPE'd K rows written
     for a, b in zip(kc_a[1:], e.kv_cache.k[1:]):  # later layers see attention outputs that differ in rounding
         assert (a.float() - b.float()).norm() / b.float().norm() < 1e-2
+
+
+@pytest.mark.parametrize("temp", [0.0, 0.8])
+def test_async_decode_matches_sync(native_lib, temp):
+    """Pipelined decode (step N + 1 launched with its ids fed on the device from step N's
+    in-graph sampling, before step N's tokens are read) produces the synchronous path's tokens,
+    greedy and sampled (same seed: both draw one uniform per row per decode step)."""
+    from llmctl.serve.engine import InferenceEngine
+    from llmctl.serve.scheduler import SamplingParams
+
+    prompts = [[1, 2, 3, 4, 5], [9] * 37, [7, 7], [3] * 70]
+    p = SamplingParams(max_tokens=24, temperature=temp, top_k=50, top_p=0.9, ignore_eos=True)
+    outs = []
+    for a in (True, False):
+        e = InferenceEngine("tiny", perf_knobs={"async_decode": a}, device="cuda", max_batch_size=4,
+                            num_kv_blocks=128, block_size=16, max_model_len=512, use_graphs=True, seed=3)
+        seqs = e.generate(prompts, p)
+        outs.append([s.output_ids for s in seqs])
+        assert all(len(s.output_ids) == 24 for s in seqs)
+        if a:
+            assert e.stats.get("async_continued", 0) > 10
+        e.release_graphs()
+    assert outs[0] == outs[1]

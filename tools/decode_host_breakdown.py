@@ -1,7 +1,14 @@
 #!/usr/bin/env python3
-"""Host-side phase timing of serving decode steps (GPT-7B, 16 x 2048-token prompts): schedule,
-decode plan, graph replay (incl. input staging), sampling + token readback, bookkeeping."""
-import collections
+"""Serving decode step cost (GPT-7B, 16 x 2048-token prompts, greedy): host wall time per decode
+step through ``InferenceEngine.step()`` with the synchronous and the pipelined (knob
+``async_decode``) decode paths, against the device time of one decode graph replay (decode +
+in-graph sampling, CUDA events, same batch).  The pipelined path launches step N + 1 before reading
+step N's tokens, so its host ms/step should sit on the device time.
+
+    python tools/decode_host_breakdown.py [--tokens 96] [--prompt 2048] [--batch 16]
+"""
+import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -11,38 +18,48 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt-7b")
+    ap.add_argument("--tokens", type=int, default=96)
+    ap.add_argument("--prompt", type=int, default=2048)
+    ap.add_argument("--batch", type=int, default=16)
+    a = ap.parse_args()
     import torch
     from llmctl.serve.engine import InferenceEngine
     from llmctl.serve.scheduler import SamplingParams
 
-    eng = InferenceEngine("gpt-7b", device="cuda", max_batch_size=16, max_model_len=2048 + 160)
-    p = SamplingParams(max_tokens=96, temperature=0.0, ignore_eos=True)
-    seqs = [eng.add_request([(7 * i + r) % 32000 for i in range(2048)], p) for r in range(16)]
-    while any(s.first_token_time is None for s in seqs):  # prefills
-        eng.step()
-    t = collections.defaultdict(float)
-    n = 0
+    eng = InferenceEngine(a.model, device="cuda", max_batch_size=a.batch, max_model_len=a.prompt + a.tokens + 64)
+    p = SamplingParams(max_tokens=a.tokens, temperature=0.0, ignore_eos=True)
+    base = eng.knobs
+    for rnd in range(3):
+        for mode in (False, True):
+            eng.knobs = dataclasses.replace(base, async_decode=mode)
+            seqs = [eng.add_request([(7 * i + r + rnd) % 32000 for i in range(a.prompt)], p) for r in range(a.batch)]
+            while any(s.first_token_time is None for s in seqs):  # prefills (+ first tokens)
+                eng.step()
+            torch.cuda.synchronize()
+            start = [len(s.output_ids) for s in seqs]
+            t0 = time.perf_counter()
+            while any(s.status != "finished" for s in seqs):
+                eng.step()
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) * 1e3
+            steps = max(len(s.output_ids) - s0 for s, s0 in zip(seqs, start))
+            if rnd > 0:
+                print(json.dumps({"async_decode": mode, "decode_steps": steps, "host_ms_per_step": round(wall / steps, 3),
+                                  "continued": eng.stats.get("async_continued", 0)}), flush=True)
+    # device time of one decode step (graph replay incl. in-graph sampling) for this batch
+    g, b = eng._graphs[eng._bucket(a.batch)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for _ in range(3):
+        g.replay()
+    ev[0].record()
+    for _ in range(20):
+        g.replay()
+    ev[1].record()
     torch.cuda.synchronize()
-    t_all = time.perf_counter()
-    while any(s.status != "finished" for s in seqs):
-        a = time.perf_counter()
-        out = eng.scheduler.schedule()
-        b = time.perf_counter()
-        plan = eng.decode_plan(out.decode)
-        c = time.perf_counter()
-        logits = eng.decode_exec(plan)
-        d = time.perf_counter()
-        toks = eng.sample(logits, out.decode)
-        e = time.perf_counter()
-        for seq, tok in zip(out.decode, toks):
-            eng.scheduler.computed(seq, 1)
-            eng._append(seq, tok)
-        f = time.perf_counter()
-        for k, v in (("schedule", b - a), ("plan", c - b), ("exec_replay", d - c), ("sample_sync", e - d), ("append", f - e)):
-            t[k] += v * 1e3
-        n += 1
-    wall = (time.perf_counter() - t_all) * 1e3
-    print(json.dumps({"steps": n, "ms_per_step": round(wall / n, 3), **{k: round(v / n, 3) for k, v in t.items()}}))
+    print(json.dumps({"gpu_ms_per_step": round(ev[0].elapsed_time(ev[1]) / 20, 3), "batch": a.batch,
+                      "context": a.prompt}), flush=True)
 
 
 if __name__ == "__main__":

@@ -6,7 +6,8 @@ Two slices of the real 70B layer (hidden 8192, ffn 28672, 64 q / 8 kv heads, voc
 L0 and L1 decoder layers train one step each on one MI355X (ZeRO-0, one rank).  Their difference
 gives, per decoder layer:
   * state bytes (bf16 param + grad, fp32 master + Adam m / v): allocated after a step;
-  * activation bytes per micro-batch: the step's peak minus the state.
+  * saved activation bytes per micro-batch: allocated at the end of the forward (before the
+    backward frees anything) minus the state -- differenced over the two slices;
 The intercept is the embedding / LM head / logits share.  The PP4 x DP2 ZeRO-3 layout's stage
 (20 layers; stage 0 holds the embedding, stage 3 the LM head) then needs
   state / dp  (ZeRO-3 shards params, grads and optimizer state over the DP pair)
@@ -46,12 +47,26 @@ def measure(model, layers, mb, seq, ac):
     torch.cuda.synchronize()
     state = torch.cuda.memory_allocated()
     torch.cuda.reset_peak_memory_stats()
+    # the forward's saved activations: allocated bytes at the end of the forward (loss computed,
+    # before backward frees anything) minus the resident state
+    fwd_end = {}
+    inner = eng._forward_backward
+
+    def fb(input_ids, labels, denom, before_backward=None):
+        def hook():
+            fwd_end["bytes"] = torch.cuda.memory_allocated()
+            if before_backward is not None:
+                before_backward()
+        return inner(input_ids, labels, denom, before_backward=hook)
+
+    eng._forward_backward = fb
     eng.train_step([data.batch(1)])
     torch.cuda.synchronize()
     peak = torch.cuda.max_memory_allocated()
     wt = sum(getattr(p, "_llmctl_wt").numel() * 2 for p in eng.model.parameters()
              if getattr(p, "_llmctl_wt", None) is not None)
     res = {"layers": layers, "state_gb": round(state / GiB, 2), "peak_gb": round(peak / GiB, 2),
+           "fwd_end_gb": round(fwd_end["bytes"] / GiB, 3),
            "weight_t_gb": round(wt / GiB, 2), "params": sum(p.numel() for p in eng.model.parameters())}
     eng.shutdown()
     del eng
@@ -93,8 +108,12 @@ def main():
     # ZeRO-3 installs no grad sink, so the projection leaves them out
     wt_layer = (r1["weight_t_gb"] - r0["weight_t_gb"]) / dl
     state_layer = (r1["state_gb"] - r0["state_gb"]) / dl - wt_layer
-    act_layer = ((r1["peak_gb"] - r1["state_gb"]) - (r0["peak_gb"] - r0["state_gb"])) / dl
+    # saved activations per layer per micro-batch: the forward-end allocation minus the state,
+    # differenced over the slices (the step's PEAK is set at the LM head / optimizer, not by the
+    # layer stack: round 4's peak difference read 0.0 per layer)
+    act_layer = ((r1["fwd_end_gb"] - r1["state_gb"]) - (r0["fwd_end_gb"] - r0["state_gb"])) / dl
     edge_state = r0["state_gb"] - r0["weight_t_gb"] - state_layer * r0["layers"]
+    # the last stage's edge: LM head / logits / loss transients above the layer activations
     edge_act = (r0["peak_gb"] - r0["state_gb"]) - act_layer * r0["layers"]
     from llmctl.models import get_model_config
     from llmctl.partition.planner import ParallelismPlanner
