@@ -109,6 +109,7 @@ class InferenceEngine:
         # in-graph sampling and the eager path draw the same stream
         self._np_rng = np.random.default_rng(seed)
         self._pending: Optional[Dict] = None  # an in-flight asynchronous decode step
+        self._last_toks: Optional[torch.Tensor] = None  # eager path: the last step's sampled ids
         self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "graph_replays": 0}
         log.info("engine: %s on %s, %d KV blocks x %d tokens (%.1f GB)", cfg.name, self.device, num_kv_blocks,
                  block_size, self.kv_cache.nbytes / 1e9)
@@ -526,20 +527,35 @@ class InferenceEngine:
 
     # ------------------------------------------------------------------ asynchronous decode
     def _launch_decode(self, seqs: List[Sequence], plan: Dict, cont: bool) -> Dict:
-        """Replay the decode graph (sampling inside) and queue the D2H copy of its tokens; the
-        tokens are read by :meth:`_finalize`."""
+        """Run a decode step with sampling (the graph replay, or the eager layer stack) and queue
+        the D2H copy of its tokens; the tokens are read by :meth:`_finalize`.  ``cont``: the
+        input ids are the previous step's sampled tokens, already on the device."""
         self.stats["decode_tokens"] += len(seqs)
-        g, b = self._stage_and_replay(plan, seqs, cont)
-        out = b["host_toks"][b["tflip"]]
-        b["tflip"] ^= 1
-        out.copy_(b["toks"], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        return {"seqs": list(seqs), "host": out, "event": ev, "n": len(seqs)}
+        n = len(seqs)
+        if self.use_graphs:
+            g, b = self._stage_and_replay(plan, seqs, cont)
+            out = b["host_toks"][b["tflip"]]
+            b["tflip"] ^= 1
+            out.copy_(b["toks"], non_blocking=True)
+        else:
+            d = self.device
+            ids = self._last_toks if cont else torch.tensor(plan["ids"], device=d)
+            logits = self._decode_body(ids, torch.tensor(plan["positions"], dtype=torch.int32, device=d),
+                                       torch.tensor(plan["slots"], device=d), torch.from_numpy(np.asarray(plan["bt"])).to(d),
+                                       torch.tensor(plan["ctx"], dtype=torch.int32, device=d))
+            toks = self._sample_rows(logits, seqs)
+            self._last_toks = toks
+            out = toks.to("cpu", non_blocking=True) if d.type == "cuda" else toks
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        return {"seqs": list(seqs), "host": out, "event": ev, "n": n}
 
     def _finalize(self, p: Dict) -> int:
         """Read an in-flight step's tokens (the one host sync of the pipeline) and append them."""
-        p["event"].synchronize()
+        if p["event"] is not None:
+            p["event"].synchronize()
         toks = p["host"][: p["n"]].tolist()
         produced = 0
         for seq, tok in zip(p["seqs"], toks):
@@ -559,7 +575,7 @@ class InferenceEngine:
         seqs = p["seqs"]
         run = self.scheduler.running
         if (not self.knobs.async_decode or self.scheduler.waiting or len(run) != len(seqs)
-                or any(a is not b for a, b in zip(run, seqs)) or self.kv.num_free_blocks() < len(seqs)):
+                or any(a is not b for a, b in zip(run, seqs)) or self.kv.num_free_blocks < len(seqs)):
             return None
         for s in seqs:
             if (s.status != "running" or len(s.output_ids) + 2 > s.params.max_tokens
@@ -578,10 +594,15 @@ class InferenceEngine:
         return self._launch_decode(seqs, plan, cont=True)
 
     def _async_ok(self) -> bool:
-        return self.use_graphs and self.knobs.async_decode and self.tp == 1
+        return self.knobs.async_decode and self.tp == 1
 
     # ------------------------------------------------------------------ sampling
     def sample(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[int]:
+        return self._sample_rows(logits, seqs).tolist()
+
+    def _sample_rows(self, logits: torch.Tensor, seqs: List[Sequence]) -> torch.Tensor:
+        """Sampled token ids (device tensor) of the rows of ``logits``, one uniform per row from
+        the engine's host RNG (the same stream the in-graph sampling draws from)."""
         n = len(seqs)
         d = self.device
         # per-row sampling parameters: rebuilt (3 host->device copies) only when the batch's
@@ -596,8 +617,7 @@ class InferenceEngine:
             self._sample_params = cached = (key, temp, topk, topp)
         _, temp, topk, topp = cached
         u = torch.from_numpy(self._np_rng.random(n, dtype=np.float32)).to(d)
-        toks = ops.sample(logits.contiguous(), temp, topk, topp, u)
-        return toks.tolist()
+        return ops.sample(logits.contiguous(), temp, topk, topp, u)
 
     # ------------------------------------------------------------------ step loop
     def add_request(self, prompt_ids: List[int], params: SamplingParams, request_id: str = "", on_token=None,
@@ -658,8 +678,10 @@ class InferenceEngine:
                 produced += 1
             self.stats["steps"] += 1
             return produced
-        if out.decode and not out.prefill and self.use_graphs and self.tp == 1:
-            # sampling inside the decode graph; asynchronous: the tokens are read next call
+        if out.decode and not out.prefill and self.tp == 1 and "sample" not in self.__dict__:
+            # sampling in the decode step (inside the graph); asynchronous: tokens read next call.
+            # (an instance-level ``sample`` override -- teacher forcing, logit capture -- keeps
+            # the host-sampling path below)
             pend = self._launch_decode(out.decode, self.decode_plan(out.decode), cont=False)
             self.stats["steps"] += 1
             if self._async_ok():

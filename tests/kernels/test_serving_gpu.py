@@ -122,7 +122,8 @@ def test_prefix_cache_and_preemption_gpu(native_lib):
 
     kw = dict(device="cuda", max_batch_size=2, num_kv_blocks=128, block_size=16, max_model_len=512)
     base = [(7 * i) % 200 + 1 for i in range(64)]
-    e = InferenceEngine("tiny", **kw)
+    # synchronous decode: the test reads the scheduler state between steps
+    e = InferenceEngine("tiny", perf_knobs={"async_decode": False}, **kw)
     p = SamplingParams(max_tokens=12, temperature=0.0)
     e.generate([base + [5, 6, 7]], p)
     before = e.stats["prefill_tokens"]

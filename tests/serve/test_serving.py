@@ -341,7 +341,9 @@ def test_preemption_resume_reuses_cached_blocks():
     """A sequence preempted mid-generation re-attaches its full cached blocks when resumed:
     only the tail past its last full block is recomputed, and greedy tokens are unchanged."""
     prompt = [(5 * i) % 97 + 1 for i in range(21)]
-    kw = dict(device="cpu", max_batch_size=2, num_kv_blocks=64, block_size=4, max_model_len=128)
+    # synchronous decode: the test reads the scheduler state between steps
+    kw = dict(device="cpu", max_batch_size=2, num_kv_blocks=64, block_size=4, max_model_len=128,
+              perf_knobs={"async_decode": False})
     e = InferenceEngine("tiny", **kw)
     seq = e.add_request(prompt, SamplingParams(max_tokens=10, temperature=0.0))
     for _ in range(4):  # prefill + 3 decodes: 24 positions computed
@@ -389,3 +391,28 @@ def test_engines_keep_their_own_knobs():
     b.add_request([1, 2, 3], SamplingParams(max_tokens=2, temperature=0.0))
     b.step()
     assert knobs().mixed_steps
+
+
+@pytest.mark.parametrize("temp", [0.0, 0.9])
+def test_async_decode_pipeline_matches_sync_cpu(temp):
+    """The pipelined decode loop (step N + 1 launched before step N's tokens are read, ids fed
+    from step N's sampled tokens) gives the synchronous loop's tokens, greedy and sampled; it
+    stops continuing at length limits and when a request waits for admission."""
+    from llmctl.serve.scheduler import SamplingParams
+
+    prompts = [[1, 2, 3, 4, 5], [9] * 11, [7, 7], [3] * 17]
+    p = SamplingParams(max_tokens=9, temperature=temp, top_k=20, top_p=0.9, ignore_eos=True)
+    outs = []
+    for a in (True, False):
+        e = InferenceEngine("tiny", device="cpu", max_batch_size=4, num_kv_blocks=64, block_size=8,
+                            max_model_len=128, seed=5, perf_knobs={"async_decode": a}, prefix_caching=False)
+        seqs = e.generate(prompts, p)
+        late = e.add_request([4, 4, 4], p)  # arrives while nothing runs
+        while late.status != "finished":
+            e.step()
+        outs.append(([s.output_ids for s in seqs], late.output_ids))
+        assert all(len(s.output_ids) == 9 for s in seqs) and len(late.output_ids) == 9
+        if a:
+            assert e.stats.get("async_continued", 0) >= 4
+        assert e.kv.num_free_blocks == 64  # every block back (speculative rows included)
+    assert outs[0] == outs[1]
