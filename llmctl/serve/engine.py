@@ -526,6 +526,7 @@ class InferenceEngine:
         return g, b
 
     # ------------------------------------------------------------------ asynchronous decode
+    @torch.inference_mode()
     def _launch_decode(self, seqs: List[Sequence], plan: Dict, cont: bool) -> Dict:
         """Run a decode step with sampling (the graph replay, or the eager layer stack) and queue
         the D2H copy of its tokens; the tokens are read by :meth:`_finalize`.  ``cont``: the
