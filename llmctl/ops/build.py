@@ -64,7 +64,7 @@ def _digest(src: Path, flags) -> str:
     import hashlib
 
     h = hashlib.sha256()
-    for d in [src] + sorted(CSRC.glob("*.h")):
+    for d in [src] + sorted(list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc"))):
         h.update(d.name.encode())
         h.update(d.read_bytes())
     h.update("\0".join(flags).encode())
