@@ -177,6 +177,10 @@ def start_softmax(st, z, masked, c="%[c]"):
     i_cs = a(f"s_cmp_lg_u64 vcc, 0\ns_cselect_b64 s[{SG(z)}:{SG(z) + 1}], -1, 0", 8, [(i_cmp, 1)])
     i_mx = a(f"v_max_f32_e32 v{T}, v{M(z)}, v{MX}", 4, [(i_cmp, 0)])
     i_mn = a(f"v_cndmask_b32_e64 v{MN}, v{M(z)}, v{T}, s[{SG(z)}:{SG(z) + 1}]", 4, [(i_cs, 1), (i_mx, 0)])
+    # the O rescale is needed only if some row already holds mass (l > 0): not on a block's first
+    # tile, where every growing row's max moves up from -inf over an O of zeros
+    i_l = a(f"v_cmp_lt_f32_e32 vcc, 0, v{L(z)}", 4, [(i_mn, 0)])
+    a(f"s_and_b64 s[{SG(z)}:{SG(z) + 1}], s[{SG(z)}:{SG(z) + 1}], vcc", 4, [(i_l, 1)])
     i_ne = a(f"v_cmp_neq_f32_e64 s[{SCMP[0]}:{SCMP[0] + 1}], s{SNINF}, v{MN}", 4, [(i_mn, 0)])
     i_nm = a(f"v_cndmask_b32_e64 v{NM(z)}, 0, -v{MN}, s[{SCMP[0]}:{SCMP[0] + 1}]", 4, [(i_ne, 2)])
     i_t2 = a(f"v_add_f32_e32 v{T2}, v{M(z)}, v{NM(z)}", 4, [(i_nm, 0)])
