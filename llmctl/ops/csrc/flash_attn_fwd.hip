@@ -870,7 +870,7 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   a.prio = knob("fa_prio", 1) != 0 ? 1 : 0;  // default on: 2-3 % at B12 S2048 (0: off, A/B)
   // one-wave-per-SIMD 64-row kernel (knob fa_w64): HD 128 without documents, on grids that do
   // not take the small-grid K/V split (fwd_launch<4, 2>'s rule, 128-row blocks)
-  if (D == 128 && !(doc_start.has_value() && doc_start->defined()) && knob("fa_w64", 3) != 0) {
+  if (D == 128 && !(doc_start.has_value() && doc_start->defined()) && knob("fa_w64", 0) != 0) {
     const int nqb128 = (S + 127) / 128;
     const int64_t e = knob("fa_split", -1);
     const bool split = e == 1   ? causal && nqb128 >= 2
@@ -879,7 +879,7 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
     if (!split) {
       dim3 grid((unsigned)(B * Hq * ((S + 255) / 256))), block(256);
       // fa_w64 = 1: compiler-scheduled phases, 2: sched_group_barrier interleave, 3: asm program
-      const int64_t var = knob("fa_w64", 3);
+      const int64_t var = knob("fa_w64", 0);
       const bool sgb = var == 2;
       if (var == 3) {
         a.stamp = reinterpret_cast<unsigned*>(knob("fa_stamp_ptr", 0));

@@ -186,7 +186,7 @@ def test_flash_attn(native_lib, B, S, Hq, Hkv, D, causal):
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [(2, 2048, 8, 8, True), (3, 1000, 8, 2, True), (1, 100, 4, 4, True),
                                                (2, 448, 6, 3, False), (1, 192, 8, 1, False), (4, 640, 16, 16, True)])
 def test_flash_attn_fwd_variants_agree(native_lib, B, S, Hq, Hkv, causal):
-    """The asm-scheduled one-wave-per-SIMD forward (knob fa_w64 = 3, the HD-128 default) against the
+    """The asm-scheduled one-wave-per-SIMD forward (knob fa_w64 = 3) against the
     fp32 oracle and the 2-waves-per-SIMD kernel (fa_w64 = 0): partial last tiles, waves with no
     rows (S < 256), GQA groups, B * H not a multiple of 8, full attention."""
     D = 128
@@ -198,7 +198,7 @@ def test_flash_attn_fwd_variants_agree(native_lib, B, S, Hq, Hkv, causal):
             native_lib.set_knob("fa_w64", var)
             outs[var] = native_lib.flash_attn_fwd(q, k, v, D ** -0.5, causal)
     finally:
-        native_lib.set_knob("fa_w64", 3)
+        native_lib.set_knob("fa_w64", 0)
         native_lib.set_knob("fa_split", -1)
     orf, lser = ref.attention_fwd(q, k, v, D ** -0.5, causal)
     for var, (o, lse) in outs.items():

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--no-causal", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="fa_w64 = 3 diagnostic build: cycles per section")
+    ap.add_argument("--qscale", type=float, default=1.0, help="scale q (score spread: softmax max growth)")
+    ap.add_argument("--packed", action="store_true", help="q / k / v as views of one [B, S, 3, H, D] QKV tensor (the training step's layout)")
     a = ap.parse_args()
     assert _lib.load(), _lib._error
     ops = torch.ops.llmctl
@@ -36,9 +38,15 @@ def main():
     for S in a.S:
         g = torch.Generator(device="cuda").manual_seed(S)
         hkv = a.Hkv or a.H
-        q = torch.randn(a.B, S, a.H, D, device="cuda", generator=g).to(torch.bfloat16)
-        k = torch.randn(a.B, S, hkv, D, device="cuda", generator=g).to(torch.bfloat16)
-        v = torch.randn(a.B, S, hkv, D, device="cuda", generator=g).to(torch.bfloat16)
+        if a.packed:
+            qkv = torch.randn(a.B, S, a.H + 2 * hkv, D, device="cuda", generator=g).to(torch.bfloat16)
+            q, k, v = qkv[:, :, :a.H], qkv[:, :, a.H:a.H + hkv], qkv[:, :, a.H + hkv:]
+        else:
+            q = torch.randn(a.B, S, a.H, D, device="cuda", generator=g).to(torch.bfloat16)
+            k = torch.randn(a.B, S, hkv, D, device="cuda", generator=g).to(torch.bfloat16)
+            v = torch.randn(a.B, S, hkv, D, device="cuda", generator=g).to(torch.bfloat16)
+        if a.qscale != 1.0:
+            q = (q.float() * a.qscale).to(torch.bfloat16)
         scale = D ** -0.5
         flops = 4 * a.B * a.H * S * S * D * (0.5 if causal else 1.0)
         ref = None
@@ -58,7 +66,7 @@ def main():
                 ops.flash_attn_fwd(q, k, v, scale, causal)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t) / a.iters * 1e3
-            print(json.dumps({"B": a.B, "S": S, "H": a.H, "Hkv": hkv, "causal": causal, "fa_w64": var,
+            print(json.dumps({"B": a.B, "S": S, "H": a.H, "Hkv": hkv, "causal": causal, "packed": a.packed, "qscale": a.qscale, "fa_w64": var,
                               "ms": round(ms, 4), "tflops": round(flops / ms / 1e9, 1),
                               "err_o_vs_w0": round(err_o, 5), "err_lse_vs_w0": round(err_l, 5)}), flush=True)
         if a.stamps:

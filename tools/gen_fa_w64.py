@@ -171,7 +171,10 @@ def start_softmax(st, z, masked, c="%[c]"):
     i = a(f"v_permlane32_swap_b32_e32 v{MX}, v{T}", 4, [(i_mov, 2)])
     i = a(f"v_max_f32_e32 v{MX}, v{MX}, v{T}", 4, [(i, 0)])
     i_mul = a(f"v_mul_f32_e32 v{MX}, {c}, v{MX}", 4, [(i, 0)])
-    i_th = a(f"v_add_f32_e32 v{T}, 0x41000000, v{M(z)}", 4, [(i, 0)])
+    # deferred rescale headroom 16 (log2): p <= 2^16 stays exact in fp32 / bf16 (only the exponent
+    # grows); a wave rescales when ANY of its 32 rows grows, so 8 triggered ~1 rescale per tile on
+    # wide score ranges (tools/attn_fwd_ab.py --qscale 6: 852 cycles per tile; the model step: +20 %)
+    i_th = a(f"v_add_f32_e32 v{T}, 0x41800000, v{M(z)}", 4, [(i, 0)])
     i_cmp = a(f"v_cmp_gt_f32_e32 vcc, v{MX}, v{T}", 4, [(i_mul, 0), (i_th, 0)])
     # one item: nothing (a DMA piece's SALU add) may clobber SCC between the two
     i_cs = a(f"s_cmp_lg_u64 vcc, 0\ns_cselect_b64 s[{SG(z)}:{SG(z) + 1}], -1, 0", 8, [(i_cmp, 1)])
