@@ -55,6 +55,50 @@ __device__ __forceinline__ void store8(unsigned short* p, const float* in) {
   *reinterpret_cast<bf16x8*>(p) = v;
 }
 
+// ---- paged KV cache element: bf16, or OCP fp8 e4m3fn (gfx950's v_cvt_pk_*fp8*; saturating at
+//      +-448, scale 1: torch.float8_e4m3fn bit patterns).  A row of 8 elements is 16 B / 8 B.
+__device__ __forceinline__ float sat_fp8(float x) { return __builtin_amdgcn_fmed3f(x, -448.f, 448.f); }
+
+__device__ __forceinline__ uint2 f32x8_to_fp8(const float* x) {
+  int lo = 0, hi = 0;
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(sat_fp8(x[0]), sat_fp8(x[1]), lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(sat_fp8(x[2]), sat_fp8(x[3]), lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(sat_fp8(x[4]), sat_fp8(x[5]), hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(sat_fp8(x[6]), sat_fp8(x[7]), hi, true);
+  return make_uint2((unsigned)lo, (unsigned)hi);
+}
+
+__device__ __forceinline__ void fp8x8_to_f32(uint2 u, float* out) {
+  const auto a = __builtin_amdgcn_cvt_pk_f32_fp8((int)u.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)u.x, true);
+  const auto c = __builtin_amdgcn_cvt_pk_f32_fp8((int)u.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)u.y, true);
+  out[0] = a[0], out[1] = a[1], out[2] = b[0], out[3] = b[1];
+  out[4] = c[0], out[5] = c[1], out[6] = d[0], out[7] = d[1];
+}
+
+// 8 cache elements starting at element index e of a cache of either type
+__device__ __forceinline__ void cache_store8(void* base, long e, const float* x, bool fp8) {
+  if (fp8) *reinterpret_cast<uint2*>(static_cast<unsigned char*>(base) + e) = f32x8_to_fp8(x);
+  else store8(static_cast<unsigned short*>(base) + e, x);
+}
+__device__ __forceinline__ void cache_load8(const void* base, long e, float* x, bool fp8) {
+  if (fp8) fp8x8_to_f32(*reinterpret_cast<const uint2*>(static_cast<const unsigned char*>(base) + e), x);
+  else load8(static_cast<const unsigned short*>(base) + e, x);
+}
+// ... as 8 bf16 (16 B) for an LDS image
+__device__ __forceinline__ uint4 cache_load8_bf16(const void* base, long e, bool fp8) {
+  if (!fp8) return *reinterpret_cast<const uint4*>(static_cast<const unsigned short*>(base) + e);
+  float x[8];
+  fp8x8_to_f32(*reinterpret_cast<const uint2*>(static_cast<const unsigned char*>(base) + e), x);
+  unsigned w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = (unsigned)f2bf(x[2 * j]) | ((unsigned)f2bf(x[2 * j + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// host: a paged KV cache tensor is bf16 or fp8 e4m3fn
+inline bool kv_fp8(const at::Tensor& c) { return c.scalar_type() == at::kFloat8_e4m3fn; }
+inline bool kv_cache_ok(const at::Tensor& c) { return c.scalar_type() == at::kBFloat16 || kv_fp8(c); }
+
 // Workgroup barrier ordering LDS only: __syncthreads() is also a release for global memory
 // (s_waitcnt vmcnt(0)), which would drain in-flight prefetch loads and no-return atomics
 // (~3k cycles each under load) at every barrier.  LDS-scoped fences lower to lgkmcnt(0).

@@ -16,9 +16,9 @@ __global__ __launch_bounds__(256) void rope_fwd_kernel(const unsigned short* __r
                                                         const PosT* __restrict__ pos, unsigned short* __restrict__ q,
                                                         unsigned short* __restrict__ k,
                                                         unsigned short* __restrict__ v, int nq, int nkv, int D,
-                                                        int S, long total, unsigned short* __restrict__ kc = nullptr,
-                                                        unsigned short* __restrict__ vc = nullptr,
-                                                        const int64_t* __restrict__ slots = nullptr) {
+                                                        int S, long total, void* __restrict__ kc = nullptr,
+                                                        void* __restrict__ vc = nullptr,
+                                                        const int64_t* __restrict__ slots = nullptr, bool kv8 = false) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   const int CH = D >> 4;
@@ -62,9 +62,9 @@ __global__ __launch_bounds__(256) void rope_fwd_kernel(const unsigned short* __r
     const long sl = slots[t];
     if (sl >= 0) {
       const bool isk = h < nq + nkv;
-      unsigned short* cdst = (isk ? kc : vc) + (sl * nkv + (isk ? h - nq : h - nq - nkv)) * (long)D;
-      store8(cdst + c * 8, o1);
-      store8(cdst + half + c * 8, o2);
+      const long e = (sl * nkv + (isk ? h - nq : h - nq - nkv)) * (long)D;  // fp8 caches: same element index
+      cache_store8(isk ? kc : vc, e + c * 8, o1, kv8);
+      cache_store8(isk ? kc : vc, e + half + c * 8, o2, kv8);
     }
   }
 }
@@ -265,26 +265,29 @@ static std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_qkv_impl(
   auto v = at::empty({T, nkv, D}, qkv.options());
   const long total = T * NH * (D / 16);
   if (total == 0) return {q, k, v};
-  unsigned short *kcp = nullptr, *vcp = nullptr;
+  void *kcp = nullptr, *vcp = nullptr;
   const int64_t* sp = nullptr;
+  bool kv8 = false;
   if (slots != nullptr) {
-    LLMCTL_CHECK(kc->is_contiguous() && vc->is_contiguous() && kc->scalar_type() == at::kBFloat16 &&
-                     vc->sizes() == kc->sizes() && kc->dim() == 4 && kc->size(2) == nkv && kc->size(3) == D,
-                 "k/v cache: contiguous bf16 [blocks, block_size, Hkv, D]");
+    LLMCTL_CHECK(kc->is_contiguous() && vc->is_contiguous() && kv_cache_ok(*kc) &&
+                     vc->scalar_type() == kc->scalar_type() && vc->sizes() == kc->sizes() && kc->dim() == 4 &&
+                     kc->size(2) == nkv && kc->size(3) == D,
+                 "k/v cache: contiguous bf16 or fp8 (e4m3fn) [blocks, block_size, Hkv, D]");
     LLMCTL_CHECK(slots->scalar_type() == at::kLong && slots->numel() == T && slots->is_contiguous(), "slots: int64 [T]");
-    kcp = bf_mut(*kc);
-    vcp = bf_mut(*vc);
+    kcp = kc->data_ptr();
+    vcp = vc->data_ptr();
     sp = slots->data_ptr<int64_t>();
+    kv8 = kv_fp8(*kc);
   }
   if (has_pos && pos->scalar_type() == at::kLong)
     hipLaunchKernelGGL(rope_fwd_kernel<int64_t>, dim3(blocks_for(total)), dim3(256), 0, stream(), bf_ptr(qkv),
                        cosT.data_ptr<float>(), sinT.data_ptr<float>(), pos->data_ptr<int64_t>(), bf_mut(q), bf_mut(k),
-                       bf_mut(v), (int)nq, (int)nkv, D, (int)seq_len, total, kcp, vcp, sp);
+                       bf_mut(v), (int)nq, (int)nkv, D, (int)seq_len, total, kcp, vcp, sp, kv8);
   else
     hipLaunchKernelGGL(rope_fwd_kernel<int32_t>, dim3(blocks_for(total)), dim3(256), 0, stream(), bf_ptr(qkv),
                        cosT.data_ptr<float>(), sinT.data_ptr<float>(),
                        has_pos ? pos->data_ptr<int32_t>() : nullptr, bf_mut(q), bf_mut(k), bf_mut(v), (int)nq,
-                       (int)nkv, D, (int)seq_len, total, kcp, vcp, sp);
+                       (int)nkv, D, (int)seq_len, total, kcp, vcp, sp, kv8);
   return {q, k, v};
 }
 

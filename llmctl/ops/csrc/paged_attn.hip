@@ -26,51 +26,59 @@ namespace llmctl {
 namespace {
 
 __global__ __launch_bounds__(256) void kv_write_kernel(const unsigned short* __restrict__ k,
-                                                        const unsigned short* __restrict__ v,
-                                                        unsigned short* __restrict__ kc,
-                                                        unsigned short* __restrict__ vc,
-                                                        const int64_t* __restrict__ slots, int N, int row8) {
-  // row8 = Hkv*D/8 vectors per token
+                                                        const unsigned short* __restrict__ v, void* __restrict__ kc,
+                                                        void* __restrict__ vc, const int64_t* __restrict__ slots,
+                                                        int N, int row8, bool fp8) {
+  // row8 = Hkv*D/8 vectors per token; fp8 caches take 8 B per vector
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)N * row8) return;
   const int t = i / row8, c = i % row8;
   const long slot = slots[t];
   if (slot < 0) return;
-  reinterpret_cast<uint4*>(kc)[slot * row8 + c] = reinterpret_cast<const uint4*>(k)[(long)t * row8 + c];
-  reinterpret_cast<uint4*>(vc)[slot * row8 + c] = reinterpret_cast<const uint4*>(v)[(long)t * row8 + c];
+  float x[8];
+  load8(k + ((long)t * row8 + c) * 8, x);
+  cache_store8(kc, (slot * row8 + c) * 8, x, fp8);
+  load8(v + ((long)t * row8 + c) * 8, x);
+  cache_store8(vc, (slot * row8 + c) * 8, x, fp8);
 }
 
-template <int D, int G, int U>
+template <int D, int G, int U, bool FP8 = false>
 __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short* __restrict__ q,
-                                                            const unsigned short* __restrict__ kc,
-                                                            const unsigned short* __restrict__ vc,
+                                                            const void* __restrict__ kc,
+                                                            const void* __restrict__ vc,
                                                             const int* __restrict__ block_tables,
                                                             const int* __restrict__ ctx_lens,
                                                             unsigned short* __restrict__ out,
                                                             float* __restrict__ part_o, float* __restrict__ part_ml,
                                                             int Hq, int Hkv, int block_size, int max_blocks,
                                                             float scale_log2, int nsplit) {
-  constexpr int LPT = D / 8;          // lanes per token (16 for D=128, 8 for D=64)
+  // EPL cache elements per lane per token: 8 (16 B of bf16), or 16 for fp8 caches with G <= 4 (the
+  // same 16 B per load, so a wave-instruction covers twice the tokens: a half-width load per lane
+  // would halve the bytes in flight of this latency-bound stream and gain nothing)
+  constexpr int EPL = (FP8 && G <= 4) ? 16 : 8;
+  constexpr int LPT = D / EPL;        // lanes per token (bf16: 16 for D=128, 8 for D=64)
   constexpr int TPW = 64 / LPT;       // tokens per wave-instruction
   __shared__ float sm_m[4 * TPW][G], sm_l[4 * TPW][G];
   __shared__ float sm_o[4 * TPW][G][D];
   const int seq = blockIdx.x / Hkv, hk = blockIdx.x % Hkv, split = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int sub = lane % LPT;         // which 8-element slice of D
+  const int sub = lane % LPT;         // which EPL-element slice of D
   const int tg = lane / LPT;          // token group inside the wave
   const int L = ctx_lens[seq];
   const int* bt = block_tables + (long)seq * max_blocks;
   // q slices for the group's heads
-  float qv[G][8];
+  float qv[G][EPL];
 #pragma unroll
-  for (int g = 0; g < G; ++g) load8(q + ((long)seq * Hq + hk * G + g) * D + sub * 8, qv[g]);
-  float m[G], l[G], o[G][8];
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int h = 0; h < EPL; h += 8) load8(q + ((long)seq * Hq + hk * G + g) * D + sub * EPL + h, qv[g] + h);
+  float m[G], l[G], o[G][EPL];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     m[g] = -INFINITY;
     l[g] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+    for (int j = 0; j < EPL; ++j) o[g][j] = 0.f;
   }
   // this workgroup's context split, then a contiguous token slice per wave
   const int chunk = (L + nsplit - 1) / nsplit;
@@ -85,14 +93,23 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
       const int tt = t + u * TPW;
       blk[u] = tt < t1 ? bt[tt / block_size] : -1;
     }
-    float kf[U][8], vf[U][8];
+    float kf[U][EPL], vf[U][EPL];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tt = t + u * TPW;
       if (blk[u] >= 0) {
-        const long base = ((long)blk[u] * block_size + (tt % block_size)) * kv_row + (long)hk * D + sub * 8;
-        load8(kc + base, kf[u]);
-        load8(vc + base, vf[u]);
+        const long base = ((long)blk[u] * block_size + (tt % block_size)) * kv_row + (long)hk * D + sub * EPL;
+        if constexpr (EPL == 16) {  // fp8: one 16-B load = 16 elements
+          const uint4 ku = *reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(kc) + base);
+          const uint4 vu = *reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(vc) + base);
+          fp8x8_to_f32(make_uint2(ku.x, ku.y), kf[u]);
+          fp8x8_to_f32(make_uint2(ku.z, ku.w), kf[u] + 8);
+          fp8x8_to_f32(make_uint2(vu.x, vu.y), vf[u]);
+          fp8x8_to_f32(make_uint2(vu.z, vu.w), vf[u] + 8);
+        } else {
+          cache_load8(kc, base, kf[u], FP8);
+          cache_load8(vc, base, vf[u], FP8);
+        }
       }
     }
 #pragma unroll
@@ -104,7 +121,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
       for (int g = 0; g < G; ++g) {
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += qv[g][j] * kf[u][j];
+        for (int j = 0; j < EPL; ++j) s += qv[g][j] * kf[u][j];
 #pragma unroll
         for (int off = LPT / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
         s *= scale_log2;
@@ -112,7 +129,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
         const float a = exp2f(m[g] - mn), p = exp2f(s - mn);
         l[g] = l[g] * a + p;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + p * vf[u][j];
+        for (int j = 0; j < EPL; ++j) o[g][j] = o[g][j] * a + p * vf[u][j];
         m[g] = mn;
       }
     }
@@ -126,7 +143,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
       sm_l[slot][g] = l[g];
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sm_o[slot][g][sub * 8 + j] = o[g][j];
+    for (int j = 0; j < EPL; ++j) sm_o[slot][g][sub * EPL + j] = o[g][j];
   }
   __syncthreads();
   // combine 4*TPW partials: thread -> (g, d)
@@ -199,7 +216,8 @@ void kv_cache_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cach
                     const at::Tensor& slot_mapping) {
   LLMCTL_CHECK(k.is_contiguous() && v.is_contiguous() && k_cache.is_contiguous() && v_cache.is_contiguous(),
                "kv_cache_write: contiguous tensors");
-  LLMCTL_CHECK(k.scalar_type() == at::kBFloat16 && k_cache.scalar_type() == at::kBFloat16, "kv_cache_write: bf16");
+  LLMCTL_CHECK(k.scalar_type() == at::kBFloat16 && kv_cache_ok(k_cache) && v_cache.scalar_type() == k_cache.scalar_type(),
+               "kv_cache_write: bf16 K/V into bf16 or fp8 (e4m3fn) caches");
   LLMCTL_CHECK(slot_mapping.scalar_type() == at::kLong && slot_mapping.numel() == k.size(0),
                "slot_mapping: int64 [N]");
   const int N = k.size(0);
@@ -210,7 +228,8 @@ void kv_cache_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cach
   const int row8 = row / 8;
   const long total = (long)N * row8;
   hipLaunchKernelGGL(kv_write_kernel, dim3((total + 255) / 256), dim3(256), 0, stream(), bf_ptr(k), bf_ptr(v),
-                     bf_mut(k_cache), bf_mut(v_cache), slot_mapping.data_ptr<int64_t>(), N, row8);
+                     k_cache.data_ptr(), v_cache.data_ptr(), slot_mapping.data_ptr<int64_t>(), N, row8,
+                     kv_fp8(k_cache));
 }
 
 namespace {
@@ -233,10 +252,18 @@ void launch_paged_decode(const unsigned short* q, const at::Tensor& k_cache,
   }
   dim3 grid(N * Hkv, nsplit), block(256);
   auto s = stream();
+  const bool fp8 = kv_fp8(k_cache);
 #define LAUNCH(DD, GG, UU)                                                                                         \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU>), grid, block, 0, s, q, bf_ptr(k_cache), bf_ptr(v_cache),   \
-                     block_tables.data_ptr<int>(), context_lens.data_ptr<int>(), bf_mut(out), po, pml, Hq, Hkv, bs,   \
-                     max_blocks, sl2, nsplit)
+  do {                                                                                                             \
+    if (fp8)                                                                                                       \
+      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU, true>), grid, block, 0, s, q, k_cache.data_ptr(),        \
+                         v_cache.data_ptr(), block_tables.data_ptr<int>(), context_lens.data_ptr<int>(),            \
+                         bf_mut(out), po, pml, Hq, Hkv, bs, max_blocks, sl2, nsplit);                             \
+    else                                                                                                           \
+      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU>), grid, block, 0, s, q, k_cache.data_ptr(),              \
+                         v_cache.data_ptr(), block_tables.data_ptr<int>(), context_lens.data_ptr<int>(),            \
+                         bf_mut(out), po, pml, Hq, Hkv, bs, max_blocks, sl2, nsplit);                             \
+  } while (0)
   if (D == 128) {
     if (G == 1) LAUNCH(128, 1, 4);
     else if (G == 2) LAUNCH(128, 2, 4);
@@ -264,9 +291,8 @@ void launch_paged_decode(const unsigned short* q, const at::Tensor& k_cache,
 void check_paged_inputs(const at::Tensor& k_cache, const at::Tensor& v_cache, const at::Tensor& block_tables,
                         const at::Tensor& context_lens, int N, int Hq, int D) {
   LLMCTL_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.sizes() == k_cache.sizes() &&
-                   v_cache.is_contiguous() && k_cache.scalar_type() == at::kBFloat16 &&
-                   v_cache.scalar_type() == at::kBFloat16,
-               "caches: contiguous bf16 [blocks, block_size, Hkv, D]");
+                   v_cache.is_contiguous() && kv_cache_ok(k_cache) && v_cache.scalar_type() == k_cache.scalar_type(),
+               "caches: contiguous bf16 or fp8 (e4m3fn) [blocks, block_size, Hkv, D]");
   LLMCTL_CHECK(block_tables.scalar_type() == at::kInt && block_tables.is_contiguous() &&
                    context_lens.scalar_type() == at::kInt && context_lens.is_contiguous(),
                "block_tables / context_lens must be contiguous int32");

@@ -28,8 +28,8 @@ constexpr float kPRescaleTh = 8.f;
 
 struct PPArgs {
   const unsigned short* q;
-  const unsigned short* kc;
-  const unsigned short* vc;
+  const void* kc;  // bf16 or fp8 e4m3fn cache (FP8 template)
+  const void* vc;
   unsigned short* o;
   const int* bt;    // [N, maxb] block tables
   const int* cu_q;  // [N + 1] packed query offsets
@@ -40,7 +40,7 @@ struct PPArgs {
   float scale_log2;
 };
 
-template <int HD>
+template <int HD, bool FP8 = false>
 __global__ __launch_bounds__(256, 2) void paged_prefill_kernel(PPArgs a) {
   constexpr int NKS = HD / 16, NDB = HD / 32, ROWB = HD * 2, CPR = HD / 8;
   constexpr int LD_ITERS = PKB * CPR / 256;
@@ -91,8 +91,8 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_kernel(PPArgs a) {
       if (key < ctx) {
         const long slot = (long)btn[key / a.bs] * a.bs + key % a.bs;
         const long off = slot * kv_row + (long)hk * HD + ch * 8;
-        kst[it] = gload16(a.kc + off);
-        vst[it] = gload16(a.vc + off);
+        kst[it] = cache_load8_bf16(a.kc, off, FP8);  // fp8: 8 B loaded, widened to the bf16 LDS image
+        vst[it] = cache_load8_bf16(a.vc, off, FP8);
       } else {
         kst[it] = make_uint4(0, 0, 0, 0);
         vst[it] = make_uint4(0, 0, 0, 0);
@@ -212,9 +212,8 @@ at::Tensor paged_prefill_attention(const at::Tensor& q, const at::Tensor& k_cach
   const int Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(2), bs = k_cache.size(1);
   LLMCTL_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128");
   LLMCTL_CHECK(k_cache.size(3) == D && Hq % Hkv == 0, "paged_prefill_attention: head shapes");
-  LLMCTL_CHECK(q.scalar_type() == at::kBFloat16 && k_cache.scalar_type() == at::kBFloat16 &&
-                   v_cache.scalar_type() == at::kBFloat16,
-               "paged_prefill_attention: bf16");
+  LLMCTL_CHECK(q.scalar_type() == at::kBFloat16 && kv_cache_ok(k_cache) && v_cache.scalar_type() == k_cache.scalar_type(),
+               "paged_prefill_attention: bf16 q, bf16 or fp8 (e4m3fn) caches");
   LLMCTL_CHECK(q.stride(2) == 1 && q.stride(0) % 8 == 0 && q.stride(1) % 8 == 0 &&
                    (reinterpret_cast<uintptr_t>(q.data_ptr()) & 15) == 0,
                "paged_prefill_attention: q rows 16-B aligned, d contiguous");
@@ -229,11 +228,14 @@ at::Tensor paged_prefill_attention(const at::Tensor& q, const at::Tensor& k_cach
   auto o = at::empty_like(q, q.options().memory_format(at::MemoryFormat::Contiguous));
   const long nwork = work.numel();
   if (nwork == 0 || q.size(0) == 0) return o;
-  PPArgs a{bf_ptr(q), bf_ptr(k_cache), bf_ptr(v_cache), bf_mut(o), block_tables.data_ptr<int>(), cu_q.data_ptr<int>(),
+  PPArgs a{bf_ptr(q), k_cache.data_ptr(), v_cache.data_ptr(), bf_mut(o), block_tables.data_ptr<int>(), cu_q.data_ptr<int>(),
            ctx_lens.data_ptr<int>(), work.data_ptr<int>(), Hq, Hkv, bs, (int)block_tables.size(1),
            q.stride(0), q.stride(1), o.stride(0), o.stride(1), (float)(scale * 1.4426950408889634)};
   const dim3 grid((unsigned)(nwork * Hq)), block(256);
-  if (D == 128) hipLaunchKernelGGL(paged_prefill_kernel<128>, grid, block, 0, stream(), a);
+  const bool fp8 = kv_fp8(k_cache);
+  if (D == 128 && fp8) hipLaunchKernelGGL((paged_prefill_kernel<128, true>), grid, block, 0, stream(), a);
+  else if (D == 128) hipLaunchKernelGGL(paged_prefill_kernel<128>, grid, block, 0, stream(), a);
+  else if (fp8) hipLaunchKernelGGL((paged_prefill_kernel<64, true>), grid, block, 0, stream(), a);
   else hipLaunchKernelGGL(paged_prefill_kernel<64>, grid, block, 0, stream(), a);
   return o;
 }

@@ -327,9 +327,8 @@ __global__ __launch_bounds__(256) void decode_fin_rope_kernel(const float* __res
                                                               const int* __restrict__ pos,
                                                               const int64_t* __restrict__ slots,
                                                               unsigned short* __restrict__ q,
-                                                              unsigned short* __restrict__ kc,
-                                                              unsigned short* __restrict__ vc, int M, int nq, int nkv,
-                                                              int D, int KS) {
+                                                              void* __restrict__ kc, void* __restrict__ vc, int M,
+                                                              int nq, int nkv, int D, int KS, bool kv8) {
   const int CH = D >> 4, NH = nq + 2 * nkv, half = D >> 1;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)M * NH * CH) return;
@@ -364,17 +363,18 @@ __global__ __launch_bounds__(256) void decode_fin_rope_kernel(const float* __res
       o2[j] = b[j];
     }
   }
-  unsigned short* dst;
   if (h < nq) {
-    dst = q + ((long)t * nq + h) * D;
+    unsigned short* dst = q + ((long)t * nq + h) * D;
+    store8(dst + c * 8, o1);
+    store8(dst + half + c * 8, o2);
   } else {
     const long sl = slots[t];
     if (sl < 0) return;
     const bool isk = h < nq + nkv;
-    dst = (isk ? kc : vc) + (sl * nkv + (isk ? h - nq : h - nq - nkv)) * (long)D;
+    const long e = (sl * nkv + (isk ? h - nq : h - nq - nkv)) * (long)D;  // element index, either cache type
+    cache_store8(isk ? kc : vc, e + c * 8, o1, kv8);
+    cache_store8(isk ? kc : vc, e + half + c * 8, o2, kv8);
   }
-  store8(dst + c * 8, o1);
-  store8(dst + half + c * 8, o2);
 }
 
 // gate/up projection [M, 2F] -> act = silu(g) * u [M, F]; thread = 4 columns of one token
@@ -625,10 +625,10 @@ at::Tensor decode_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w, const
                "decode_qkv_rope_cache: positions int32 [M]");
   LLMCTL_CHECK(slots.scalar_type() == at::kLong && slots.is_contiguous() && slots.numel() == M,
                "decode_qkv_rope_cache: slots int64 [M]");
-  LLMCTL_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.scalar_type() == at::kBFloat16 &&
-                   v_cache.sizes() == k_cache.sizes() && k_cache.dim() == 4 && k_cache.size(2) == nkv &&
-                   k_cache.size(3) == D,
-               "decode_qkv_rope_cache: k/v cache contiguous bf16 [blocks, block_size, Hkv, D]");
+  LLMCTL_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && kv_cache_ok(k_cache) &&
+                   v_cache.scalar_type() == k_cache.scalar_type() && v_cache.sizes() == k_cache.sizes() &&
+                   k_cache.dim() == 4 && k_cache.size(2) == nkv && k_cache.size(3) == D,
+               "decode_qkv_rope_cache: k/v cache contiguous bf16 or fp8 (e4m3fn) [blocks, block_size, Hkv, D]");
   const c10::DeviceGuard guard(x.device());
   at::Tensor ws;
   const int KS = decode_partials(x, w, ws);
@@ -636,8 +636,8 @@ at::Tensor decode_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w, const
   const long total = (long)M * NH * (D / 16);
   hipLaunchKernelGGL(decode_fin_rope_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(),
                      ws.data_ptr<float>(), bias_ptr(bias), cosT.data_ptr<float>(), sinT.data_ptr<float>(),
-                     positions.data_ptr<int>(), slots.data_ptr<int64_t>(), bf_mut(q), bf_mut(k_cache),
-                     bf_mut(v_cache), M, (int)nq, (int)nkv, D, KS);
+                     positions.data_ptr<int>(), slots.data_ptr<int64_t>(), bf_mut(q), k_cache.data_ptr(),
+                     v_cache.data_ptr(), M, (int)nq, (int)nkv, D, KS, kv_fp8(k_cache));
   return q;
 }
 

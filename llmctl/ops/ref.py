@@ -256,6 +256,8 @@ def kv_cache_write(k, v, k_cache, v_cache, slot_mapping):
     vc = v_cache.view(nb * bs, *v_cache.shape[2:])
     idx = slot_mapping.long()
     valid = idx >= 0
+    if kc.dtype == torch.float8_e4m3fn:  # saturating, like the kernels (torch's cast maps > 448 to NaN)
+        k, v = k.float().clamp(-448.0, 448.0), v.float().clamp(-448.0, 448.0)
     kc[idx[valid]] = k[valid].to(kc.dtype)
     vc[idx[valid]] = v[valid].to(vc.dtype)
 

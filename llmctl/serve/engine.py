@@ -50,7 +50,8 @@ class InferenceEngine:
                  max_batch_tokens: int = 8192, max_model_len: Optional[int] = None, kv_cache_fraction: float = 0.85,
                  block_size: int = 16, num_kv_blocks: Optional[int] = None, scheduler: str = "dynamic",
                  use_graphs: bool = True, seed: int = 0, pc=None, prefix_caching: bool = True,
-                 tuning_cache: Optional[str] = None, perf_knobs: Optional[Dict] = None):
+                 tuning_cache: Optional[str] = None, perf_knobs: Optional[Dict] = None,
+                 kv_cache_dtype: str = "auto"):
         from llmctl.config import knobs as perf
 
         self.knobs = perf.configure(perf_knobs)  # defaults + perf_knobs + LLMCTL_KNOBS
@@ -82,6 +83,14 @@ class InferenceEngine:
         self.max_model_len = max_model_len or cfg.max_position_embeddings
         self.block_size = block_size
         self.max_blocks_per_seq = (self.max_model_len + block_size - 1) // block_size
+        # KV cache element: the model dtype ("auto"), or OCP fp8 e4m3fn ("fp8": half the bytes per
+        # token, so twice the blocks and half the decode attention's HBM stream; saturating at +-448)
+        if kv_cache_dtype in ("auto", "model", "bf16", "bfloat16"):
+            self.kv_dtype = dtype
+        elif kv_cache_dtype in ("fp8", "fp8_e4m3", "float8_e4m3fn"):
+            self.kv_dtype = torch.float8_e4m3fn
+        else:
+            raise ValueError(f"kv_cache_dtype must be auto / bf16 / fp8, got {kv_cache_dtype!r}")
         if num_kv_blocks is None:
             if self.device.type == "cuda":
                 torch.cuda.synchronize()
@@ -90,12 +99,12 @@ class InferenceEngine:
             else:
                 budget = 256 * 2 ** 20
             num_kv_blocks = PagedKVCache.blocks_for_memory(budget, cfg.layers, block_size, cfg.kv_heads // self.tp,
-                                                           cfg.head_dim, torch.tensor([], dtype=dtype).element_size())
+                                                           cfg.head_dim, torch.tensor([], dtype=self.kv_dtype).element_size())
             num_kv_blocks = min(num_kv_blocks, 1 << 20)
             num_kv_blocks = self._agree_min(num_kv_blocks)
         # each TP rank caches only its own KV heads
         self.kv_cache = PagedKVCache(cfg.layers, num_kv_blocks, block_size, cfg.kv_heads // self.tp, cfg.head_dim,
-                                     dtype, self.device)
+                                     self.kv_dtype, self.device)
         self.kv = make_kv_manager(num_kv_blocks, block_size)
         self.prefix_cache = PrefixCache(self.kv, block_size) if prefix_caching else None
         self.scheduler = ContinuousBatchScheduler(self.kv, max_batch_size, max_batch_tokens, self.max_model_len,

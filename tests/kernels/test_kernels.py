@@ -351,6 +351,85 @@ def test_kv_cache_write(native_lib):
     assert torch.equal(kc, kr) and torch.equal(vc, vr)
 
 
+# ---- fp8 (OCP e4m3fn) paged KV caches: writes saturate like the oracle's cast; reads widen in-kernel
+FP8 = torch.float8_e4m3fn
+
+
+def test_kv_cache_write_fp8(native_lib):
+    nb, bs, H, D = 8, 16, 4, 128
+    kc = torch.zeros(nb, bs, H, D, dtype=FP8, device=DEV)
+    vc = torch.zeros_like(kc)
+    k, v = _bf(10, H, D, seed=51, scale=4.0), _bf(10, H, D, seed=52, scale=4.0)
+    k[0, 0, :4] = torch.tensor([600.0, -1000.0, 447.0, 1e-5])  # saturation / subnormal
+    slots = torch.tensor([0, 5, 17, 33, 127, 64, 65, 66, -1, 100], device=DEV)
+    native_lib.kv_cache_write(k, v, kc, vc, slots)
+    kr, vr = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.kv_cache_write(k, v, kr, vr, slots)
+    assert torch.equal(kc.view(torch.uint8), kr.view(torch.uint8)) and torch.equal(vc.view(torch.uint8), vr.view(torch.uint8))
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 32, 128), (8, 2, 128), (16, 2, 64)])
+@pytest.mark.parametrize("splits", ["1", "auto"])
+def test_paged_attention_decode_fp8(native_lib, Hq, Hkv, D, splits):
+    """Decode attention over an fp8 cache == the fp32 oracle on the same (dequantised) cache."""
+    from llmctl.config.knobs import configure
+
+    configure({"decode_splits": 0 if splits == "auto" else int(splits)})
+    nb, bs, N, maxb = 400, 16, 3, 128
+    kc = _bf(nb, bs, Hkv, D, seed=61).to(FP8)
+    vc = _bf(nb, bs, Hkv, D, seed=62).to(FP8)
+    lens = torch.tensor([2, 700, 2048], dtype=torch.int32, device=DEV)
+    bt = torch.randperm(nb, device=DEV)[: N * maxb].view(N, maxb).to(torch.int32).contiguous()
+    q = _bf(N, Hq, D, seed=63)
+    o = native_lib.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+    orf = ref.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+    assert _row_err(o, orf) < 2e-2, _row_err(o, orf)
+
+
+@pytest.mark.parametrize("with_pos", [False, True])
+def test_rope_qkv_cache_fused_write_fp8(native_lib, with_pos):
+    """RoPE + paged-KV write into an fp8 cache: rows within one e4m3 step of the bf16 path's
+    rows cast by the oracle (the kernel rounds the fp32 rotation directly, the oracle its bf16)."""
+    nq, nkv, D, S, bs, nb = 8, 2, 128, 24, 16, 16
+    T = 2 * S
+    qkv = _bf(T, (nq + 2 * nkv) * D, seed=81)
+    cos, sin = ref.rope_tables(S + 8, D, base=10000.0, device=DEV)
+    pos = torch.randint(0, S + 8, (T,), device=DEV, dtype=torch.int32) if with_pos else None
+    slots = torch.randperm(nb * bs, device=DEV)[:T]
+    slots[3] = -1
+    kc = torch.zeros(nb, bs, nkv, D, dtype=FP8, device=DEV)
+    vc = torch.zeros_like(kc)
+    q, k, v = native_lib.rope_qkv_cache_fwd(qkv, cos, sin, nq, nkv, S, pos, kc, vc, slots)
+    kr, vr = torch.zeros_like(kc), torch.zeros_like(kc)
+    ref.kv_cache_write(k, v, kr, vr, slots)
+    for got, want in ((kc, kr), (vc, vr)):
+        g, w = got.float(), want.float()
+        assert ((g - w).abs() <= w.abs() * 2.0 ** -3 + 2.0 ** -9).all()
+    assert torch.equal(vc.view(torch.uint8), vr.view(torch.uint8))  # V is not rotated: exact
+
+
+def test_decode_qkv_rope_cache_fused_fp8(native_lib):
+    """The decode QKV finalize writing an fp8 cache == the bf16-cache path's rows cast to fp8
+    (within one e4m3 step; V exact)."""
+    M, K, nq, nkv, D, bs, nb = 16, 2048, 8, 2, 128, 16, 8
+    N = (nq + 2 * nkv) * D
+    x = _bf(M, K, seed=91)
+    w = _bf(N, K, scale=0.05, seed=92)
+    cos, sin = ref.rope_tables(256, D, base=10000.0, device=DEV)
+    pos = torch.randint(0, 256, (M,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nb * bs, device=DEV)[:M]
+    kc = torch.zeros(nb, bs, nkv, D, dtype=FP8, device=DEV)
+    vc = torch.zeros_like(kc)
+    q = native_lib.decode_qkv_rope_cache(x, w, None, cos, sin, nq, nkv, pos, kc, vc, slots)
+    kb = torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV)
+    vb = torch.zeros_like(kb)
+    q2 = native_lib.decode_qkv_rope_cache(x, w, None, cos, sin, nq, nkv, pos, kb, vb, slots)
+    assert torch.equal(q, q2)
+    for got, want in ((kc, kb), (vc, vb)):
+        w32 = want.float().clamp(-448, 448)
+        assert ((got.float() - w32).abs() <= w32.abs() * 2.0 ** -3 + 2.0 ** -9).all()
+
+
 def test_sampling(native_lib):
     torch.manual_seed(0)
     N, V = 64, 32000

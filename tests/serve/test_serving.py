@@ -416,3 +416,24 @@ def test_async_decode_pipeline_matches_sync_cpu(temp):
             assert e.stats.get("async_continued", 0) >= 4
         assert e.kv.num_free_blocks == 64  # every block back (speculative rows included)
     assert outs[0] == outs[1]
+
+
+def test_engine_fp8_kv_cache_cpu():
+    """kv_cache_dtype="fp8": the cache holds float8_e4m3fn (a quarter of the CPU oracle's fp32 bytes,
+    so four times the blocks for the same budget), the oracle paths quantise on write and widen
+    on read, and the first greedy token (prefill attends the un-quantised K/V) is unchanged."""
+    import torch
+
+    from llmctl.serve.engine import InferenceEngine
+    from llmctl.serve.scheduler import SamplingParams
+
+    prompts = [[(7 * i + r) % 200 + 1 for i in range(24 + 5 * r)] for r in range(3)]
+    p = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    engs = {k: InferenceEngine("tiny", device="cpu", max_batch_size=3, kv_cache_dtype=k) for k in ("auto", "fp8")}
+    assert engs["fp8"].kv_cache.k.dtype == torch.float8_e4m3fn
+    assert engs["fp8"].kv_cache.num_blocks == 4 * engs["auto"].kv_cache.num_blocks
+    outs = {k: [s.output_ids for s in e.generate(prompts, p)] for k, e in engs.items()}
+    assert all(len(o) == 6 for o in outs["fp8"])
+    assert [o[0] for o in outs["fp8"]] == [o[0] for o in outs["auto"]]
+    with pytest.raises(ValueError):
+        InferenceEngine("tiny", device="cpu", kv_cache_dtype="int4")
