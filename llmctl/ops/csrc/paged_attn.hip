@@ -6,19 +6,18 @@
 // Decode (one new token per sequence) is HBM-bound: every cached K/V byte is read once.
 // Workgroup = one (sequence, kv-head, context split) = 4 waves; the `group = Hq/Hkv` query
 // heads that share the kv head are handled together so GQA reads K/V once per group.  Inside a
-// wave, 16 lanes cooperate on one token (8 contiguous bf16 of D=128 per lane: 16-B loads), so
-// a wave-instruction covers 4 tokens; q·k is reduced over the 16 lanes with xor-shuffles.
-// Each wave streams a contiguous slice of its split with an online softmax, U tokens per lane
-// per iteration: all U block-table reads, then all 2U K/V loads are issued before the first
-// use (with one token per iteration the loop is latency-bound: one 16-B load pair in flight
-// per lane).  The 4 waves (and the 4 token groups within each wave) are merged through LDS.
-// Small batches (N·Hkv workgroups, far fewer than the ~2k that cover 256 CUs' HBM latency)
-// split the context over `nsplit` workgroups (flash-decoding): fp32 partials (O unnormalised,
-// running max m in the log2 domain, sum l) + a combine kernel.  nsplit depends only on
-// shapes (batch rounded up to the decode-graph bucket), so a captured hipGraph stays valid for
-// any context lengths and graph / eager decode agree bit for bit.
+// wave, LPT lanes cooperate on one token, each holding one 16-B slice of its K / V row (8 bf16,
+// or 16 fp8 e4m3 elements), so a wave-instruction covers 64/LPT tokens; q.k is reduced over the
+// LPT lanes with xor-shuffles.  Each wave streams a contiguous slice of its split, software-
+// pipelined: stage i+1's raw K/V loads are in flight while stage i runs its online softmax
+// (paged_decode_kernel below).  The 4 waves (and the token groups within each wave) are merged
+// through LDS.  Small grids split the context over `nsplit` workgroups (flash-decoding): fp32
+// partials (O unnormalised, running max m in the log2 domain, sum l) + a combine kernel.
+// nsplit depends only on shapes (batch rounded up to the decode-graph bucket), so a captured
+// hipGraph stays valid for any context lengths and graph / eager decode agree bit for bit.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -42,98 +41,19 @@ __global__ __launch_bounds__(256) void kv_write_kernel(const unsigned short* __r
   cache_store8(vc, (slot * row8 + c) * 8, x, fp8);
 }
 
-template <int D, int G, int U, bool FP8 = false>
-__global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short* __restrict__ q,
-                                                            const void* __restrict__ kc,
-                                                            const void* __restrict__ vc,
-                                                            const int* __restrict__ block_tables,
-                                                            const int* __restrict__ ctx_lens,
-                                                            unsigned short* __restrict__ out,
-                                                            float* __restrict__ part_o, float* __restrict__ part_ml,
-                                                            int Hq, int Hkv, int block_size, int max_blocks,
-                                                            float scale_log2, int nsplit) {
-  // EPL cache elements per lane per token: 8 (16 B of bf16), or 16 for fp8 caches with G <= 4 (the
-  // same 16 B per load, so a wave-instruction covers twice the tokens: a half-width load per lane
-  // would halve the bytes in flight of this latency-bound stream and gain nothing)
-  constexpr int EPL = (FP8 && G <= 4) ? 16 : 8;
-  constexpr int LPT = D / EPL;        // lanes per token (bf16: 16 for D=128, 8 for D=64)
-  constexpr int TPW = 64 / LPT;       // tokens per wave-instruction
+// Merge the 4 waves x TPW token groups' online-softmax partials (m, l in the log2 domain, O
+// unnormalised) of one workgroup through LDS; write the normalised row (nsplit 1) or the split's
+// fp32 partial for paged_combine_kernel.
+template <int D, int G, int EPL>
+__device__ __forceinline__ void decode_merge(const float (&m)[G], const float (&l)[G], const float (&o)[G][EPL],
+                                             unsigned short* __restrict__ out, float* __restrict__ part_o,
+                                             float* __restrict__ part_ml, int seq, int hk, int Hq, int split,
+                                             int nsplit) {
+  constexpr int LPT = D / EPL, TPW = 64 / LPT;
   __shared__ float sm_m[4 * TPW][G], sm_l[4 * TPW][G];
   __shared__ float sm_o[4 * TPW][G][D];
-  const int seq = blockIdx.x / Hkv, hk = blockIdx.x % Hkv, split = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int sub = lane % LPT;         // which EPL-element slice of D
-  const int tg = lane / LPT;          // token group inside the wave
-  const int L = ctx_lens[seq];
-  const int* bt = block_tables + (long)seq * max_blocks;
-  // q slices for the group's heads
-  float qv[G][EPL];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int h = 0; h < EPL; h += 8) load8(q + ((long)seq * Hq + hk * G + g) * D + sub * EPL + h, qv[g] + h);
-  float m[G], l[G], o[G][EPL];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    m[g] = -INFINITY;
-    l[g] = 0.f;
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) o[g][j] = 0.f;
-  }
-  // this workgroup's context split, then a contiguous token slice per wave
-  const int chunk = (L + nsplit - 1) / nsplit;
-  const int c0 = min(L, split * chunk), c1 = min(L, c0 + chunk);
-  const int per_wave = (c1 - c0 + 3) / 4;
-  const int t0 = c0 + wave * per_wave, t1 = min(c1, t0 + per_wave);
-  const long kv_row = (long)Hkv * D;
-  for (int t = t0 + tg; t < t1; t += TPW * U) {
-    int blk[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tt = t + u * TPW;
-      blk[u] = tt < t1 ? bt[tt / block_size] : -1;
-    }
-    float kf[U][EPL], vf[U][EPL];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tt = t + u * TPW;
-      if (blk[u] >= 0) {
-        const long base = ((long)blk[u] * block_size + (tt % block_size)) * kv_row + (long)hk * D + sub * EPL;
-        if constexpr (EPL == 16) {  // fp8: one 16-B load = 16 elements
-          const uint4 ku = *reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(kc) + base);
-          const uint4 vu = *reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(vc) + base);
-          fp8x8_to_f32(make_uint2(ku.x, ku.y), kf[u]);
-          fp8x8_to_f32(make_uint2(ku.z, ku.w), kf[u] + 8);
-          fp8x8_to_f32(make_uint2(vu.x, vu.y), vf[u]);
-          fp8x8_to_f32(make_uint2(vu.z, vu.w), vf[u] + 8);
-        } else {
-          cache_load8(kc, base, kf[u], FP8);
-          cache_load8(vc, base, vf[u], FP8);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      // validity is uniform over the LPT lanes of a token group, so the shuffles below only
-      // ever read lanes that take the same branch
-      if (blk[u] < 0) continue;
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < EPL; ++j) s += qv[g][j] * kf[u][j];
-#pragma unroll
-        for (int off = LPT / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        s *= scale_log2;
-        const float mn = fmaxf(m[g], s);
-        const float a = exp2f(m[g] - mn), p = exp2f(s - mn);
-        l[g] = l[g] * a + p;
-#pragma unroll
-        for (int j = 0; j < EPL; ++j) o[g][j] = o[g][j] * a + p * vf[u][j];
-        m[g] = mn;
-      }
-    }
-  }
+  const int sub = lane % LPT, tg = lane / LPT;
   // publish per (wave, token-group) partials
   const int slot = wave * TPW + tg;
 #pragma unroll
@@ -173,6 +93,157 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
   }
 }
 
+// Software-pipelined form: the wave's token slice is walked in stages of U tokens per lane; the
+// raw 16-B K/V loads of stage i+1 are issued before stage i is computed (two register buffers of
+// raw cache bytes, converted at use), so a wave keeps its loads in flight through its own softmax
+// work.  Every lane loads every stage (tokens past the slice re-read its last token and are
+// masked to p = 0), keeping the control flow uniform and the vmcnt accounting exact.  Block ids
+// come from a 64-block window held one per lane (ds_bpermute per token, a reload every 64
+// blocks), so no block-table round trip precedes a K/V load.  The U tokens of a stage share one
+// running-max update (one rescale of O per stage, not per token).
+template <int D, int G, int U, bool FP8>
+__global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short* __restrict__ q,
+                                                             const void* __restrict__ kc,
+                                                             const void* __restrict__ vc,
+                                                             const int* __restrict__ block_tables,
+                                                             const int* __restrict__ ctx_lens,
+                                                             unsigned short* __restrict__ out,
+                                                             float* __restrict__ part_o, float* __restrict__ part_ml,
+                                                             int Hq, int Hkv, int block_size, int max_blocks,
+                                                             float scale_log2, int nsplit) {
+  constexpr int EPL = (FP8 && G <= 4) ? 16 : 8;  // elements per 16-B lane load (bf16 8, fp8 16)
+  constexpr int EB = FP8 ? 1 : 2;                // bytes per element
+  constexpr int NL = EPL * EB / 16;              // 16-B loads per lane per token row slice (1, or 2... below)
+  static_assert(EPL * EB == 16 || EPL * EB == 8, "slice of 8 or 16 B");
+  constexpr int LPT = D / EPL, TPW = 64 / LPT, SPAN = TPW * U;
+  using raw_t = typename std::conditional<EPL * EB == 16, uint4, uint2>::type;
+  (void)NL;
+  const int seq = blockIdx.x / Hkv, hk = blockIdx.x % Hkv, split = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane % LPT, tg = lane / LPT;
+  const int L = ctx_lens[seq];
+  const int* bt = block_tables + (long)seq * max_blocks;
+  float qv[G][EPL];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int h = 0; h < EPL; h += 8) load8(q + ((long)seq * Hq + hk * G + g) * D + sub * EPL + h, qv[g] + h);
+  float m[G], l[G], o[G][EPL];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) o[g][j] = 0.f;
+  }
+  const int chunk = (L + nsplit - 1) / nsplit;
+  const int c0 = min(L, split * chunk), c1 = min(L, c0 + chunk);
+  const int per_wave = (c1 - c0 + 3) / 4;
+  const int t0 = c0 + wave * per_wave, t1 = min(c1, t0 + per_wave);
+  const int nst = t1 > t0 ? (t1 - t0 + SPAN - 1) / SPAN : 0;  // stages (wave-uniform)
+  const long kv_row = (long)Hkv * D;
+  const unsigned char* kb = static_cast<const unsigned char*>(kc);
+  const unsigned char* vb = static_cast<const unsigned char*>(vc);
+  int wbase = t0 / block_size;
+  int wblk = bt[min(wbase + lane, max_blocks - 1)];
+  auto issue = [&](int st, raw_t (&kr)[U], raw_t (&vr)[U]) {
+    const int ts = t0 + st * SPAN;
+    const int last = min(t1 - 1, ts + SPAN - 1) / block_size;
+    if (last - wbase >= 64) {  // wave-uniform: slide the block-id window
+      wbase = ts / block_size;
+      wblk = bt[min(wbase + lane, max_blocks - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tt = min(ts + tg + u * TPW, t1 - 1);
+      const int b = __shfl(wblk, tt / block_size - wbase);
+      const long e = ((long)b * block_size + (tt % block_size)) * kv_row + (long)hk * D + sub * EPL;
+      kr[u] = *reinterpret_cast<const raw_t*>(kb + e * EB);
+      vr[u] = *reinterpret_cast<const raw_t*>(vb + e * EB);
+    }
+  };
+  auto unpack = [&](const raw_t& r, float* x) {
+    if constexpr (FP8) {
+      if constexpr (EPL == 16) {
+        fp8x8_to_f32(make_uint2(r.x, r.y), x);
+        fp8x8_to_f32(make_uint2(r.z, r.w), x + 8);
+      } else {
+        fp8x8_to_f32(r, x);
+      }
+    } else {
+      const unsigned w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[2 * j] = __uint_as_float(w[j] << 16);
+        x[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      }
+    }
+  };
+  auto compute = [&](int st, const raw_t (&kr)[U], const raw_t (&vr)[U]) {
+    const int ts = t0 + st * SPAN;
+    float sc[U][G];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float kf[EPL];
+      unpack(kr[u], kf);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) a += qv[g][j] * kf[j];
+        sc[u][g] = a;
+      }
+    }
+#pragma unroll
+    for (int off = LPT / 2; off > 0; off >>= 1)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int g = 0; g < G; ++g) sc[u][g] += __shfl_xor(sc[u][g], off);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = ts + tg + u * TPW < t1;
+#pragma unroll
+      for (int g = 0; g < G; ++g) sc[u][g] = ok ? sc[u][g] * scale_log2 : -INFINITY;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float mx = m[g];
+#pragma unroll
+      for (int u = 0; u < U; ++u) mx = fmaxf(mx, sc[u][g]);
+      const float ms = mx == -INFINITY ? 0.f : mx;
+      const float al = exp2f(m[g] - ms);
+      l[g] *= al;
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) o[g][j] *= al;
+      m[g] = mx;
+#pragma unroll
+      for (int u = 0; u < U; ++u) sc[u][g] = exp2f(sc[u][g] - ms);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float vf[EPL];
+      unpack(vr[u], vf);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        l[g] += sc[u][g];
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) o[g][j] += sc[u][g] * vf[j];
+      }
+    }
+  };
+  raw_t kA[U], vA[U], kB[U], vB[U];
+  if (nst > 0) issue(0, kA, vA);
+  for (int st = 0; st < nst; st += 2) {
+    if (st + 1 < nst) issue(st + 1, kB, vB);
+    compute(st, kA, vA);
+    if (st + 1 >= nst) break;
+    if (st + 2 < nst) issue(st + 2, kA, vA);
+    compute(st + 1, kB, vB);
+  }
+  decode_merge<D, G, EPL>(m, l, o, out, part_o, part_ml, seq, hk, Hq, split, nsplit);
+}
+
 // out[row] = sum_s O_s 2^(m_s - M) / sum_s l_s 2^(m_s - M); empty splits carry m = -inf.
 template <int D>
 __global__ __launch_bounds__(D) void paged_combine_kernel(const float* __restrict__ part_o,
@@ -194,20 +265,19 @@ __global__ __launch_bounds__(D) void paged_combine_kernel(const float* __restric
   out[row * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
 }
 
-// Context splits per (sequence, kv-head): enough workgroups for ~4-8 per CU, at least 128
-// context slots per split, at most 16.  The batch is rounded up to a power of two, as the
-// serving engine's decode-graph buckets are, so graph replay and eager decode pick the same
-// split.  Knob decode_splits > 0 overrides (tests, A/B; llmctl.config.knobs).
+// Context splits per (sequence, kv-head): about 512 workgroups (2 per CU: each wave keeps two
+// stages of loads in flight, so 8 waves per CU cover the HBM latency), at least 256 context slots
+// per split, at most 64.  The batch is rounded up to a power of two, as the serving engine's
+// decode-graph buckets are, so graph replay and eager decode pick the same split.  Measured
+// (tools/paged_decode_bw.py, profiles/paged_decode_r5.txt): GPT-7B 16 x 2k best at 1 split
+// (512 workgroups), 32 q / 8 kv heads 16 x 2k and 4 x 4k at 2-4, one 8k sequence at 16+.
+// Knob decode_splits > 0 overrides (tests, A/B; llmctl.config.knobs).
 int decode_splits(int N, int Hkv, int max_ctx) {
   if (const int64_t v = knob("decode_splits", 0); v > 0) return (int)std::min<int64_t>(v, 64);
   int np = 1;
   while (np < N) np *= 2;
   const int wgs = std::max(1, np * Hkv);
-  // a (sequence, kv-head) grid of 512-1023 workgroups needs only ~4 per CU: GPT-7B, 16 x 2k decode
-  // step 7.04 ms at 2 splits vs 7.11 at 4 (the auto value before), 7.5 at 3, 8.6 at 1
-  // (profiles/serve_r2_session6.txt); other grids (unmeasured against this) keep ~8 per CU
-  const int target = (wgs >= 512 && wgs < 1024) ? 1024 : 2048;
-  return std::max(1, std::min({(target + wgs - 1) / wgs, max_ctx / 128, 16}));
+  return std::max(1, std::min({(512 + wgs - 1) / wgs, max_ctx / 256, 64}));
 }
 
 }  // namespace
@@ -253,28 +323,28 @@ void launch_paged_decode(const unsigned short* q, const at::Tensor& k_cache,
   dim3 grid(N * Hkv, nsplit), block(256);
   auto s = stream();
   const bool fp8 = kv_fp8(k_cache);
-#define LAUNCH(DD, GG, UU)                                                                                         \
+#define LAUNCH(DD, GG)                                                                                             \
   do {                                                                                                             \
     if (fp8)                                                                                                       \
-      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU, true>), grid, block, 0, s, q, k_cache.data_ptr(),        \
+      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, 2, true>), grid, block, 0, s, q, k_cache.data_ptr(),        \
                          v_cache.data_ptr(), block_tables.data_ptr<int>(), context_lens.data_ptr<int>(),            \
                          bf_mut(out), po, pml, Hq, Hkv, bs, max_blocks, sl2, nsplit);                             \
     else                                                                                                           \
-      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, UU>), grid, block, 0, s, q, k_cache.data_ptr(),              \
-                         v_cache.data_ptr(), block_tables.data_ptr<int>(), context_lens.data_ptr<int>(),            \
-                         bf_mut(out), po, pml, Hq, Hkv, bs, max_blocks, sl2, nsplit);                             \
+      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, (GG == 8 ? 4 : 2), false>), grid, block, 0, s, q,     \
+                         k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),                     \
+                         context_lens.data_ptr<int>(), bf_mut(out), po, pml, Hq, Hkv, bs, max_blocks, sl2, nsplit); \
   } while (0)
   if (D == 128) {
-    if (G == 1) LAUNCH(128, 1, 4);
-    else if (G == 2) LAUNCH(128, 2, 4);
-    else if (G == 4) LAUNCH(128, 4, 2);
-    else if (G == 8) LAUNCH(128, 8, 2);
+    if (G == 1) LAUNCH(128, 1);
+    else if (G == 2) LAUNCH(128, 2);
+    else if (G == 4) LAUNCH(128, 4);
+    else if (G == 8) LAUNCH(128, 8);
     else LLMCTL_CHECK(false, "GQA group must be 1/2/4/8");
   } else if (D == 64) {
-    if (G == 1) LAUNCH(64, 1, 4);
-    else if (G == 2) LAUNCH(64, 2, 4);
-    else if (G == 4) LAUNCH(64, 4, 2);
-    else if (G == 8) LAUNCH(64, 8, 2);
+    if (G == 1) LAUNCH(64, 1);
+    else if (G == 2) LAUNCH(64, 2);
+    else if (G == 4) LAUNCH(64, 4);
+    else if (G == 8) LAUNCH(64, 8);
     else LLMCTL_CHECK(false, "GQA group must be 1/2/4/8");
   } else {
     LLMCTL_CHECK(false, "head_dim must be 64 or 128");

@@ -36,6 +36,7 @@ from llmctl import ops
 from llmctl.config.knobs import use as use_knobs
 from llmctl.io.artifact import load_model
 from llmctl.models import DecoderLM
+from llmctl.utils.env import graph_capture_gc_guard
 
 from .block_manager import PagedKVCache, make_kv_manager
 from .prefix_cache import PrefixCache
@@ -456,7 +457,7 @@ class InferenceEngine:
                 self._graph_body(bufs)
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture_gc_guard(), torch.cuda.graph(g):
             self._graph_body(bufs)
         self._graphs[nb] = (g, bufs)
 

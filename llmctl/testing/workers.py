@@ -231,7 +231,9 @@ def custom_ar_check(rank: int, world: int, sizes=(8, 4096, 65536, 524288), iters
         torch.cuda.current_stream().wait_stream(s)
         dist.barrier()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        from llmctl.utils.env import graph_capture_gc_guard
+
+        with graph_capture_gc_guard(), torch.cuda.graph(graph):
             car.all_reduce(static, out)
         dist.barrier()
         for it in range(5):

@@ -7,6 +7,7 @@ exposed through the ``torch.cuda`` namespace and the ``"nccl"`` backend is RCCL.
 
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass
 
@@ -88,3 +89,24 @@ def install_hang_dump() -> None:
         import faulthandler
 
         faulthandler.dump_traceback_later(float(s), repeat=True, exit=False)
+
+
+@contextlib.contextmanager
+def graph_capture_gc_guard():
+    """Collect garbage before a hipGraph capture and keep the cyclic collector off during it.
+
+    A collection inside a capture can run the destructor of an unrelated, unreachable engine
+    whose captured graphs then free their executable graphs and pools on a capturing device;
+    the runtime refuses that ("operation not permitted when stream is capturing") and the error
+    raised inside a destructor aborts the process.  torch's ``torch.cuda.graph`` only collects
+    beforehand under ``force_cudagraph_gc``."""
+    import gc
+
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
