@@ -15,7 +15,9 @@
 // Measured (uncached weights, tools/decode_bench.py): 1.5-1.9x hipBLASLt on the narrow
 // projections (o-proj, down-proj), slower than it on the wide ones at M >= 8, which is why
 // ops.decode_linear routes only out_features <= 4096 here.
-// Weights are read with plain loads (they are not reused within a step; the L2/MALL decides).
+// Weights are read with plain loads (they are not reused within a step; the L2/MALL decides):
+// non-temporal (nt) weight loads measured 30 % slower on every GPT-7B projection (qkv 35.4 vs
+// 24.6 us, decode step 8.26 vs 6.87 ms; profiles/decode_gemm_nt_r5.txt).
 #include <cstdlib>
 
 #include "attn_common.h"
