@@ -234,13 +234,17 @@ __global__ __launch_bounds__(256) void decode_gemm_pre_kernel(const unsigned sho
   const int kc0 = blockIdx.y * KC;
   const int kc = min(KC, K - kc0);
   const int nb = kc / KBLK;
-  const unsigned short* wrow = w + (long)(n0 + r) * K + kc0 + 32 * g;
+  // MFMA step s of lane group g reads k = 32 s + 8 g: a wave-instruction covers 64 contiguous bytes
+  // of each of its 16 rows (k = 32 g + 8 s, 4 x 16 B at a 64-B stride per row, measured 0.6 % slower
+  // in the decode step: profiles/decode_gemm_var_r5.txt)
+  const int ko = 8 * g, ks = 32;
+  const unsigned short* wrow = w + (long)(n0 + r) * K + kc0 + ko;
   bf16x8_t a[NB][4];
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     const int bu = u < nb ? u : nb - 1;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) a[u][s] = ld16(wrow + bu * KBLK + 8 * s);
+    for (int s = 0; s < 4; ++s) a[u][s] = ld16(wrow + bu * KBLK + ks * s);
   }
   __builtin_amdgcn_sched_barrier(0);
   const int c8 = kc >> 3;
@@ -251,13 +255,13 @@ __global__ __launch_bounds__(256) void decode_gemm_pre_kernel(const unsigned sho
     *reinterpret_cast<uint4*>(xs + m * XST + c * 8) = v;
   }
   __syncthreads();
-  const unsigned short* xrow = xs + r * XST + 32 * g;
+  const unsigned short* xrow = xs + r * XST + ko;
   f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     if (u < nb) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma16(a[u][s], *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 8 * s), acc);
+      for (int s = 0; s < 4; ++s) acc = mfma16(a[u][s], *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + ks * s), acc);
     }
   }
   if (r >= M) return;
@@ -473,6 +477,14 @@ void launch_decode(const at::Tensor& x, const at::Tensor& w, const unsigned shor
   }
 }
 
+// v3 decode GEMM launch: K chunks of 1024 (KS = gridDim.y), 8 K blocks in flight per lane
+void launch_pre(const unsigned short* x, const unsigned short* w, const unsigned short* bp, unsigned short* y,
+                float* wsp, int M, int N, int K, int KS) {
+  constexpr int KC = 1024;
+  hipLaunchKernelGGL((decode_gemm_pre_kernel<KC / KBLK>), dim3(N / 64, KS), dim3(256), (size_t)16 * (KC + 8) * 2,
+                     stream(), x, w, bp, y, wsp, M, N, K);
+}
+
 // v3 launch (KC = 1024): chunk partials + decode_finalize_kernel
 void launch_decode_v3(const at::Tensor& x, const at::Tensor& w, const unsigned short* bp, at::Tensor& y, int M, int N,
                       int K) {
@@ -485,8 +497,7 @@ void launch_decode_v3(const at::Tensor& x, const at::Tensor& w, const unsigned s
     ws = at::empty({(long)KS * M * N}, x.options().dtype(at::kFloat));
     wsp = ws.data_ptr<float>();
   }
-  hipLaunchKernelGGL((decode_gemm_pre_kernel<KC / KBLK>), dim3(N / 64, KS), dim3(256), (size_t)16 * (KC + 8) * 2,
-                     stream(), bf_ptr(x), bf_ptr(w), bp, bf_mut(y), wsp, M, N, K);
+  launch_pre(bf_ptr(x), bf_ptr(w), bp, bf_mut(y), wsp, M, N, K, KS);
   if (KS > 1) {
     const long n4 = (long)M * N / 4;
     hipLaunchKernelGGL(decode_finalize_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream(), wsp, bp,
@@ -588,9 +599,7 @@ int decode_partials(const at::Tensor& x, const at::Tensor& w, at::Tensor& ws) {
   const int KS = (K + KC - 1) / KC;
   ws = at::empty({(long)KS * M * N}, x.options().dtype(at::kFloat));
   if (decode_v3())  // (its LDS row stride is the full chunk's, whatever K is)
-    hipLaunchKernelGGL((decode_gemm_pre_kernel<kFusedKC / KBLK>), dim3(N / 64, KS), dim3(256),
-                       (size_t)16 * (kFusedKC + 8) * 2, stream(), bf_ptr(x),
-                       bf_ptr(w), nullptr, nullptr, ws.data_ptr<float>(), M, N, K);
+    launch_pre(bf_ptr(x), bf_ptr(w), nullptr, nullptr, ws.data_ptr<float>(), M, N, K, KS);
   else
     hipLaunchKernelGGL((decode_gemm_kernel<4>), dim3(N / 64, KS), dim3(256), (size_t)16 * (KC + 8) * 2, stream(),
                        bf_ptr(x), bf_ptr(w), nullptr, nullptr, ws.data_ptr<float>(), M, N, K, KC);

@@ -37,7 +37,9 @@ def main():
         row = {"shape": name, "N": N, "K": K, "M": a.m}
         runs = [(f"c{c}", lambda w, c=c: ops.skinny_linear_cfg(x, w, None, c)) for c in a.configs]
         runs.append(("hipblaslt", lambda w: torch.nn.functional.linear(x, w)))
+        ref = (x.float() @ ws[0].float().t())
         for tag, fn in runs:
+            row[tag + "_err"] = round(((fn(ws[0]).float() - ref).abs().max() / ref.abs().max()).item(), 5)
             # captured: a graph of `iters` back-to-back calls times the kernels, not the host
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
