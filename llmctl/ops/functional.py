@@ -424,7 +424,9 @@ def decode_linear(x, w, b=None):
     (``csrc/skinny_gemm.hip``) where they beat hipBLASLt on uncached weights
     (``profiles/skinny_sweep_r2*.jsonl``): every projection up to 16 tokens (at 16 tokens the
     LDS-staged v2 kernel: QKV 3.78 vs 3.55 TB/s, up 3.89 vs 3.35, down 3.16 vs 2.07) and the
-    4096 x 4096 o-projection up to 32; wide projections at 17-32 tokens stay on hipBLASLt.
+    4096 x 4096 o-projection up to 32; wide projections at 17-32 tokens stay on hipBLASLt, and so
+    does the vocabulary projection (out features >= 16384) from 8 tokens (GPT-7B LM head at 16
+    tokens: 59.7 vs 68.5 us, ``profiles/decode_gemm_nt_r5.txt``).
     Knob ``skinny_gemm``: ``off`` / ``all`` force the library / kernel path (A/B)."""
     from llmctl.exec.linear import forward_linear
 
@@ -439,7 +441,8 @@ def decode_linear(x, w, b=None):
     if (mode != "off" and use_native(x) and x.dim() == 2 and M <= 32 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and w.shape[0] % 16 == 0 and x.shape[1] % 128 == 0
             and x.is_contiguous() and w.is_contiguous() and (b is None or b.is_contiguous())
-            and (mode == "all" or M <= 16 or (w.shape[0] <= 4096 and x.shape[1] <= 4096))):
+            and (mode == "all" or (M <= 16 and not (M >= 8 and w.shape[0] >= 16384))
+                 or (w.shape[0] <= 4096 and x.shape[1] <= 4096))):
         return native().skinny_linear(x, w, b)
     return forward_linear(x, w, b)
 
