@@ -84,14 +84,16 @@ __device__ __forceinline__ void cache_load8(const void* base, long e, float* x, 
   if (fp8) fp8x8_to_f32(*reinterpret_cast<const uint2*>(static_cast<const unsigned char*>(base) + e), x);
   else load8(static_cast<const unsigned short*>(base) + e, x);
 }
-// ... as 8 bf16 (16 B) for an LDS image
+// ... as 8 bf16 (16 B) for an LDS image.  An e4m3 value (3 mantissa bits) is exact in bf16, so its
+// f32 image has a zero low half: the bf16 is the f32's high 16 bits (one v_perm_b32 per pair).
 __device__ __forceinline__ uint4 cache_load8_bf16(const void* base, long e, bool fp8) {
   if (!fp8) return *reinterpret_cast<const uint4*>(static_cast<const unsigned short*>(base) + e);
   float x[8];
   fp8x8_to_f32(*reinterpret_cast<const uint2*>(static_cast<const unsigned char*>(base) + e), x);
   unsigned w[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) w[j] = (unsigned)f2bf(x[2 * j]) | ((unsigned)f2bf(x[2 * j + 1]) << 16);
+  for (int j = 0; j < 4; ++j)
+    w[j] = __builtin_amdgcn_perm(__float_as_uint(x[2 * j + 1]), __float_as_uint(x[2 * j]), 0x07060302u);
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
