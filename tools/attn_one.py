@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Run ONE flash-attention kernel repeatedly (for rocprofv3 --pmc passes):
-    attn_one.py {fwd|dkv|dq|dkv_old|dkv_pipe} [iters] [B S H D]"""
+    attn_one.py {fwd|dkv|dq|dkv_old|dkv_pipe} [iters] [B S H D]
+Env ATTN_KNOBS="name=value,..." sets native knobs first (e.g. fa_w64=3)."""
+import os
 import sys
 
 import torch
@@ -12,6 +14,9 @@ kind = sys.argv[1]
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 B, S, H, D = (int(x) for x in (sys.argv[3:7] if len(sys.argv) > 6 else (8, 2048, 32, 128)))
 ops = _lib.native()
+for kv in filter(None, os.environ.get("ATTN_KNOBS", "").split(",")):
+    name, val = kv.split("=")
+    ops.set_knob(name, int(val))
 q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
 k, v, do = (torch.randn_like(q) for _ in range(3))
 scale = D ** -0.5
