@@ -188,10 +188,12 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
       unpack(kr[u], kf);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float a = 0.f;
+        // four independent partial sums: a single serial FMA chain of EPL links sat on the
+        // critical path of every stage (latency, not issue, bounds this loop)
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < EPL; ++j) a += qv[g][j] * kf[j];
-        sc[u][g] = a;
+        for (int j = 0; j < EPL; ++j) a[j & 3] = fmaf(qv[g][j], kf[j], a[j & 3]);
+        sc[u][g] = (a[0] + a[1]) + (a[2] + a[3]);
       }
     }
 #pragma unroll
