@@ -219,6 +219,21 @@ def test_tp2_serving_two_processes_custom_ar_graphs(native_lib):
     _forced_match(2, "tiny", 3e-2)
 
 
+def test_tp2_serving_fp8_kv_cache(native_lib):
+    """TP=2 serving with the fp8 (e4m3fn) paged KV cache: each rank's head shard of the cache is
+    fp8; logits follow the TP=1 fp8 engine on the same token stream."""
+    from llmctl.testing.harness import run_ranks
+    from llmctl.testing.numerics import row_err
+    from llmctl.testing.workers import serve_forced_gpu
+
+    kw = {"kv_cache_dtype": "fp8"}
+    ref = serve_forced_gpu(0, 1, 8, "tiny", None, None, kw)
+    out = run_ranks(serve_forced_gpu, 2, 8, "tiny", ref["tokens"], None, kw, timeout=300)
+    assert out[0]["graph_replays"] > 0
+    err = row_err(_logit_rows(out[0]), _logit_rows(ref))
+    assert err < 3e-2, err
+
+
 def test_tp8_serving_eight_processes_custom_ar_graphs(native_lib):
     """BASELINE config #5's degree (TP=8), eight processes on one GPU: one query and one KV head
     per rank (tiny-wide), 8-way custom all-reduces.  One hardware queue per rank: the custom
