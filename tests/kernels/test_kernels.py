@@ -386,6 +386,32 @@ def test_paged_attention_decode_fp8(native_lib, Hq, Hkv, D, splits):
     assert _row_err(o, orf) < 2e-2, _row_err(o, orf)
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("Hq,Hkv,bs", [(8, 8, 16), (16, 4, 8)])
+def test_paged_attention_decode_long_slices(native_lib, fp8, Hq, Hkv, bs):
+    """One context split over long contexts: a wave's token slice spans more than the 64 block
+    ids it holds one per lane, so the window slides mid-slice (and the last stage is partial)."""
+    from llmctl.config.knobs import configure
+
+    configure({"decode_splits": 1})
+    try:
+        D, N = 128, 2
+        lens = torch.tensor([5003, 4097], dtype=torch.int32, device=DEV)
+        maxb = (5003 + bs - 1) // bs + 3
+        nb = N * maxb + 5
+        kc = _bf(nb, bs, Hkv, D, seed=91)
+        vc = _bf(nb, bs, Hkv, D, seed=92)
+        if fp8:
+            kc, vc = kc.to(FP8), vc.to(FP8)
+        bt = torch.randperm(nb, device=DEV)[: N * maxb].view(N, maxb).to(torch.int32).contiguous()
+        q = _bf(N, Hq, D, seed=93)
+        o = native_lib.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+        orf = ref.paged_attention_decode(q, kc, vc, bt, lens, D ** -0.5)
+        assert _row_err(o, orf) < 2e-2, _row_err(o, orf)
+    finally:
+        configure({})
+
+
 @pytest.mark.parametrize("with_pos", [False, True])
 def test_rope_qkv_cache_fused_write_fp8(native_lib, with_pos):
     """RoPE + paged-KV write into an fp8 cache: rows within one e4m3 step of the bf16 path's
