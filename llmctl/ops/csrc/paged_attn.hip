@@ -113,11 +113,9 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(const unsigned short*
                                                              float scale_log2, int nsplit) {
   constexpr int EPL = (FP8 && G <= 4) ? 16 : 8;  // elements per 16-B lane load (bf16 8, fp8 16)
   constexpr int EB = FP8 ? 1 : 2;                // bytes per element
-  constexpr int NL = EPL * EB / 16;              // 16-B loads per lane per token row slice (1, or 2... below)
   static_assert(EPL * EB == 16 || EPL * EB == 8, "slice of 8 or 16 B");
   constexpr int LPT = D / EPL, TPW = 64 / LPT, SPAN = TPW * U;
-  using raw_t = typename std::conditional<EPL * EB == 16, uint4, uint2>::type;
-  (void)NL;
+  using raw_t = typename std::conditional<EPL * EB == 16, uint4, uint2>::type;  // one lane's raw slice
   const int seq = blockIdx.x / Hkv, hk = blockIdx.x % Hkv, split = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane % LPT, tg = lane / LPT;
