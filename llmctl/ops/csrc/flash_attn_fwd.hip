@@ -29,7 +29,7 @@
 //     K/V loop starts at the block's first document start, so the work is sum(doc_len^2);
 //   * small grids (e.g. a single 2k-token prefill: 1 x 32 heads x 16 q-blocks = 512 workgroups,
 //     all resident at once, so the run time is the heaviest block's): the K/V range of every
-//     q-block is split over two workgroups that write fp32 partial outputs + LSEs, merged by a
+//     q-block is split over two workgroups that write bf16 partial outputs + fp32 LSEs, merged by a
 //     combine kernel — halves the critical path of the causal tail.
 // Outputs O [B,S,Hq,HD] bf16 and LSE [B,Hq,S] fp32 (natural log) for the backward pass.
 #include <cstdlib>
@@ -59,7 +59,7 @@ struct FwdArgs {
   long o_sb, o_ss, o_sh;
   float scale_log2;  // softmax_scale * log2(e)
   const int* doc;    // [B, S] document start per token, or nullptr
-  float* o_part;     // SPLIT: [2, B, S, Hq, HD] fp32 normalised partial outputs
+  unsigned short* o_part;  // SPLIT: [2, B, S, Hq, HD] bf16 normalised partial outputs
   float* lse_part;   // SPLIT: [2, B, Hq, S] natural-log partial LSEs
   int prio;          // raise the wave priority over its MFMA phases (A/B knob fa_prio)
   unsigned* stamp;   // fa_fwd_w64a_kernel diagnostic build: [workgroup][wave][16] cycle totals
@@ -308,14 +308,20 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
   if constexpr (SPLIT) {
     if (my_q < a.S) {
       const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
-      float* Op = a.o_part + ((((long)part * a.B + b) * a.S + my_q) * a.Hq + hq) * HD;
+      // bf16 partials: each is a normalised output, rounded like the final one; the combine's
+      // convex merge adds at most about half an ulp (fp32 partials: 69.9 vs 65.4 us per
+      // single-prompt layer, tools/attn_prefill_split_ab.py)
+      unsigned short* Op = a.o_part + ((((long)part * a.B + b) * a.S + my_q) * a.Hq + hq) * HD;
 #pragma unroll
       for (int d = 0; d < NDB; ++d)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int col = d * 32 + 8 * g + 4 * hh;
-          *reinterpret_cast<float4*>(Op + col) =
-              make_float4(o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+          unsigned short w4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w4[j] = f2bf(o[d][4 * g + j] * inv);
+          *reinterpret_cast<uint2*>(Op + col) =
+              make_uint2((unsigned)w4[0] | ((unsigned)w4[1] << 16), (unsigned)w4[2] | ((unsigned)w4[3] << 16));
         }
       if (hh == 0)
         a.lse_part[(((long)part * a.B + b) * a.Hq + hq) * a.S + my_q] =
@@ -744,7 +750,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 
 // merge the two K/V-range halves: lse = logaddexp(l0, l1), o = o0 e^(l0-lse) + o1 e^(l1-lse)
 template <int HD>
-__global__ __launch_bounds__(256) void fa_combine_kernel(const float* __restrict__ o_part,
+__global__ __launch_bounds__(256) void fa_combine_kernel(const unsigned short* __restrict__ o_part,
                                                          const float* __restrict__ lse_part,
                                                          unsigned short* __restrict__ o, float* __restrict__ lse,
                                                          int B, int S, int Hq, long o_sb, long o_ss, long o_sh) {
@@ -770,16 +776,11 @@ __global__ __launch_bounds__(256) void fa_combine_kernel(const float* __restrict
   }
   const long ob = row * HD + sub * 8;
   const long osz = (long)B * S * Hq * HD;
-  float out[8];
+  float out[8], x0[8], x1[8];
+  load8(o_part + ob, x0);
+  load8(o_part + osz + ob, x1);
 #pragma unroll
-  for (int j = 0; j < 8; j += 4) {
-    const float4 x0 = *reinterpret_cast<const float4*>(o_part + ob + j);
-    const float4 x1 = *reinterpret_cast<const float4*>(o_part + osz + ob + j);
-    out[j] = w0 * x0.x + w1 * x1.x;
-    out[j + 1] = w0 * x0.y + w1 * x1.y;
-    out[j + 2] = w0 * x0.z + w1 * x1.z;
-    out[j + 3] = w0 * x0.w + w1 * x1.w;
-  }
+  for (int j = 0; j < 8; ++j) out[j] = w0 * x0[j] + w1 * x1[j];
   store8(o + b * o_sb + (long)sq * o_ss + (long)hq * o_sh + sub * 8, out);
   if (sub == 0) lse[li] = l;
 }
@@ -800,9 +801,9 @@ std::tuple<at::Tensor, at::Tensor> fwd_launch(const at::Tensor& q, at::Tensor& o
   if (const int64_t e = knob("fa_split", -1); e == 0) split = false;
   else if (e == 1) split = causal && !(doc_start.has_value() && doc_start->defined()) && nqb >= 2;
   if (split) {
-    auto o_part = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
+    auto o_part = at::empty({2, B, S, Hq, D}, q.options());
     auto lse_part = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));
-    a.o_part = o_part.data_ptr<float>();
+    a.o_part = bf_mut(o_part);
     a.lse_part = lse_part.data_ptr<float>();
     dim3 g2((unsigned)(2 * B * Hq * nqb));
     const long threads = (long)B * S * Hq * (D / 8);
