@@ -19,7 +19,7 @@ def run_serving_benchmark(model: str = "gpt-7b", prompt_length: int = 2048, gen_
                           qps: Optional[float] = None, num_requests: int = 16, max_batch_size: int = 16,
                           device: str = "auto", max_batch_tokens: Optional[int] = None, use_graphs: bool = True,
                           seed: int = 0, warmup: bool = True, scheduler: str = "dynamic",
-                          kv_cache_dtype: str = "auto") -> Dict[str, Any]:
+                          kv_cache_dtype: str = "auto", weight_dtype: str = "auto") -> Dict[str, Any]:
     import torch
 
     from llmctl.serve.engine import InferenceEngine
@@ -30,7 +30,8 @@ def run_serving_benchmark(model: str = "gpt-7b", prompt_length: int = 2048, gen_
                           max_batch_tokens=max_batch_tokens or max(prompt_length,
                                                                    4096 if scheduler == "prefill_first" else 8192),
                           max_model_len=max_len,
-                          use_graphs=use_graphs, seed=seed, scheduler=scheduler, kv_cache_dtype=kv_cache_dtype)
+                          use_graphs=use_graphs, seed=seed, scheduler=scheduler, kv_cache_dtype=kv_cache_dtype,
+                          weight_dtype=weight_dtype)
     V = eng.cfg.vocab_size
     rng = random.Random(seed)
     params = SamplingParams(max_tokens=gen_length, temperature=0.0, ignore_eos=True)
@@ -70,7 +71,7 @@ def run_serving_benchmark(model: str = "gpt-7b", prompt_length: int = 2048, gen_
     return {
         "model": eng.cfg.name, "device": str(eng.device), "num_requests": num_requests,
         "prompt_length": prompt_length, "gen_length": gen_length, "qps": qps, "max_batch_size": max_batch_size, "scheduler": scheduler,
-        "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""),
+        "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""), "decode_weight_dtype": eng.weight_dtype,
         "max_batch_tokens": eng.scheduler.max_batch_tokens,
         "ttft_p50_ms": round(float(np.percentile(ttft, 50)) * 1e3, 2),
         "ttft_p90_ms": round(float(np.percentile(ttft, 90)) * 1e3, 2),

@@ -51,6 +51,7 @@ def e2e(
     max_batch_tokens: Optional[int] = typer.Option(None, help="Prefill token budget per step (default: 4096 "
                                                                  "for prefill_first, 8192 otherwise)"),
     kv_cache_dtype: str = typer.Option("auto", help="KV cache element: auto (model dtype) | fp8 (e4m3fn)"),
+    weight_dtype: str = typer.Option("auto", help="Decode projection weights: auto (model dtype) | fp8 (e4m3fn, row scales)"),
 ) -> None:
     """End-to-end serving benchmark (TTFT p50/p99, TPOT, tokens/s).
 
@@ -62,7 +63,8 @@ def e2e(
 
     res = run_serving_benchmark(model=model, prompt_length=prompt_length, gen_length=gen_length, qps=qps,
                                 num_requests=num_requests, max_batch_size=max_batch_size, device=device,
-                                scheduler=scheduler, max_batch_tokens=max_batch_tokens, kv_cache_dtype=kv_cache_dtype)
+                                scheduler=scheduler, max_batch_tokens=max_batch_tokens, kv_cache_dtype=kv_cache_dtype,
+                                weight_dtype=weight_dtype)
     console.print_json(json.dumps(res))
 
 

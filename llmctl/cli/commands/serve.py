@@ -33,6 +33,8 @@ def start(
     cuda_graphs: bool = typer.Option(True, "--hip-graphs/--no-hip-graphs", help="Capture decode steps in hipGraphs"),
     tensor_parallel: int = typer.Option(1, help="TP degree (run under torchrun for >1)"),
     kv_cache_dtype: str = typer.Option("auto", help="KV cache element: auto (the model dtype) or fp8 (OCP e4m3fn)"),
+    weight_dtype: str = typer.Option("auto", help="Decode projection weights: auto (the model dtype) or fp8 (OCP "
+                                                  "e4m3fn, per-row scales; prefill keeps the model dtype)"),
 ) -> None:
     """Start the inference server."""
     from llmctl.serve.server import create_inference_server
@@ -60,14 +62,14 @@ def start(
                "--max-batch-size", str(max_batch_size), "--max-batch-tokens", str(max_batch_tokens),
                "--max-concurrent", str(max_concurrent), "--kv-cache-fraction", str(kv_cache_fraction),
                "--block-size", str(block_size), "--scheduler", scheduler,
-               "--kv-cache-dtype", kv_cache_dtype] + ([] if cuda_graphs else ["--no-graphs"])
+               "--kv-cache-dtype", kv_cache_dtype, "--weight-dtype", weight_dtype] + ([] if cuda_graphs else ["--no-graphs"])
         console.print(f"[yellow]Tensor parallel: {tensor_parallel} ranks (RCCL)[/yellow]")
         raise typer.Exit(subprocess.call(cmd))
     server = create_inference_server(model_path=artifact, host=host, port=port, max_batch_size=max_batch_size,
                                      max_batch_tokens=max_batch_tokens, max_concurrent=max_concurrent,
                                      scheduler=scheduler, device=device, kv_cache_fraction=kv_cache_fraction,
                                      block_size=block_size, use_graphs=cuda_graphs, tensor_parallel=tensor_parallel,
-                                     kv_cache_dtype=kv_cache_dtype)
+                                     kv_cache_dtype=kv_cache_dtype, weight_dtype=weight_dtype)
     try:
         server.run()
     except KeyboardInterrupt:
@@ -90,4 +92,4 @@ def main(
         raise typer.Exit(1)
     start(artifact=artifact, port=port, host=host, scheduler="dynamic", max_batch_size=8, max_batch_tokens=8192,
           max_concurrent=128, device=device, kv_cache_fraction=0.85, block_size=16, cuda_graphs=True,
-          tensor_parallel=1, kv_cache_dtype="auto")
+          tensor_parallel=1, kv_cache_dtype="auto", weight_dtype="auto")

@@ -15,6 +15,7 @@ from .functional import (
     decode_attention_qkv,
     decode_fused_ok,
     decode_linear,
+    decode_linear_fp8,
     decode_linear_add_rmsnorm,
     decode_qkv_rope_cache,
     decode_up_swiglu,

@@ -49,10 +49,11 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("paged_attention_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, float scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w, Tensor? bias) -> Tensor");
   m.def("skinny_linear_cfg(Tensor x, Tensor w, Tensor? bias, int config) -> Tensor");
-  m.def("decode_qkv_rope_cache(Tensor x, Tensor w, Tensor? bias, Tensor cos, Tensor sin, int nq, int nkv, Tensor positions, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> Tensor");
-  m.def("decode_up_swiglu(Tensor x, Tensor w, Tensor? bias) -> Tensor");
-  m.def("decode_linear_partials(Tensor x, Tensor w) -> Tensor");
-  m.def("decode_linear_add_rmsnorm(Tensor x, Tensor w, Tensor? bias, Tensor residual, Tensor norm_w, float eps) -> (Tensor, Tensor)");
+  m.def("decode_qkv_rope_cache(Tensor x, Tensor w, Tensor? bias, Tensor cos, Tensor sin, int nq, int nkv, Tensor positions, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots, Tensor? w_scale=None) -> Tensor");
+  m.def("decode_up_swiglu(Tensor x, Tensor w, Tensor? bias, Tensor? w_scale=None) -> Tensor");
+  m.def("decode_linear_partials(Tensor x, Tensor w, Tensor? w_scale=None) -> Tensor");
+  m.def("decode_linear_add_rmsnorm(Tensor x, Tensor w, Tensor? bias, Tensor residual, Tensor norm_w, float eps, Tensor? w_scale=None) -> (Tensor, Tensor)");
+  m.def("decode_linear_fp8(Tensor x, Tensor w, Tensor w_scale, Tensor? bias) -> Tensor");
   m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor uniform) -> Tensor");
   // benchmarks / tuning (gemm_bf16.hip, hbm_stream.hip)
   m.def("gemm_bf16(Tensor a, Tensor b) -> Tensor");

@@ -283,6 +283,92 @@ __global__ __launch_bounds__(256) void decode_gemm_pre_kernel(const unsigned sho
   }
 }
 
+// fp8 (OCP e4m3fn) weights, per-output-row fp32 scales (W8A16, decode only): the weight stream is
+// half the bytes.  A lane's 16-B load holds 16 consecutive k of its row (k = 64 h + 16 g + [0, 16)
+// in each 128-deep block, h = 0, 1), i.e. the A operands of two MFMA steps; e4m3 -> bf16 is exact
+// (the f32 image's high half), and the B operand (token rows staged in LDS) follows the same k
+// order.  The row scale multiplies the fp32 partial before it is stored, so the finalize passes
+// (RoPE / SwiGLU / residual + RMSNorm) are the bf16 path's.
+__device__ __forceinline__ bf16x8_t fp8x8_to_bf16x8(unsigned lo, unsigned hi) {
+  float x[8];
+  fp8x8_to_f32(make_uint2(lo, hi), x);
+  bf16x8_t r;
+  unsigned* w = reinterpret_cast<unsigned*>(&r);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_perm(__float_as_uint(x[2 * j + 1]), __float_as_uint(x[2 * j]), 0x07060302u);
+  return r;
+}
+
+template <int NB, int RT = 1>
+__global__ __launch_bounds__(256) void decode_gemm_w8_kernel(const unsigned short* __restrict__ x,
+                                                             const unsigned char* __restrict__ w,
+                                                             const float* __restrict__ wscale,
+                                                             float* __restrict__ ws, int M, int N, int K) {
+  // RT 16-row tiles per wave (a workgroup covers 64 RT weight rows): the token rows staged in LDS
+  // serve RT times the weight bytes
+  extern __shared__ __attribute__((aligned(16))) unsigned char xs_raw[];
+  unsigned short* xs = reinterpret_cast<unsigned short*>(xs_raw);
+  constexpr int KC = NB * KBLK, XST = KC + 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 64 * RT + wave * 16 * RT;
+  const int kc0 = blockIdx.y * KC;
+  const int kc = min(KC, K - kc0);
+  const int nb = kc / KBLK;
+  uint4 a[RT][NB][2];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const unsigned char* wrow = w + (long)(n0 + 16 * t + r) * K + kc0 + 16 * g;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int bu = u < nb ? u : nb - 1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) a[t][u][h] = *reinterpret_cast<const uint4*>(wrow + bu * KBLK + 64 * h);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const int c8 = kc >> 3;
+  for (int i = threadIdx.x; i < 16 * c8; i += 256) {
+    const int m = i / c8, c = i - m * c8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (m < M) v = *reinterpret_cast<const uint4*>(x + (long)m * K + kc0 + c * 8);
+    *reinterpret_cast<uint4*>(xs + m * XST + c * 8) = v;
+  }
+  __syncthreads();
+  const unsigned short* xrow = xs + r * XST + 16 * g;
+  f32x4_t acc[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    if (u < nb) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bf16x8_t x0 = *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 64 * h);
+        const bf16x8_t x1 = *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 64 * h + 8);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+          const uint4 q = a[t][u][h];
+          acc[t] = mfma16(fp8x8_to_bf16x8(q.x, q.y), x0, acc[t]);
+          acc[t] = mfma16(fp8x8_to_bf16x8(q.z, q.w), x1, acc[t]);
+        }
+      }
+    }
+  }
+  if (r >= M) return;
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float4 sc = *reinterpret_cast<const float4*>(wscale + n);
+    f32x4_t o = acc[t];
+    o[0] *= sc.x;
+    o[1] *= sc.y;
+    o[2] *= sc.z;
+    o[3] *= sc.w;
+    *reinterpret_cast<f32x4_t*>(ws + ((long)blockIdx.y * M + r) * N + n) = o;
+  }
+}
+
 // y[m][n] = bf16(sum_s ws[s][m][n] + bias[n]), 4 columns per thread
 __global__ __launch_bounds__(256) void decode_finalize_kernel(const float* __restrict__ ws,
                                                               const unsigned short* __restrict__ bias,
@@ -578,8 +664,9 @@ constexpr int kFusedKC = 1024;  // K chunk of the fused projections (config 23's
 void check_decode_operands(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                            const char* who) {
   LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(), who, ": 2-D contiguous");
-  LLMCTL_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
-               who, ": bf16 GPU operands");
+  LLMCTL_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 &&
+                   (w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kFloat8_e4m3fn),
+               who, ": bf16 GPU activations, bf16 or fp8 (e4m3fn) weights");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
   LLMCTL_CHECK(w.size(1) == K && M >= 1 && M <= 16 && N % 64 == 0 && K % KBLK == 0, who,
                ": needs M <= 16, N % 64 == 0, K % 128 == 0 (got ", M, "x", N, "x", K, ")");
@@ -592,13 +679,26 @@ const unsigned short* bias_ptr(const c10::optional<at::Tensor>& bias) {
   return bias.has_value() && bias->defined() ? bf_ptr(*bias) : nullptr;
 }
 
-// x W^T as fp32 K-chunk partials ws [KS][M][N]; returns KS
-int decode_partials(const at::Tensor& x, const at::Tensor& w, at::Tensor& ws) {
+bool w_fp8(const at::Tensor& w) { return w.scalar_type() == at::kFloat8_e4m3fn; }
+
+// x W^T as fp32 K-chunk partials ws [KS][M][N]; returns KS.  fp8 W: w_scale [N] fp32 row scales.
+int decode_partials(const at::Tensor& x, const at::Tensor& w, at::Tensor& ws,
+                    const c10::optional<at::Tensor>& w_scale = c10::nullopt) {
   const int M = x.size(0), K = x.size(1), N = w.size(0);
   const int KC = std::min(kFusedKC, K);
   const int KS = (K + KC - 1) / KC;
   ws = at::empty({(long)KS * M * N}, x.options().dtype(at::kFloat));
-  if (decode_v3())  // (its LDS row stride is the full chunk's, whatever K is)
+  if (w_fp8(w)) {
+    // (two 16-row tiles per wave, and K chunks of 512 / 2048, measured 3-6 % slower in the decode
+    // step: profiles/decode_w8_r5.txt)
+    LLMCTL_CHECK(w_scale.has_value() && w_scale->defined() && w_scale->scalar_type() == at::kFloat &&
+                     w_scale->is_contiguous() && w_scale->numel() == N && w_scale->is_cuda(),
+                 "fp8 decode weights need fp32 row scales [N] on the GPU");
+    hipLaunchKernelGGL((decode_gemm_w8_kernel<kFusedKC / KBLK>), dim3(N / 64, KS), dim3(256),
+                       (size_t)16 * (kFusedKC + 8) * 2, stream(), bf_ptr(x),
+                       static_cast<const unsigned char*>(w.data_ptr()), w_scale->data_ptr<float>(),
+                       ws.data_ptr<float>(), M, N, K);
+  } else if (decode_v3())  // (its LDS row stride is the full chunk's, whatever K is)
     launch_pre(bf_ptr(x), bf_ptr(w), nullptr, nullptr, ws.data_ptr<float>(), M, N, K, KS);
   else
     hipLaunchKernelGGL((decode_gemm_kernel<4>), dim3(N / 64, KS), dim3(256), (size_t)16 * (KC + 8) * 2, stream(),
@@ -608,12 +708,12 @@ int decode_partials(const at::Tensor& x, const at::Tensor& w, at::Tensor& ws) {
 }  // namespace
 
 // x W^T as fp32 K-chunk partials [KS, M, N] (the fused decode attention sums them itself)
-at::Tensor decode_linear_partials(const at::Tensor& x, const at::Tensor& w) {
+at::Tensor decode_linear_partials(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& w_scale) {
   check_decode_operands(x, w, c10::nullopt, "decode_linear_partials");
   const int M = x.size(0), N = w.size(0);
   const c10::DeviceGuard guard(x.device());
   at::Tensor ws;
-  const int KS = decode_partials(x, w, ws);
+  const int KS = decode_partials(x, w, ws, w_scale);
   return ws.view({KS, M, N});
 }
 
@@ -621,7 +721,7 @@ at::Tensor decode_linear_partials(const at::Tensor& x, const at::Tensor& w) {
 at::Tensor decode_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                  const at::Tensor& cosT, const at::Tensor& sinT, int64_t nq, int64_t nkv,
                                  const at::Tensor& positions, at::Tensor& k_cache, at::Tensor& v_cache,
-                                 const at::Tensor& slots) {
+                                 const at::Tensor& slots, const c10::optional<at::Tensor>& w_scale) {
   check_decode_operands(x, w, bias, "decode_qkv_rope_cache");
   const int M = x.size(0), N = w.size(0);
   const int NH = nq + 2 * nkv;
@@ -642,7 +742,7 @@ at::Tensor decode_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w, const
                "decode_qkv_rope_cache: k/v cache contiguous bf16 or fp8 (e4m3fn) [blocks, block_size, Hkv, D]");
   const c10::DeviceGuard guard(x.device());
   at::Tensor ws;
-  const int KS = decode_partials(x, w, ws);
+  const int KS = decode_partials(x, w, ws, w_scale);
   auto q = at::empty({M, nq, D}, x.options());
   const long total = (long)M * NH * (D / 16);
   hipLaunchKernelGGL(decode_fin_rope_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(),
@@ -653,12 +753,13 @@ at::Tensor decode_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w, const
 }
 
 // act [M, F] = silu(g) * u of the gate/up projection gu = x W^T + b  ([M, 2F], gate first)
-at::Tensor decode_up_swiglu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+at::Tensor decode_up_swiglu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                            const c10::optional<at::Tensor>& w_scale) {
   check_decode_operands(x, w, bias, "decode_up_swiglu");
   const int M = x.size(0), N = w.size(0), F = N / 2;
   const c10::DeviceGuard guard(x.device());
   at::Tensor ws;
-  const int KS = decode_partials(x, w, ws);
+  const int KS = decode_partials(x, w, ws, w_scale);
   auto act = at::empty({M, F}, x.options());
   const long n4 = (long)M * F / 4;
   hipLaunchKernelGGL(decode_fin_swiglu_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream(),
@@ -670,7 +771,7 @@ at::Tensor decode_up_swiglu(const at::Tensor& x, const at::Tensor& w, const c10:
 std::tuple<at::Tensor, at::Tensor> decode_linear_add_rmsnorm(const at::Tensor& x, const at::Tensor& w,
                                                              const c10::optional<at::Tensor>& bias,
                                                              const at::Tensor& res, const at::Tensor& norm_w,
-                                                             double eps) {
+                                                             double eps, const c10::optional<at::Tensor>& w_scale) {
   check_decode_operands(x, w, bias, "decode_linear_add_rmsnorm");
   const int M = x.size(0), N = w.size(0);
   LLMCTL_CHECK(res.is_contiguous() && res.scalar_type() == at::kBFloat16 && res.dim() == 2 && res.size(0) == M &&
@@ -681,7 +782,7 @@ std::tuple<at::Tensor, at::Tensor> decode_linear_add_rmsnorm(const at::Tensor& x
   LLMCTL_CHECK(N <= 16384, "decode_linear_add_rmsnorm: N <= 16384 (row staged in LDS)");
   const c10::DeviceGuard guard(x.device());
   at::Tensor ws;
-  const int KS = decode_partials(x, w, ws);
+  const int KS = decode_partials(x, w, ws, w_scale);
   auto y = at::empty({M, N}, x.options());
   auto res_out = at::empty({M, N}, x.options());
   hipLaunchKernelGGL(decode_fin_add_rmsnorm_kernel, dim3(M), dim3(1024), (size_t)N * 4, stream(), ws.data_ptr<float>(),
@@ -689,7 +790,24 @@ std::tuple<at::Tensor, at::Tensor> decode_linear_add_rmsnorm(const at::Tensor& x
   return {y, res_out};
 }
 
+// y [M, N] = x W^T (+ b) with fp8 (e4m3fn) W and fp32 row scales: partials + decode_finalize_kernel
+at::Tensor decode_linear_fp8(const at::Tensor& x, const at::Tensor& w, const at::Tensor& w_scale,
+                             const c10::optional<at::Tensor>& bias) {
+  check_decode_operands(x, w, bias, "decode_linear_fp8");
+  LLMCTL_CHECK(w_fp8(w), "decode_linear_fp8: fp8 (e4m3fn) weights");
+  const int M = x.size(0), N = w.size(0);
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor ws;
+  const int KS = decode_partials(x, w, ws, w_scale);
+  auto y = at::empty({M, N}, x.options());
+  const long n4 = (long)M * N / 4;
+  hipLaunchKernelGGL(decode_finalize_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream(),
+                     ws.data_ptr<float>(), bias_ptr(bias), bf_mut(y), M, N, KS);
+  return y;
+}
+
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("decode_linear_fp8", &decode_linear_fp8);
   m.impl("skinny_linear", &skinny_linear);
   m.impl("skinny_linear_cfg", &skinny_linear_cfg);
   m.impl("decode_qkv_rope_cache", &decode_qkv_rope_cache);

@@ -447,33 +447,51 @@ def decode_linear(x, w, b=None):
     return forward_linear(x, w, b)
 
 
+def _dequant(w, w_scale, dtype):
+    """bf16 image of an fp8 (e4m3fn) weight with fp32 row scales (fallback paths)."""
+    return w if w_scale is None else (w.float() * w_scale.float().unsqueeze(1)).to(dtype)
+
+
+def decode_linear_fp8(x, w, w_scale, b=None):
+    """``x @ (w * w_scale[:, None])^T (+ b)`` for decode-shaped inputs with fp8 (OCP e4m3fn)
+    weights and fp32 row scales (W8A16: ``csrc/skinny_gemm.hip``'s fp8 weight stream, half the
+    bytes of the bf16 one)."""
+    if decode_fused_ok(x, w):
+        return native().decode_linear_fp8(x, w, w_scale, b)
+    return decode_linear(x, _dequant(w, w_scale, x.dtype), b)
+
+
 def decode_fused_ok(x, w) -> bool:
     """Can this decode projection run with a fused epilogue (``csrc/skinny_gemm.hip``: the v2
     weight-streaming GEMM's K-chunk partials summed by a finalize pass that also applies RoPE +
     paged-cache write, SwiGLU or residual + RMSNorm)?  <= 16 tokens, bf16, out features a
     multiple of 64, in features of 128.  Knob ``decode_fused`` off disables (A/B)."""
     return (knobs().decode_fused and use_native(x) and x.dim() == 2
-            and 1 <= x.shape[0] <= 16 and x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous()
+            and 1 <= x.shape[0] <= 16 and x.dtype == torch.bfloat16
+            and w.dtype in (torch.bfloat16, torch.float8_e4m3fn) and x.is_contiguous()
             and w.is_contiguous() and w.shape[0] % 64 == 0 and x.shape[1] % 128 == 0)
 
 
-def decode_qkv_rope_cache(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cache, v_cache, slots):
+def decode_qkv_rope_cache(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cache, v_cache, slots,
+                          w_scale=None):
     """Decode QKV projection + RoPE + paged-cache write of K/V in one finalize pass; returns
-    ``q [T, nq, D]``.  Same result as ``rope_qkv_cache(decode_linear(x, w, b), ...)[0]``."""
+    ``q [T, nq, D]``.  Same result as ``rope_qkv_cache(decode_linear(x, w, b), ...)[0]``.
+    ``w_scale``: fp32 row scales of an fp8 (e4m3fn) ``w``."""
     if decode_fused_ok(x, w):
         return native().decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, positions.to(torch.int32).contiguous(),
-                                              k_cache, v_cache, slots)
-    return rope_qkv_cache(decode_linear(x, w, b), cos, sin, nq, nkv, 0, positions, k_cache, v_cache, slots)[0]
+                                              k_cache, v_cache, slots, w_scale)
+    return rope_qkv_cache(decode_linear(x, _dequant(w, w_scale, x.dtype), b), cos, sin, nq, nkv, 0, positions,
+                          k_cache, v_cache, slots)[0]
 
 
 def decode_attention_qkv(x, w, b, cos, sin, nq: int, nkv: int, positions, k_cache, v_cache, slots, block_tables,
-                         ctx_lens, scale: Optional[float] = None):
+                         ctx_lens, scale: Optional[float] = None, w_scale=None):
     """Decode QKV projection -> RoPE -> paged-cache write (one finalize pass) -> paged attention.
     (Round 2's variant that summed the projection partials inside the attention kernel measured
     0.1-0.2 ms slower per 16 x 2k GPT-7B step, profiles/serve_r2_session6.txt, and was retired.)"""
     D = w.shape[0] // (nq + 2 * nkv)
     scale = scale if scale is not None else D ** -0.5
-    q = decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, positions, k_cache, v_cache, slots)
+    q = decode_qkv_rope_cache(x, w, b, cos, sin, nq, nkv, positions, k_cache, v_cache, slots, w_scale)
     return paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
 
 
@@ -498,20 +516,20 @@ def up_swiglu(x, w, b=None):
     return swiglu(forward_linear(x, w, b))
 
 
-def decode_up_swiglu(x, w, b=None):
+def decode_up_swiglu(x, w, b=None, w_scale=None):
     """Decode gate/up projection with SwiGLU in its finalize pass: ``silu(g) * u`` of
     ``x @ w^T (+ b)`` (gate = first half of the out features)."""
     if decode_fused_ok(x, w):
-        return native().decode_up_swiglu(x, w, b)
-    return swiglu(decode_linear(x, w, b))
+        return native().decode_up_swiglu(x, w, b, w_scale)
+    return swiglu(decode_linear(x, _dequant(w, w_scale, x.dtype), b))
 
 
-def decode_linear_add_rmsnorm(x, w, b, residual, norm_w, eps: float):
+def decode_linear_add_rmsnorm(x, w, b, residual, norm_w, eps: float, w_scale=None):
     """Decode row projection + residual add + RMSNorm in one finalize pass:
     ``(rmsnorm(y + residual) * norm_w, y + residual)`` with ``y = x @ w^T (+ b)``."""
     if decode_fused_ok(x, w) and w.shape[0] <= 16384:
-        return native().decode_linear_add_rmsnorm(x, w, b, residual, norm_w, eps)
-    y = decode_linear(x, w, b)
+        return native().decode_linear_add_rmsnorm(x, w, b, residual, norm_w, eps, w_scale)
+    y = decode_linear(x, _dequant(w, w_scale, x.dtype), b)
     return add_rmsnorm(y, residual, norm_w, eps)
 
 
@@ -526,6 +544,6 @@ __all__ = [
     "rmsnorm", "add_rmsnorm", "layernorm", "add_layernorm", "rope_qkv", "flash_attention", "rope_flash_attention",
     "swiglu",
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
-    "sample", "decode_linear", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu", "decode_attention_qkv", "up_swiglu",
+    "sample", "decode_linear", "decode_linear_fp8", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu", "decode_attention_qkv", "up_swiglu",
     "decode_linear_add_rmsnorm", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
 ]

@@ -52,7 +52,7 @@ class InferenceEngine:
                  block_size: int = 16, num_kv_blocks: Optional[int] = None, scheduler: str = "dynamic",
                  use_graphs: bool = True, seed: int = 0, pc=None, prefix_caching: bool = True,
                  tuning_cache: Optional[str] = None, perf_knobs: Optional[Dict] = None,
-                 kv_cache_dtype: str = "auto"):
+                 kv_cache_dtype: str = "auto", weight_dtype: str = "auto"):
         from llmctl.config import knobs as perf
 
         self.knobs = perf.configure(perf_knobs)  # defaults + perf_knobs + LLMCTL_KNOBS
@@ -84,6 +84,16 @@ class InferenceEngine:
         self.max_model_len = max_model_len or cfg.max_position_embeddings
         self.block_size = block_size
         self.max_blocks_per_seq = (self.max_model_len + block_size - 1) // block_size
+        # decode projection weights: the model's ("auto"), or an fp8 (OCP e4m3fn) copy with fp32 row
+        # scales ("fp8", W8A16) that the fused decode path streams instead (half the bytes of the
+        # HBM-bound decode GEMMs); prefill keeps the bf16 weights.  Made before the KV cache is sized.
+        self._w8: Optional[List[Dict[str, Tuple[torch.Tensor, torch.Tensor]]]] = None
+        if weight_dtype in ("fp8", "fp8_e4m3", "float8_e4m3fn"):
+            if self.device.type == "cuda":
+                self._w8 = self._quantize_decode_weights()
+        elif weight_dtype not in ("auto", "model", "bf16", "bfloat16"):
+            raise ValueError(f"weight_dtype must be auto / bf16 / fp8, got {weight_dtype!r}")
+        self.weight_dtype = "fp8" if self._w8 is not None else "auto"
         # KV cache element: the model dtype ("auto"), or OCP fp8 e4m3fn ("fp8": half the bytes per
         # token, so twice the blocks and half the decode attention's HBM stream; saturating at +-448)
         if kv_cache_dtype in ("auto", "model", "bf16", "bfloat16"):
@@ -377,6 +387,32 @@ class InferenceEngine:
             x = self._mlp(layer, xn)
         return self._final(x, res)
 
+    _W8_NAMES = ("wqkv", "wo", "w_up", "w_down")
+
+    @torch.no_grad()
+    def _quantize_decode_weights(self) -> List[Dict[str, Tuple[torch.Tensor, torch.Tensor]]]:
+        """Per layer: fp8 (e4m3fn) copies of the decode projection weights + fp32 row scales
+        (``llmctl.plugins.quantizers.quantize_fp8``: absmax / 448 per output row)."""
+        from llmctl.plugins.quantizers import quantize_fp8
+
+        out = []
+        for layer in self.model.layers:
+            d = {}
+            for name in self._W8_NAMES:
+                w = getattr(layer, name, None)
+                if w is None or w.dim() != 2 or w.shape[0] % 64:
+                    continue
+                qd = quantize_fp8(w.detach())
+                d[name] = (qd["qweight"].contiguous(), qd["scale"].float().contiguous())
+            out.append(d)
+        return out
+
+    def _dw(self, li: int, layer, name: str):
+        """(weight, row scales or None) the fused decode path streams for ``layer.name``."""
+        if self._w8 is not None and name in self._w8[li]:
+            return self._w8[li][name]
+        return getattr(layer, name), None
+
     def _decode_body_fused(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
         m = self.model
         eps = self.cfg.layer_norm_eps
@@ -385,21 +421,27 @@ class InferenceEngine:
         x = self._embed(ids, positions)
         xn, res = ops.rmsnorm(x, layers[0].attn_norm_w, eps), x
         tp = self.tp > 1
+        def lin(x, w, s):  # a plain decode projection (TP row-parallel partial): bf16 or fp8 weights
+            return ops.decode_linear(x, w) if s is None else ops.decode_linear_fp8(x, w, s)
+
         for li, layer in enumerate(layers):
-            o = ops.decode_attention_qkv(xn, layer.wqkv, layer.bqkv, self.rope[0], self.rope[1], layer.nq,
-                                         layer.nkv, positions, kc[li], vc[li], slots, block_tables, ctx_lens)
+            (wqkv, sqkv), (wo, so) = self._dw(li, layer, "wqkv"), self._dw(li, layer, "wo")
+            (wu, su), (wd, sd) = self._dw(li, layer, "w_up"), self._dw(li, layer, "w_down")
+            o = ops.decode_attention_qkv(xn, wqkv, layer.bqkv, self.rope[0], self.rope[1], layer.nq,
+                                         layer.nkv, positions, kc[li], vc[li], slots, block_tables, ctx_lens,
+                                         w_scale=sqkv)
             if tp:  # row-parallel o-proj partial -> one kernel: all-reduce + bias + residual + RMSNorm
-                xn, res = self._reduce_add_rmsnorm(ops.decode_linear(o.view(o.shape[0], -1), layer.wo), layer.bo,
+                xn, res = self._reduce_add_rmsnorm(lin(o.view(o.shape[0], -1), wo, so), layer.bo,
                                                    res, layer.mlp_norm_w, eps)
             else:
-                xn, res = ops.decode_linear_add_rmsnorm(o.view(o.shape[0], -1), layer.wo, layer.bo, res,
-                                                        layer.mlp_norm_w, eps)
-            act = ops.decode_up_swiglu(xn, layer.w_up, layer.b_up)  # the local F shard
+                xn, res = ops.decode_linear_add_rmsnorm(o.view(o.shape[0], -1), wo, layer.bo, res,
+                                                        layer.mlp_norm_w, eps, w_scale=so)
+            act = ops.decode_up_swiglu(xn, wu, layer.b_up, w_scale=su)  # the local F shard
             nw = layers[li + 1].attn_norm_w if li + 1 < len(layers) else m.final_norm_w
             if tp:
-                xn, res = self._reduce_add_rmsnorm(ops.decode_linear(act, layer.w_down), layer.b_down, res, nw, eps)
+                xn, res = self._reduce_add_rmsnorm(lin(act, wd, sd), layer.b_down, res, nw, eps)
             else:
-                xn, res = ops.decode_linear_add_rmsnorm(act, layer.w_down, layer.b_down, res, nw, eps)
+                xn, res = ops.decode_linear_add_rmsnorm(act, wd, layer.b_down, res, nw, eps, w_scale=sd)
         return self._gather_vocab(ops.decode_linear(xn, m.head_weight()))
 
     def _bucket(self, n: int) -> int:

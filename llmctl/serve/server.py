@@ -53,7 +53,7 @@ class InferenceServer:
     def __init__(self, model_path: str, host: str = "0.0.0.0", port: int = 8080, max_batch_size: int = 8,
                  max_batch_tokens: int = 8192, max_concurrent: int = 128, scheduler: str = "dynamic",
                  device: str = "auto", kv_cache_fraction: float = 0.85, block_size: int = 16, use_graphs: bool = True,
-                 tensor_parallel: int = 1, engine=None, kv_cache_dtype: str = "auto"):
+                 tensor_parallel: int = 1, engine=None, kv_cache_dtype: str = "auto", weight_dtype: str = "auto"):
         from fastapi import FastAPI, HTTPException
         from fastapi.middleware.cors import CORSMiddleware
         from fastapi.responses import PlainTextResponse, StreamingResponse
@@ -63,7 +63,7 @@ class InferenceServer:
         self.engine_kwargs = dict(model_path=model_path, device=device, max_batch_size=max_batch_size,
                                   max_batch_tokens=max_batch_tokens, kv_cache_fraction=kv_cache_fraction,
                                   block_size=block_size, scheduler=scheduler, use_graphs=use_graphs,
-                                  kv_cache_dtype=kv_cache_dtype)
+                                  kv_cache_dtype=kv_cache_dtype, weight_dtype=weight_dtype)
         if tensor_parallel != 1 and engine is None:
             raise ValueError("TP serving runs one engine per rank under torchrun: use llmctl.serve.tp "
                              "(`llmctl serve start --tensor-parallel N` launches it)")

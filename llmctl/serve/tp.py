@@ -250,12 +250,13 @@ def main(argv=None) -> int:
     ap.add_argument("--scheduler", default="dynamic")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv-cache-dtype", default="auto")
+    ap.add_argument("--weight-dtype", default="auto")
     a = ap.parse_args(argv)
     group, dev = init_tp()
     eng = TPInferenceEngine(a.artifact, tp_group=group, device=dev, max_batch_size=a.max_batch_size,
                             max_batch_tokens=a.max_batch_tokens, kv_cache_fraction=a.kv_cache_fraction,
                             block_size=a.block_size, scheduler=a.scheduler, use_graphs=not a.no_graphs,
-                            kv_cache_dtype=a.kv_cache_dtype)
+                            kv_cache_dtype=a.kv_cache_dtype, weight_dtype=a.weight_dtype)
     if eng.tp_rank != 0:
         eng.worker_loop()
         eng.close()

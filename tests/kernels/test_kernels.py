@@ -781,6 +781,61 @@ def test_decode_linear_add_rmsnorm_fused(native_lib, M, N, K, bias):
     assert _row_err(res_out, s) < 1.5e-2 and _row_err(y, ref_y) < 2e-2
 
 
+# ---- fp8 (e4m3fn) decode weights with fp32 row scales (W8A16 decode GEMM)
+def _w8(N, K, seed):
+    from llmctl.plugins.quantizers import quantize_fp8
+
+    qd = quantize_fp8(_bf(N, K, scale=0.05, seed=seed))
+    w8, sc = qd["qweight"].contiguous(), qd["scale"].float().contiguous()
+    return w8, sc, w8.float() * sc.unsqueeze(1)  # fp32 image of the dequantised weight
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(1, 4096, 4096, False), (16, 12288, 4096, True), (7, 4096, 11008, False),
+                                        (16, 1024, 384, True), (3, 256, 1152, False)])
+def test_decode_linear_fp8_weights(native_lib, M, N, K, bias):
+    """fp8-weight decode projection == the fp32 product with the dequantised weight (short last
+    K chunks: K % 1024 != 0; several chunks; one token)."""
+    x = _bf(M, K, seed=101)
+    w8, sc, wd = _w8(N, K, 102)
+    b = _bf(N, seed=103) if bias else None
+    y = native_lib.decode_linear_fp8(x, w8, sc, b)
+    yr = x.float() @ wd.t() + (b.float() if bias else 0.0)
+    assert y.shape == (M, N) and _row_err(y, yr) < 1e-2, _row_err(y, yr)
+
+
+def test_decode_fused_ops_fp8_weights(native_lib):
+    """The fused decode ops (QKV + RoPE + cache write, up + SwiGLU, row projection + residual +
+    RMSNorm) with fp8 weights == the same ops on the bf16 image of the dequantised weights."""
+    M, K = 16, 4096
+    nq, nkv, D, bs, nb = 8, 2, 128, 16, 8
+    x = _bf(M, K, seed=111)
+    # QKV
+    w8, sc, wd = _w8((nq + 2 * nkv) * D, K, 112)
+    cos, sin = ref.rope_tables(256, D, base=10000.0, device=DEV)
+    pos = torch.randint(0, 256, (M,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nb * bs, device=DEV)[:M]
+    kc, vc = torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV), torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    q = native_lib.decode_qkv_rope_cache(x, w8, None, cos, sin, nq, nkv, pos, kc, vc, slots, sc)
+    q2 = native_lib.decode_qkv_rope_cache(x, wd.to(torch.bfloat16), None, cos, sin, nq, nkv, pos, kc2, vc2, slots)
+    assert _row_err(q, q2.float()) < 1e-2 and _row_err(kc, kc2.float()) < 1e-2 and _row_err(vc, vc2.float()) < 1e-2
+    # up + SwiGLU
+    F = 1024
+    w8, sc, wd = _w8(2 * F, K, 113)
+    act = native_lib.decode_up_swiglu(x, w8, None, sc)
+    gu = x.float() @ wd.t()
+    assert _row_err(act, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]) < 2e-2
+    # row projection + residual + RMSNorm
+    N = 4096
+    w8, sc, wd = _w8(N, K, 114)
+    res = _bf(M, N, seed=115)
+    nw = (1.0 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    y, res_out = native_lib.decode_linear_add_rmsnorm(x, w8, None, res, nw, 1e-5, sc)
+    s_ = x.float() @ wd.t() + res.float()
+    assert _row_err(res_out, s_) < 1.5e-2
+    assert _row_err(y, s_ * torch.rsqrt(s_.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()) < 2e-2
+
+
 @pytest.mark.parametrize("M,F,K", [(256, 128, 256), (2048, 11008, 4096), (512, 384, 1152)])
 def test_gemm64_swiglu_fwd(native_lib, M, F, K):
     """Gate/up projection with the SwiGLU in the gemm64 epilogue (gate rows and the matching up

@@ -234,6 +234,27 @@ def test_tp2_serving_fp8_kv_cache(native_lib):
     assert err < 3e-2, err
 
 
+def test_engine_fp8_decode_weights(native_lib):
+    """weight_dtype="fp8": the fused decode path streams fp8 (e4m3fn) copies of the projection
+    weights (fp32 row scales); prefill keeps bf16.  On the bf16 engine's token stream the decode
+    logits stay close to the bf16 weights' (per-row fp8 rounding of every weight), and the
+    TP=2 fp8-weight engine follows the TP=1 one within the same noise."""
+    from llmctl.testing.harness import run_ranks
+    from llmctl.testing.numerics import row_err
+    from llmctl.testing.workers import serve_forced_gpu
+
+    ref = serve_forced_gpu(0, 1, 8, "tiny")
+    w8 = serve_forced_gpu(0, 1, 8, "tiny", ref["tokens"], None, {"weight_dtype": "fp8"})
+    assert w8["fused_decode"] and w8["graph_replays"] > 0
+    err = row_err(_logit_rows(w8), _logit_rows(ref))
+    assert 0 < err < 0.1, err
+    # each TP rank quantises its own shard: the row-parallel (o / down) shards get their own row
+    # scales, so TP=2 differs from TP=1 by the quantisation noise, not by bf16 rounding only
+    tp = run_ranks(serve_forced_gpu, 2, 8, "tiny", w8["tokens"], None, {"weight_dtype": "fp8"}, timeout=300)
+    err_tp = row_err(_logit_rows(tp[0]), _logit_rows(w8))
+    assert err_tp < max(0.1, 2 * err), (err_tp, err)
+
+
 def test_tp8_serving_eight_processes_custom_ar_graphs(native_lib):
     """BASELINE config #5's degree (TP=8), eight processes on one GPU: one query and one KV head
     per rank (tiny-wide), 8-way custom all-reduces.  One hardware queue per rank: the custom

@@ -24,13 +24,14 @@ def main():
     ap.add_argument("--prompt", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--kv-cache-dtype", default="auto")
+    ap.add_argument("--weight-dtype", default="auto", help="decode projection weights: auto (bf16) | fp8")
     a = ap.parse_args()
     import torch
     from llmctl.serve.engine import InferenceEngine
     from llmctl.serve.scheduler import SamplingParams
 
     eng = InferenceEngine(a.model, device="cuda", max_batch_size=a.batch, max_model_len=a.prompt + a.tokens + 64,
-                          kv_cache_dtype=a.kv_cache_dtype)
+                          kv_cache_dtype=a.kv_cache_dtype, weight_dtype=a.weight_dtype)
     p = SamplingParams(max_tokens=a.tokens, temperature=0.0, ignore_eos=True)
     base = eng.knobs
     for rnd in range(3):
@@ -61,7 +62,8 @@ def main():
     ev[1].record()
     torch.cuda.synchronize()
     print(json.dumps({"gpu_ms_per_step": round(ev[0].elapsed_time(ev[1]) / 20, 3), "batch": a.batch,
-                      "context": a.prompt, "kv_cache_dtype": a.kv_cache_dtype}), flush=True)
+                      "context": a.prompt, "kv_cache_dtype": a.kv_cache_dtype,
+                      "weight_dtype": a.weight_dtype}), flush=True)
 
 
 if __name__ == "__main__":
