@@ -46,3 +46,21 @@ def test_decode_qkv_rope_cache_and_attention_cpu():
     kc2, vc2 = kc.clone(), vc.clone()
     o = ops.decode_attention_qkv(x, w, None, cos, sin, nq, nkv, pos, kc2, vc2, slots, bt, ctx)
     torch.testing.assert_close(o, ref.paged_attention_decode(qr, kc, vc, bt, ctx, D ** -0.5))
+
+
+def test_fp8_decode_weights_cpu_fallbacks():
+    """fp8 (e4m3fn) weights + fp32 row scales: the CPU paths use the dequantised weight."""
+    from llmctl.plugins.quantizers import quantize_fp8
+
+    x = _x(3, 64, seed=21)
+    qd = quantize_fp8(_x(96, 64, seed=22) * 0.1)
+    w8, sc = qd["qweight"], qd["scale"].float()
+    wd = w8.float() * sc.unsqueeze(1)
+    assert not ops.decode_fused_ok(x, w8)
+    torch.testing.assert_close(ops.decode_linear_fp8(x, w8, sc), x @ wd.t())
+    torch.testing.assert_close(ops.decode_up_swiglu(x, w8, None, w_scale=sc), ops.swiglu(x @ wd.t()))
+    res, nw = _x(3, 96, seed=23), 1 + 0.1 * _x(96, seed=24)
+    y, r = ops.decode_linear_add_rmsnorm(x, w8, None, res, nw, 1e-5, w_scale=sc)
+    torch.testing.assert_close(r, x @ wd.t() + res)
+    # the fp8 image is within e4m3 rounding of the original
+    assert ((wd - _x(96, 64, seed=22) * 0.1).abs() <= 0.07 * (_x(96, 64, seed=22) * 0.1).abs() + 1e-6).all()
