@@ -88,6 +88,7 @@ class InferenceEngine:
         # scales ("fp8", W8A16) that the fused decode path streams instead (half the bytes of the
         # HBM-bound decode GEMMs); prefill keeps the bf16 weights.  Made before the KV cache is sized.
         self._w8: Optional[List[Dict[str, Tuple[torch.Tensor, torch.Tensor]]]] = None
+        self._w8_head: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
         if weight_dtype in ("fp8", "fp8_e4m3", "float8_e4m3fn"):
             if self.device.type == "cuda":
                 self._w8 = self._quantize_decode_weights()
@@ -405,6 +406,10 @@ class InferenceEngine:
                 qd = quantize_fp8(w.detach())
                 d[name] = (qd["qweight"].contiguous(), qd["scale"].float().contiguous())
             out.append(d)
+        hw = self.model.head_weight()
+        if hw.dim() == 2 and hw.shape[0] % 64 == 0:  # the (local shard of the) vocabulary projection
+            qd = quantize_fp8(hw.detach())
+            self._w8_head = (qd["qweight"].contiguous(), qd["scale"].float().contiguous())
         return out
 
     def _dw(self, li: int, layer, name: str):
@@ -442,6 +447,8 @@ class InferenceEngine:
                 xn, res = self._reduce_add_rmsnorm(lin(act, wd, sd), layer.b_down, res, nw, eps)
             else:
                 xn, res = ops.decode_linear_add_rmsnorm(act, wd, layer.b_down, res, nw, eps, w_scale=sd)
+        if self._w8_head is not None:
+            return self._gather_vocab(ops.decode_linear_fp8(xn, *self._w8_head))
         return self._gather_vocab(ops.decode_linear(xn, m.head_weight()))
 
     def _bucket(self, n: int) -> int:
