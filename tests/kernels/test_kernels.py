@@ -812,13 +812,17 @@ def test_decode_fused_ops_fp8_weights(native_lib):
     # QKV
     w8, sc, wd = _w8((nq + 2 * nkv) * D, K, 112)
     cos, sin = ref.rope_tables(256, D, base=10000.0, device=DEV)
-    pos = torch.randint(0, 256, (M,), device=DEV, dtype=torch.int32)
-    slots = torch.randperm(nb * bs, device=DEV)[:M]
+    gen = torch.Generator().manual_seed(116)
+    pos = torch.randint(0, 256, (M,), generator=gen, dtype=torch.int32).to(DEV)
+    slots = torch.randperm(nb * bs, generator=gen)[:M].to(DEV)
     kc, vc = torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV), torch.zeros(nb, bs, nkv, D, dtype=torch.bfloat16, device=DEV)
     kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
     q = native_lib.decode_qkv_rope_cache(x, w8, None, cos, sin, nq, nkv, pos, kc, vc, slots, sc)
+    # reference: the bf16 image of the dequantised weight (one more bf16 rounding per weight than
+    # the kernel's exact e4m3 x fp32 scale), same kernels otherwise
     q2 = native_lib.decode_qkv_rope_cache(x, wd.to(torch.bfloat16), None, cos, sin, nq, nkv, pos, kc2, vc2, slots)
-    assert _row_err(q, q2.float()) < 1e-2 and _row_err(kc, kc2.float()) < 1e-2 and _row_err(vc, vc2.float()) < 1e-2
+    errs = (_row_err(q, q2.float()), _row_err(kc, kc2.float()), _row_err(vc, vc2.float()))
+    assert max(errs) < 2e-2, errs
     # up + SwiGLU
     F = 1024
     w8, sc, wd = _w8(2 * F, K, 113)
