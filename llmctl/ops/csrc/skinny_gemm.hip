@@ -299,32 +299,27 @@ __device__ __forceinline__ bf16x8_t fp8x8_to_bf16x8(unsigned lo, unsigned hi) {
   return r;
 }
 
-template <int NB, int RT = 1>
+template <int NB>
 __global__ __launch_bounds__(256) void decode_gemm_w8_kernel(const unsigned short* __restrict__ x,
                                                              const unsigned char* __restrict__ w,
                                                              const float* __restrict__ wscale,
                                                              float* __restrict__ ws, int M, int N, int K) {
-  // RT 16-row tiles per wave (a workgroup covers 64 RT weight rows): the token rows staged in LDS
-  // serve RT times the weight bytes
   extern __shared__ __attribute__((aligned(16))) unsigned char xs_raw[];
   unsigned short* xs = reinterpret_cast<unsigned short*>(xs_raw);
   constexpr int KC = NB * KBLK, XST = KC + 8;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 64 * RT + wave * 16 * RT;
+  const int n0 = blockIdx.x * 64 + wave * 16;
   const int kc0 = blockIdx.y * KC;
   const int kc = min(KC, K - kc0);
   const int nb = kc / KBLK;
-  uint4 a[RT][NB][2];
+  const unsigned char* wrow = w + (long)(n0 + r) * K + kc0 + 16 * g;
+  uint4 a[NB][2];
 #pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const unsigned char* wrow = w + (long)(n0 + 16 * t + r) * K + kc0 + 16 * g;
+  for (int u = 0; u < NB; ++u) {
+    const int bu = u < nb ? u : nb - 1;
 #pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int bu = u < nb ? u : nb - 1;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) a[t][u][h] = *reinterpret_cast<const uint4*>(wrow + bu * KBLK + 64 * h);
-    }
+    for (int h = 0; h < 2; ++h) a[u][h] = *reinterpret_cast<const uint4*>(wrow + bu * KBLK + 64 * h);
   }
   __builtin_amdgcn_sched_barrier(0);
   const int c8 = kc >> 3;
@@ -336,37 +331,26 @@ __global__ __launch_bounds__(256) void decode_gemm_w8_kernel(const unsigned shor
   }
   __syncthreads();
   const unsigned short* xrow = xs + r * XST + 16 * g;
-  f32x4_t acc[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     if (u < nb) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const bf16x8_t x0 = *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 64 * h);
-        const bf16x8_t x1 = *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 64 * h + 8);
-#pragma unroll
-        for (int t = 0; t < RT; ++t) {
-          const uint4 q = a[t][u][h];
-          acc[t] = mfma16(fp8x8_to_bf16x8(q.x, q.y), x0, acc[t]);
-          acc[t] = mfma16(fp8x8_to_bf16x8(q.z, q.w), x1, acc[t]);
-        }
+        const uint4 q = a[u][h];
+        acc = mfma16(fp8x8_to_bf16x8(q.x, q.y), *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 64 * h), acc);
+        acc = mfma16(fp8x8_to_bf16x8(q.z, q.w), *reinterpret_cast<const bf16x8_t*>(xrow + u * KBLK + 64 * h + 8), acc);
       }
     }
   }
   if (r >= M) return;
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int n = n0 + 16 * t + 4 * g;
-    const float4 sc = *reinterpret_cast<const float4*>(wscale + n);
-    f32x4_t o = acc[t];
-    o[0] *= sc.x;
-    o[1] *= sc.y;
-    o[2] *= sc.z;
-    o[3] *= sc.w;
-    *reinterpret_cast<f32x4_t*>(ws + ((long)blockIdx.y * M + r) * N + n) = o;
-  }
+  const int n = n0 + 4 * g;
+  const float4 sc = *reinterpret_cast<const float4*>(wscale + n);
+  acc[0] *= sc.x;
+  acc[1] *= sc.y;
+  acc[2] *= sc.z;
+  acc[3] *= sc.w;
+  *reinterpret_cast<f32x4_t*>(ws + ((long)blockIdx.y * M + r) * N + n) = acc;
 }
 
 // y[m][n] = bf16(sum_s ws[s][m][n] + bias[n]), 4 columns per thread
