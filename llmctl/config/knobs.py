@@ -54,9 +54,6 @@ class PerfKnobs:
     fa_split: int = -1             # forward causal K/V split: -1 auto, 0 off, 1 on
     fa_prio: int = 1               # s_setprio around the forward MFMA clusters
     fa_nw: int = 4                 # forward waves per workgroup: 4 or 8
-    fa_w64: int = 0                # forward HD 128: 0 the 2-waves-per-SIMD kernel; 3 the asm-scheduled
-                                   # one-wave-per-SIMD 64-row kernel (faster on gaussian inputs, 4 % slower
-                                   # on the model's: profiles/attn_fwd_w64_r5.txt), 1 / 2 its C++ forms
     dkv: int = 2                   # dK/dV kernel: 0 plain, 1 pipelined, 2 persistent
     dkv_nwg: int = 0               # persistent dK/dV workgroups (0: one per CU; debug)
     # ---- parallelism
@@ -81,7 +78,7 @@ class PerfKnobs:
         return dataclasses.asdict(self)
 
 
-NATIVE = ("fa_split", "fa_prio", "fa_nw", "fa_w64", "dkv", "dkv_nwg", "decode_splits", "decode_v3")
+NATIVE = ("fa_split", "fa_prio", "fa_nw", "dkv", "dkv_nwg", "decode_splits", "decode_v3")
 _FIELDS = {f.name: f for f in fields(PerfKnobs)}
 
 

@@ -44,6 +44,9 @@ def compile_flags(arch: str, save_temps: bool = False):
     flags += [f"-I{i}" for i in incs]
     if save_temps:
         flags += ["-save-temps=obj"]
+    # diagnostic builds only (e.g. LLMCTL_BUILD_DEFINES="LLMCTL_STAMP LLMCTL_STAMP_EXP=2" for the
+    # persistent GEMM's cycle stamps, tools/gemm_stamps.py); the production library sets none
+    flags += [f"-D{d}" for d in os.environ.get("LLMCTL_BUILD_DEFINES", "").split() if d]
     return flags
 
 

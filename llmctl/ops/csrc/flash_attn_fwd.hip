@@ -33,10 +33,8 @@
 //     combine kernel — halves the critical path of the causal tail.
 // Outputs O [B,S,Hq,HD] bf16 and LSE [B,Hq,S] fp32 (natural log) for the backward pass.
 #include <cstdlib>
-#include <utility>
 
 #include "attn_common.h"
-#include "fa_w64_asm.inc"
 
 namespace llmctl {
 using namespace attn;
@@ -62,7 +60,6 @@ struct FwdArgs {
   unsigned short* o_part;  // SPLIT: [2, B, S, Hq, HD] bf16 normalised partial outputs
   float* lse_part;   // SPLIT: [2, B, Hq, S] natural-log partial LSEs
   int prio;          // raise the wave priority over its MFMA phases (A/B knob fa_prio)
-  unsigned* stamp;   // fa_fwd_w64a_kernel diagnostic build: [workgroup][wave][16] cycle totals
 };
 
 template <int HD, bool CAUSAL, bool DOC = false, bool SPLIT = false, int NW = 4, int NBUF = 2>
@@ -350,404 +347,6 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd_kernel(FwdArgs a) {
   }
 }
 
-// Scheduling template of one 32-MFMA phase of fa_fwd_w64_kernel (T19 sched_group_barrier): the
-// fragment reads run two MFMAs ahead (1 ds_read_b128 per QK^T MFMA, 2 ds_read_b64_tr_b16 per PV
-// MFMA) and every MFMA gap carries up to 5 VALU of the other block's softmax.
-template <int I>
-__device__ __forceinline__ void w64_slot() {
-  __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);  // MFMA I
-  constexpr int nr = I < 14 ? 1 : I < 30 ? 2 : 0;    // the reads of MFMA I + 2
-  if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
-  __builtin_amdgcn_sched_group_barrier(0x2, 5, 0);
-}
-template <int... I>
-__device__ __forceinline__ void w64_phase(std::integer_sequence<int, I...>) {
-  __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-  (w64_slot<I>(), ...);
-}
-
-// ---- one wave per SIMD, 64 query rows per wave (HD = 128; no documents, no K/V split) ---------
-// The MI355X guide's one-wave-per-SIMD attention structure (App. B; MI355X_MICROARCH: a
-// compiler-scheduled 4-wave x 64-row stream runs ~36 cycles per 32x32x16 MFMA): workgroup =
-// 4 waves x 64 rows, one per CU, each wave holding two 32-row query blocks A | B and the whole
-// 512-register file.  The blocks are software-pipelined half a tile apart, so every 32-MFMA phase
-// carries exactly one block's softmax in its gaps (~5 VALU per MFMA gap, one of them an exp):
-//   phase 2t   : S_A(t) = K_t Q_A^T  ;  O_A += V_{t-1}^T P_A(t-1)  |  softmax B(t-1)
-//   phase 2t+1 : S_B(t) = K_t Q_B^T  ;  O_B += V_{t-1}^T P_B(t-1)  |  softmax A(t)
-// (the 2-waves-per-SIMD kernel above relies on the partner wave to fill the MFMA gaps and left
-// the matrix pipe ~70 % idle, profiles/attn_*).  K/V tiles arrive by LDS-DMA into a 4-slot ring,
-// issued two tiles ahead; one barrier per tile.  Only a wave's last tile (its causal diagonal /
-// the sequence end) is masked: block A's softmax of it in the last loop phase, B's in the tail.
-template <bool CAUSAL, bool SGB>
-__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_fwd_w64_kernel(FwdArgs a) {
-  constexpr int HD = 128, NW = 4, QB = 256, NBUF = 4;
-  constexpr int NKS = HD / 16, NDB = HD / 32, ROWB = HD * 2, TILE = KB * ROWB;
-  constexpr int PPW = TILE / 1024 / NW, SLOT = 2 * TILE;
-  static_assert(PPW * NW * 1024 == TILE, "pieces must split evenly over the waves");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * SLOT];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, hh = lane >> 5;
-  const int nqb = (a.S + QB - 1) / QB;
-  const int BH = a.B * a.Hq;
-  int bh, rest;
-  if (BH % 8) {
-    bh = blockIdx.x % BH;
-    rest = blockIdx.x / BH;
-  } else {  // XCD-aware order, as fa_fwd_kernel
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-    bh = x * (BH >> 3) + j / nqb;
-    rest = j % nqb;
-  }
-  const int qblk = nqb - 1 - rest;  // heaviest first
-  const int b = bh / a.Hq, hq = bh % a.Hq;
-  const int hk = hq / (a.Hq / a.Hkv);
-  const int q_row0 = qblk * QB + wave * 64;  // wave-uniform; block A rows +0..31, B +32..63
-  const int myA = q_row0 + r, myB = q_row0 + 32 + r;
-
-  const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh;
-  const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh;
-  const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh;
-
-#pragma unroll
-  for (int i = 0; i < NBUF * SLOT / (256 * 16); ++i)
-    *reinterpret_cast<uint4*>(smem + i * 256 * 16 + tid * 16) = make_uint4(0, 0, 0, 0);
-
-  bf16x8_t qa[NKS], qb[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    uint4 u = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
-    if (myA < a.S) u = gload16(Qp + (long)myA * a.q_ss + ks * 16 + 8 * hh);
-    if (myB < a.S) w = gload16(Qp + (long)myB * a.q_ss + ks * 16 + 8 * hh);
-    qa[ks] = __builtin_bit_cast(bf16x8_t, u);
-    qb[ks] = __builtin_bit_cast(bf16x8_t, w);
-  }
-  f32x16 oa[NDB], ob[NDB], sa[2], sb[2];
-#pragma unroll
-  for (int d = 0; d < NDB; ++d)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) oa[d][i] = ob[d][i] = 0.f;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sb[kb][i] = -INFINITY;  // "S_B(-1)": the first phase's softmax B is a no-op
-  bf16x8_t pa[2][2], pb[2][2];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pa[kb][st][j] = pb[kb][st][j] = (__bf16)0.f;  // "P_A(-1)" = 0
-  float ma = -INFINITY, la = 0.f, mb = -INFINITY, lb = 0.f;
-  float alpha_a = 1.f, alpha_b = 1.f;
-  bool grow_a = false, grow_b = false;
-
-  const int kv_end = CAUSAL ? min(a.S, qblk * QB + QB) : a.S;
-  const int ntiles = (kv_end + KB - 1) / KB;
-  // the wave's last live tile (causal: its diagonal tile q_row0 / KB; -1: no row < S)
-  const int tw = q_row0 >= a.S ? -1 : CAUSAL ? q_row0 / KB : ntiles - 1;
-
-  unsigned vk[PPW], vv[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int byte = (i * NW + wave) * 1024 + lane * 16;
-    const int row = byte / ROWB, pch = (byte % ROWB) >> 4;
-    vk[i] = (unsigned)((row * a.k_ss + ((pch ^ swz_row<HD>(row)) << 3)) * 2);
-    vv[i] = (unsigned)((row * a.v_ss + ((pch ^ swz_tr<HD>(row)) << 3)) * 2);
-  }
-  const unsigned lds0 = lds_addr(smem);
-  int ik0 = 0;
-  const unsigned short* kc = Kp;
-  const unsigned short* vc = Vp;
-  const long k_step = (long)KB * a.k_ss, v_step = (long)KB * a.v_ss;
-  // tile j goes to ring slot j % NBUF (runtime: one copy of the loop body; the slot's LDS offset
-  // is added once per tile to the lanes' fragment offsets)
-  auto issue = [&](int slot_i) __attribute__((always_inline)) {
-    const int nk = min(KB, a.S - ik0);
-    i32x4_t rk = buf_rsrc(kc, (unsigned)(((nk - 1) * a.k_ss + HD) * 2));
-    i32x4_t rv = buf_rsrc(vc, (unsigned)(((nk - 1) * a.v_ss + HD) * 2));
-    asm volatile("s_nop 4" : "+s"(rk), "+s"(rv));
-    const unsigned slot = lds0 + (unsigned)(slot_i * SLOT) + wave * 1024;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      buf_dma16(rk, vk[i], slot + i * NW * 1024);
-      buf_dma16(rv, vv[i], slot + TILE + i * NW * 1024);
-    }
-    ik0 += KB;
-    kc += k_step;
-    vc += v_step;
-  };
-
-  const float c = a.scale_log2;
-  int vlo[NDB], vhi[NDB];
-#pragma unroll
-  for (int d = 0; d < NDB; ++d) tr_frag_offs<HD>(d * 32, lane, vlo[d], vhi[d]);
-  int kofs[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) kofs[ks] = row_off<HD>(r, 2 * ks + hh);
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qa[ks]), "v"(qb[ks]));
-
-  // fragment byte addresses of the current tile (K_t, V_{t-1}): lane offset + slot offset
-  int ka[NKS], va[NDB][2];
-  auto qk = [&](const bf16x8_t* qf, f32x16* s) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) s[kb] = mfma32(lds_read_b128(smem, kb * 32 * ROWB + ka[ks]), qf[ks], s[kb]);
-    }
-  };
-  auto pv = [&](bf16x8_t (*p)[2], f32x16* o) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int d = 0; d < NDB; ++d) o[d] = mfma32(tr_frag_at<HD>(smem, kb * 32 + 16 * st, va[d][0], va[d][1]), p[kb][st], o[d]);
-  };
-  // online softmax of one block's S^T tile -> P^T (bf16), the new running max / sum and the
-  // rescale factor of its O (applied right before the block's next PV); key_hi < 0: unmasked
-  auto softmax = [&](f32x16* s, int kv0, int key_hi, float& m_i, float& l_i, bf16x8_t (*p)[2], float& alpha,
-                     bool& grow) __attribute__((always_inline)) {
-    if (key_hi >= 0) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[kb][i] = kv0 + kb * 32 + acc_row(i, hh) <= key_hi ? s[kb][i] : -INFINITY;
-    }
-    float mx = s[0][0];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = (kb == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[kb][i]);
-    mx = xor32_max(mx) * c;
-    grow = __builtin_amdgcn_ballot_w64(mx > m_i + kRescaleTh) != 0;
-    const float m_new = grow ? fmaxf(m_i, mx) : m_i;
-    const float nm = (m_new == -INFINITY) ? 0.f : -m_new;
-    float rs = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      float pf[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        pf[i] = fast_exp2(__builtin_fmaf(s[kb][i], c, nm));
-        rs += pf[i];
-      }
-      p[kb][0] = to_bf16x8(pf);
-      p[kb][1] = to_bf16x8(pf + 8);
-    }
-    rs = xor32_add(rs);
-    // alpha = 2^(m_old - m_new) is exactly 1 when the max did not move; computed unconditionally
-    // (not as grow ? .. : 1, which lets the compiler fold the rescale branch into 64
-    // unconditional multiplies per tile)
-    alpha = fast_exp2(m_i + nm);
-    l_i = l_i * alpha + rs;
-    m_i = m_new;
-  };
-  auto rescale = [&](f32x16* o, bool grow, float alpha) __attribute__((always_inline)) {
-    if (grow) {
-#pragma unroll
-      for (int d = 0; d < NDB; ++d)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
-    }
-  };
-  const int hiA = CAUSAL ? min(myA, a.S - 1) : a.S - 1, hiB = CAUSAL ? min(myB, a.S - 1) : a.S - 1;
-  // the second phase re-reads the K / V fragments: opaque addresses keep the compiler from holding
-  // the first phase's 32 fragments (128 VGPRs) live into it
-  auto launder = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(ka[ks]));
-#pragma unroll
-    for (int d = 0; d < NDB; ++d) asm volatile("" : "+v"(va[d][0]), "+v"(va[d][1]));
-  };
-  auto address = [&](int t) __attribute__((always_inline)) {
-    const int kb_ = (t % NBUF) * SLOT, vb_ = ((t + NBUF - 1) % NBUF) * SLOT + TILE;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) ka[ks] = kofs[ks] + kb_;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d) {
-      va[d][0] = vlo[d] + vb_;
-      va[d][1] = vhi[d] + vb_;
-    }
-  };
-  // tile t's two phases; last: mask block A's S(t)
-  auto body = [&](int t, bool last) __attribute__((always_inline)) {
-    address(t);
-    rescale(oa, grow_a, alpha_a);
-    qk(qa, sa);
-    pv(pa, oa);
-    softmax(sb, t * KB - KB, -1, mb, lb, pb, alpha_b, grow_b);
-    if constexpr (SGB) w64_phase(std::make_integer_sequence<int, 32>{});
-    rescale(ob, grow_b, alpha_b);
-    launder();
-    qk(qb, sb);
-    pv(pb, ob);
-    softmax(sa, t * KB, last ? hiA : -1, ma, la, pa, alpha_a, grow_a);
-    if constexpr (SGB) w64_phase(std::make_integer_sequence<int, 32>{});
-  };
-  // after the last tile t: block A's PV and block B's (masked) softmax + PV of it
-  auto tail = [&](int t) __attribute__((always_inline)) {
-    address(t + 1);  // V_t
-    rescale(oa, grow_a, alpha_a);
-    pv(pa, oa);
-    softmax(sb, t * KB, hiB, mb, lb, pb, alpha_b, grow_b);
-    rescale(ob, grow_b, alpha_b);
-    launder();
-    pv(pb, ob);
-  };
-
-  __syncthreads();
-  // two tiles in flight ahead of the one computed; every wave passes ntiles barriers
-  auto sync = [&](int t) __attribute__((always_inline)) {
-    if (t + 1 < ntiles) vm_wait_n<2 * PPW>();  // tile t + 1's pieces may still fly
-    else vm_wait_n<0>();
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of t landed; every wave is done with t-2
-    if (t + 2 < ntiles) issue((t + 2) % NBUF);
-  };
-  if (0 < ntiles) issue(0);
-  if (1 < ntiles) issue(1);
-  int t = 0;
-  for (; t < tw; ++t) {
-    sync(t);
-    body(t, false);
-  }
-  if (tw >= 0) {
-    sync(tw);
-    body(tw, true);
-    tail(tw);
-    ++t;
-  }
-  for (; t < ntiles; ++t) sync(t);
-
-  auto store = [&](int my_q, f32x16* o, float m_i, float l_i) __attribute__((always_inline)) {
-    if (my_q >= a.S) return;
-    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
-    unsigned short* Op = a.o + b * a.o_sb + (long)my_q * a.o_ss + hq * a.o_sh;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int col = d * 32 + 8 * g + 4 * hh;
-        unsigned short w4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w4[j] = f2bf(o[d][4 * g + j] * inv);
-        *reinterpret_cast<uint2*>(Op + col) =
-            make_uint2((unsigned)w4[0] | ((unsigned)w4[1] << 16), (unsigned)w4[2] | ((unsigned)w4[3] << 16));
-      }
-    if (hh == 0)
-      a.lse[((long)b * a.Hq + hq) * a.S + my_q] =
-          (l_i > 0.f) ? (m_i + __log2f(l_i)) * 0.69314718055994531f : -INFINITY;
-  };
-  store(myA, oa, ma, la);
-  store(myB, ob, mb, lb);
-}
-
-// ---- the same structure with the K/V loop as one hand-scheduled asm program -----------------
-// (tools/gen_fa_w64.py -> fa_w64_asm.inc): the compiler-scheduled kernel above serialises every
-// LDS fragment read with its MFMA and clusters the softmax VALU after the MFMAs (~385 TF at B16
-// S2048, profiles/attn_fwd_w64_r5.txt); the program issues the reads two MFMAs ahead under counted
-// lgkmcnt waits and fills each MFMA gap with <= 24 issue cycles of the other block's softmax.  The
-// C++ part only computes lane offsets and buffer bounds; rows >= S load zeros / drop their
-// stores through the descriptors' record counts.
-template <bool CAUSAL, int MODE = 0>
-__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_fwd_w64a_kernel(FwdArgs a) {
-  constexpr bool STAMP = MODE > 0;
-  constexpr int HD = 128, NW = 4, QB = 256, NBUF = 4;
-  constexpr int ROWB = HD * 2, TILE = KB * ROWB, PPW = TILE / 1024 / NW, SLOT = 2 * TILE;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * SLOT];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, hh = lane >> 5;
-  const int nqb = (a.S + QB - 1) / QB;
-  const int BH = a.B * a.Hq;
-  int bh, rest;
-  if (BH % 8) {
-    bh = blockIdx.x % BH;
-    rest = blockIdx.x / BH;
-  } else {
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-    bh = x * (BH >> 3) + j / nqb;
-    rest = j % nqb;
-  }
-  const int qblk = nqb - 1 - rest;
-  const int b = bh / a.Hq, hq = bh % a.Hq;
-  const int hk = hq / (a.Hq / a.Hkv);
-  const int q_row0 = qblk * QB + wave * 64;
-  const int myA = q_row0 + r, myB = q_row0 + 32 + r;
-  const unsigned short* Qp = a.q + b * a.q_sb + hq * a.q_sh;
-  const unsigned short* Kp = a.k + b * a.k_sb + hk * a.k_sh;
-  const unsigned short* Vp = a.v + b * a.v_sb + hk * a.v_sh;
-  unsigned short* Op = a.o + b * a.o_sb + hq * a.o_sh;
-  float* Lp = a.lse + ((long)b * a.Hq + hq) * a.S;
-
-#pragma unroll
-  for (int i = 0; i < NBUF * SLOT / (256 * 16); ++i)
-    *reinterpret_cast<uint4*>(smem + i * 256 * 16 + tid * 16) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-
-  const int kv_end = CAUSAL ? min(a.S, qblk * QB + QB) : a.S;
-  const int ntiles = (kv_end + KB - 1) / KB;
-  const int tw = q_row0 >= a.S ? -1 : CAUSAL ? q_row0 / KB : ntiles - 1;
-  unsigned vk[PPW], vv[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int byte = (i * NW + wave) * 1024 + lane * 16;
-    const int row = byte / ROWB, pch = (byte % ROWB) >> 4;
-    vk[i] = (unsigned)((row * a.k_ss + ((pch ^ swz_row<HD>(row)) << 3)) * 2);
-    vv[i] = (unsigned)((row * a.v_ss + ((pch ^ swz_tr<HD>(row)) << 3)) * 2);
-  }
-  int ka[8], va[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) ka[ks] = row_off<HD>(r, 2 * ks + hh);
-#pragma unroll
-  for (int d = 0; d < 4; ++d) tr_frag_offs<HD>(d * 32, lane, va[2 * d], va[2 * d + 1]);
-  const unsigned long qb = (unsigned long)Qp, kb_ = (unsigned long)Kp, vb = (unsigned long)Vp;
-  const unsigned long ob = (unsigned long)Op, lb = (unsigned long)Lp;
-  const unsigned qlo = (unsigned)qb, qhi = (unsigned)(qb >> 32), kblo = (unsigned)kb_, kbhi = (unsigned)(kb_ >> 32);
-  const unsigned vblo = (unsigned)vb, vbhi = (unsigned)(vb >> 32), olo = (unsigned)ob, ohi = (unsigned)(ob >> 32);
-  const unsigned llo = (unsigned)lb, lhi = (unsigned)(lb >> 32);
-  const unsigned qnrec = (unsigned)(((a.S - 1) * a.q_ss + HD) * 2), onrec = (unsigned)(((a.S - 1) * a.o_ss + HD) * 2);
-  const unsigned lnrec = (unsigned)(a.S * 4);
-  const unsigned kstep = (unsigned)(KB * a.k_ss * 2), vstep = (unsigned)(KB * a.v_ss * 2);
-  const unsigned kss2 = (unsigned)(a.k_ss * 2), vss2 = (unsigned)(a.v_ss * 2);
-  const unsigned ldsdma = lds_addr(smem) + wave * 1024;
-  const unsigned vqA = (unsigned)(myA * a.q_ss * 2 + 16 * hh), vqB = (unsigned)(myB * a.q_ss * 2 + 16 * hh);
-  const unsigned vo0 = (unsigned)(myA * a.o_ss * 2 + 8 * hh), vo1 = (unsigned)(myB * a.o_ss * 2 + 8 * hh);
-  const unsigned vl0 = hh ? 0x40000000u : (unsigned)(myA * 4), vl1 = hh ? 0x40000000u : (unsigned)(myB * 4);
-  const int khi0 = (CAUSAL ? min(myA, a.S - 1) : a.S - 1) - 4 * hh;
-  const int khi1 = (CAUSAL ? min(myB, a.S - 1) : a.S - 1) - 4 * hh;
-  const float c = a.scale_log2;
-  const int S = a.S;
-  // diagnostic build: per-wave cycle totals of the program's sections (tools/attn_fwd_ab.py --stamps)
-  const unsigned long sp = (unsigned long)a.stamp;
-  const unsigned stlo = (unsigned)sp, sthi = (unsigned)(sp >> 32);
-  const unsigned vst = (STAMP && lane == 0 && blockIdx.x < 1024) ? (blockIdx.x * 4 + wave) * 64 : 0x40000000u;
-#define FA_W64_OPERANDS \
-               : [qlo] "s"(qlo), [qhi] "s"(qhi), [qnrec] "s"(qnrec), [kblo] "s"(kblo), [kbhi] "s"(kbhi), \
-                 [vblo] "s"(vblo), [vbhi] "s"(vbhi), [kstep] "s"(kstep), [vstep] "s"(vstep), [kss2] "s"(kss2), \
-                 [vss2] "s"(vss2), [S] "s"(S), [ntiles] "s"(ntiles), [tw] "s"(tw), [c] "s"(c), \
-                 [ldsdma] "s"(ldsdma), [olo] "s"(olo), [ohi] "s"(ohi), [onrec] "s"(onrec), [llo] "s"(llo), \
-                 [lhi] "s"(lhi), [lnrec] "s"(lnrec), [vqA] "v"(vqA), [vqB] "v"(vqB), [vk0] "v"(vk[0]), \
-                 [vk1] "v"(vk[1]), [vk2] "v"(vk[2]), [vk3] "v"(vk[3]), [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), \
-                 [vv2] "v"(vv[2]), [vv3] "v"(vv[3]), [ka0] "v"(ka[0]), [ka1] "v"(ka[1]), [ka2] "v"(ka[2]), \
-                 [ka3] "v"(ka[3]), [ka4] "v"(ka[4]), [ka5] "v"(ka[5]), [ka6] "v"(ka[6]), [ka7] "v"(ka[7]), \
-                 [va0] "v"(va[0]), [va1] "v"(va[1]), [va2] "v"(va[2]), [va3] "v"(va[3]), [va4] "v"(va[4]), \
-                 [va5] "v"(va[5]), [va6] "v"(va[6]), [va7] "v"(va[7]), [khi0] "v"(khi0), [khi1] "v"(khi1), \
-                 [vo0] "v"(vo0), [vo1] "v"(vo1), [vl0] "v"(vl0), [vl1] "v"(vl1), [stlo] "s"(stlo), [sthi] "s"(sthi), [vst] "v"(vst)
-  if constexpr (MODE == 1) asm volatile(FA_W64_ASM_S1 : FA_W64_OPERANDS : FA_W64_CLOBBERS);
-  else if constexpr (MODE == 2) asm volatile(FA_W64_ASM_S2 : FA_W64_OPERANDS : FA_W64_CLOBBERS);
-  else if constexpr (MODE == 3) asm volatile(FA_W64_ASM_S3 : FA_W64_OPERANDS : FA_W64_CLOBBERS);
-  else if constexpr (MODE == 4) asm volatile(FA_W64_ASM_S4 : FA_W64_OPERANDS : FA_W64_CLOBBERS);
-  else asm volatile(FA_W64_ASM : FA_W64_OPERANDS : FA_W64_CLOBBERS);
-#undef FA_W64_OPERANDS
-}
-
 // merge the two K/V-range halves: lse = logaddexp(l0, l1), o = o0 e^(l0-lse) + o1 e^(l1-lse)
 template <int HD>
 __global__ __launch_bounds__(256) void fa_combine_kernel(const unsigned short* __restrict__ o_part,
@@ -869,35 +468,6 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
             v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2),
             (float)(scale * 1.4426950408889634), nullptr, nullptr, nullptr, 0};
   a.prio = knob("fa_prio", 1) != 0 ? 1 : 0;  // default on: 2-3 % at B12 S2048 (0: off, A/B)
-  // one-wave-per-SIMD 64-row kernel (knob fa_w64): HD 128 without documents, on grids that do
-  // not take the small-grid K/V split (fwd_launch<4, 2>'s rule, 128-row blocks)
-  if (D == 128 && !(doc_start.has_value() && doc_start->defined()) && knob("fa_w64", 0) != 0) {
-    const int nqb128 = (S + 127) / 128;
-    const int64_t e = knob("fa_split", -1);
-    const bool split = e == 1   ? causal && nqb128 >= 2
-                       : e == 0 ? false
-                                : causal && nqb128 >= 4 && (long)B * Hq * nqb128 <= 2L * num_cus();
-    if (!split) {
-      dim3 grid((unsigned)(B * Hq * ((S + 255) / 256))), block(256);
-      // fa_w64 = 1: compiler-scheduled phases, 2: sched_group_barrier interleave, 3: asm program
-      const int64_t var = knob("fa_w64", 0);
-      const bool sgb = var == 2;
-      if (var == 3) {
-        a.stamp = reinterpret_cast<unsigned*>(knob("fa_stamp_ptr", 0));
-        const int64_t mode = a.stamp && causal ? knob("fa_w64_mode", 1) : 0;  // 2-4: timing ablations
-        if (mode == 1) hipLaunchKernelGGL((fa_fwd_w64a_kernel<true, 1>), grid, block, 0, stream(), a);
-        else if (mode == 2) hipLaunchKernelGGL((fa_fwd_w64a_kernel<true, 2>), grid, block, 0, stream(), a);
-        else if (mode == 3) hipLaunchKernelGGL((fa_fwd_w64a_kernel<true, 3>), grid, block, 0, stream(), a);
-        else if (mode == 4) hipLaunchKernelGGL((fa_fwd_w64a_kernel<true, 4>), grid, block, 0, stream(), a);
-        else if (causal) hipLaunchKernelGGL((fa_fwd_w64a_kernel<true>), grid, block, 0, stream(), a);
-        else hipLaunchKernelGGL((fa_fwd_w64a_kernel<false>), grid, block, 0, stream(), a);
-      } else if (causal && sgb) hipLaunchKernelGGL((fa_fwd_w64_kernel<true, true>), grid, block, 0, stream(), a);
-      else if (causal) hipLaunchKernelGGL((fa_fwd_w64_kernel<true, false>), grid, block, 0, stream(), a);
-      else if (sgb) hipLaunchKernelGGL((fa_fwd_w64_kernel<false, true>), grid, block, 0, stream(), a);
-      else hipLaunchKernelGGL((fa_fwd_w64_kernel<false, false>), grid, block, 0, stream(), a);
-      return {o, lse};
-    }
-  }
   // workgroup shape: knob fa_nw = 8 -> 8 waves (256 rows) with a 3-slot ring, one workgroup per
   // CU; default 4 waves (128 rows) with a 2-slot ring, two per CU (A/B knob, tools/attn_bench.py)
   if (knob("fa_nw", 4) == 8) return fwd_launch<8, 3>(q, o, lse, a, B, S, Hq, D, causal, doc_start);

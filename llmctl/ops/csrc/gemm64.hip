@@ -1290,16 +1290,27 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 // of an SGPR (v_readlane reload) ahead of an inline-asm buffer_load was not confirmed --
 // tools/sgpr_hazard_check.py found only SALU writers ahead of those loads.  K >= 256.
 // Phase schedule: the one-shot 4-wave kernel's.
-// STAMP (diagnostic build, knobs gemm_stamp=1 + gemm_stamp_ptr=<device u32 buffer>): lane 0 of every
-// wave records s_memtime (low 32 bits) at the start of every phase of its first 4 items into LDS and
-// copies them out after each item's epilogue: [block < 32][wave][item < 4][STAMPS] (tools/gemm_stamps.py).
+// STAMP (diagnostic build only: compile with -DLLMCTL_STAMP, then knob gemm_stamp_ptr=<device u32
+// buffer>): lane 0 of every wave records s_memtime (low 32 bits) at the start of every phase of its
+// first 4 items into LDS and copies them out after each item's epilogue: [block < 32][wave][item <
+// 4][STAMPS] (tools/gemm_stamps.py).  The production library carries no diagnostic code.
 // Measured-neutral variants tried on this kernel (round 5, profiles/gemm_r5_ab.txt): DMA waits 4 / 8
 // pieces tighter (fewer loads in flight), and a phase's DMA pieces spread over the whole phase (wrong
 // results: an LDS-DMA interleaved with the phase's fragment reads).
 constexpr int STAMPS = 272;
-// EXP (with STAMP; knob gemm_exp, results garbage): 1 = no DMA pieces in the loop, 2 = no workgroup
-// barriers (waits kept), 3 = no fragment reads -- each phase's cycles without that component.
-template <bool AT, bool BT, int EPI, int GROUP, int STAMP = 0, int EXP = 0>
+// EXP (diagnostic build, -DLLMCTL_STAMP_EXP=n; results garbage): 1 = no DMA pieces in the loop, 2 = no
+// workgroup barriers (waits kept), 3 = no fragment reads -- each phase's cycles without that component.
+#ifdef LLMCTL_STAMP
+constexpr int STAMP = 1;
+#ifdef LLMCTL_STAMP_EXP
+constexpr int EXP = LLMCTL_STAMP_EXP;
+#else
+constexpr int EXP = 0;
+#endif
+#else
+constexpr int STAMP = 0, EXP = 0;
+#endif
+template <bool AT, bool BT, int EPI, int GROUP>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4wp_kernel(G64Args args,
                                                                                                   int n_items) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF + (STAMP ? 4 * STAMPS * 4 : 0)];
@@ -1532,192 +1543,6 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   }
 }
 
-// ---- 2-phase persistent 4-wave kernel (config variant 5) ---------------------------------------
-// Same tile (256 x 256, 4 waves of 128 x 128, 64-deep K-tiles in two LDS slots) and the same LDS
-// images as the 4-phase kernels above, but the K-tile is computed in TWO phases of 64 MFMAs, one per
-// 32-deep K-slice, each over all 8 x 8 accumulator tiles (cf. hipBLASLt's gfx950 256x256x64 kernel,
-// which also runs one wave per SIMD and two K-slices per tile).  What the 4-phase kernel spent per
-// phase (tools/gemm_stamps.py, profiles/gemm_stamps_r5.txt: 608-684 cycles for 512 cycles of MFMA):
-// ~35-40 cycles per workgroup barrier, ~30-50 for its 4 DMA pieces, 10-30 for the fragment reads.
-// Here a K-tile has 2 barriers instead of 4, and the counted waits are gone:
-//   phase (t, 0): MFMAs on set 0 (slice 0 of tile t); read set 1 (slice 1 of tile t, slot t & 1);
-//                 vmcnt(0) + lgkmcnt(0) + barrier  -- retires tile t + 1 (issued one phase ago)
-//   phase (t, 1): MFMAs on set 1; read set 0 (slice 0 of tile t + 1, slot (t + 1) & 1); the 16 DMA
-//                 pieces of tile t + 2 into slot t & 1 (its last reads were retired before the
-//                 barrier above: WAR) inside statements 16-31; lgkmcnt(0) + barrier
-// A DMA piece has one and a half phases (~1.5k cycles) to land.  Every vmcnt wait is vmcnt(0) and
-// only ever waits for the one tile the next phase reads (plus an item's epilogue stores, at its next
-// item's first wait), so the count is exact whatever order stores and loads retire in.  Items
-// stream as in the 4-phase persistent kernel: the last two K-tiles' DMA pieces (and the last
-// phase's set-0 reads) belong to the next item; after the last item they are issued out of range
-// (num_records 0: no memory traffic, zeros into slots nobody reads).
-template <bool AT, bool BT, int EPI, int GROUP>
-__global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm2p_kernel(G64Args args,
-                                                                                                  int n_items) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int wr = wave >> 1, wc = wave & 1;
-  constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;
-  const long lda = args.lda, ldb = args.ldb;
-  const unsigned a_kstep = AT ? (unsigned)(TK * lda * 2) : (unsigned)(TK * 2);
-  const unsigned b_kstep = BT ? (unsigned)(TK * ldb * 2) : (unsigned)(TK * 2);
-
-  auto decode = [&](int bid, int& tm, int& tn, int& sp, int& u, int& KT, unsigned& kt0, i32x4_t& ra, i32x4_t& rb,
-                    i32x4_t& rb_hi) __attribute__((always_inline)) {
-    int wg;
-    sp = -1;
-    u = 0;
-    if (bid < args.n_main) {
-      const int nwg = args.n_main;
-      const int q = nwg / 8, rem = nwg % 8, x = bid % 8;
-      wg = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + bid / 8;
-    } else {
-      const int i = bid - args.n_main;
-      u = i / args.splits;
-      sp = i - u * args.splits;
-      wg = args.n_main + u;
-    }
-    const int per_group = GROUP * args.tiles_n;
-    const int grp = wg / per_group;
-    const int gsz = min(GROUP, args.tiles_m - grp * GROUP);
-    const int inner = wg - grp * per_group;
-    tm = grp * GROUP + inner % gsz;
-    tn = inner / gsz;
-    KT = sp < 0 ? args.K / TK : args.kt_part;
-    kt0 = sp < 0 ? 0u : (unsigned)(sp * args.kt_part);
-    const unsigned short* Ab = AT ? args.a + (long)tm * TM : args.a + (long)tm * TM * lda;
-    const unsigned short* Bb = PAIRED_B ? args.b + (long)tn * (TN / 2) * ldb
-                               : BT ? args.b + (long)tn * TN : args.b + (long)tn * TN * ldb;
-    ra = make_rsrc(Ab);
-    rb = make_rsrc(Bb);
-    rb_hi = PAIRED_B ? make_rsrc(args.b + ((long)args.N + (long)tn * (TN / 2) - TN / 2) * ldb) : rb;
-  };
-
-  unsigned vo[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    vo[A_LO][i] = stage_voff<AT, A_LO, NT4>(i, tid, lda);
-    vo[A_HI][i] = stage_voff<AT, A_HI, NT4>(i, tid, lda);
-    vo[B_H0][i] = stage_voff<BT, B_H0, NT4>(i, tid, ldb);
-    vo[B_H1][i] = stage_voff<BT, B_H1, NT4>(i, tid, ldb);
-  }
-  const unsigned lds0 = lds_addr(smem) + wave * 1024;
-  const int ap = wr * 64;
-  const int bo03 = PAIRED_B ? B_H0 * HALF : (B_H0 + wc) * HALF, p03 = PAIRED_B ? wc * 64 : 0;
-  const int bo47 = PAIRED_B ? B_H1 * HALF : (B_H0 + wc) * HALF, p47 = PAIRED_B ? wc * 64 : 64;
-
-  int g = blockIdx.x;
-  int c_tm, c_tn, c_sp, c_u, c_KT, n_tm, n_tn, n_sp, n_u, n_KT;
-  unsigned c_kt0, n_kt0;
-  i32x4_t c_ra, c_rb, c_rbh, n_ra, n_rb, n_rbh;
-  decode(g, c_tm, c_tn, c_sp, c_u, c_KT, c_kt0, c_ra, c_rb, c_rbh);
-
-  f32x4_t acc[8][8];
-  bf16x8_t fa[2][8], fb[2][8];  // fragment sets by K-slice: m-tiles 0-7 / n-tiles 0-7
-  // fragment k (0-7: A m-tile k, 8-15: B n-tile k - 8) of K-slice ks of the slot at buf -> set S
-  auto rd = [&](auto set_c, int k, const unsigned char* buf, int ks) __attribute__((always_inline)) {
-    constexpr int S = decltype(set_c)::value;
-    if (k < 8) fa[S][k] = frag<AT>(buf + (k < 4 ? A_LO : A_HI) * HALF, ap + 16 * (k & 3), ks, lane);
-    else {
-      const int j = k - 8;
-      fb[S][j] = frag<BT>(buf + (j < 4 ? bo03 : bo47), (j < 4 ? p03 : p47) + 16 * (j & 3), ks, lane);
-    }
-  };
-  // one phase: 32 statements of 2 MFMAs on set S (acc row i = s >> 2, n-tile pair s & 3); the 16
-  // reads of the other set after statements 0-15; with DMA, piece s - 16 of stream slot t + 2
-  // (kind (s - 16) >> 2) inside statements 16-31
-  auto phase = [&](auto set_c, auto zero_c, auto dma_c, auto next_c, auto read_c, const unsigned char* rbuf, int t)
-                   __attribute__((always_inline)) {
-    constexpr int S = decltype(set_c)::value;
-    constexpr bool ZERO = decltype(zero_c)::value, DMA = decltype(dma_c)::value, NEXT = decltype(next_c)::value;
-    constexpr bool READ = decltype(read_c)::value;
-    unsigned so_a = 0, so_b = 0;
-    i32x4_t r_a = c_ra, r_b0 = c_rb, r_b1 = c_rbh;
-    if constexpr (DMA) {
-      const unsigned tc = NEXT ? n_kt0 + (unsigned)(t + 2 - c_KT) : c_kt0 + (unsigned)(t + 2);
-      so_a = __builtin_amdgcn_readfirstlane(tc * a_kstep);
-      so_b = __builtin_amdgcn_readfirstlane(tc * b_kstep);
-      if constexpr (NEXT) {
-        r_a = n_ra;
-        r_b0 = n_rb;
-        r_b1 = n_rbh;
-      }
-    }
-    const unsigned ldst = lds0 + (t & 1) * BUF;
-#pragma unroll
-    for (int s = 0; s < 32; ++s) {
-      const int i = s >> 2, jp = s & 3;
-      f32x4_t& c0 = acc[i][2 * jp];
-      f32x4_t& c1 = acc[i][2 * jp + 1];
-      if (DMA && s >= 16) {
-        const int p = s - 16, kind = p >> 2, pi = p & 3;
-        const i32x4_t rr = kind <= A_HI ? r_a : kind == B_H1 ? r_b1 : r_b0;
-        g4w_pair_dma(c0, c1, fa[S][i], fb[S][2 * jp], fb[S][2 * jp + 1], vo[kind][pi], rr,
-                     kind <= A_HI ? so_a : so_b, ldst + kind * HALF + pi * 4096);
-      } else if (ZERO) {
-        g4w_pair_z(c0, c1, fa[S][i], fb[S][2 * jp], fb[S][2 * jp + 1]);
-      } else {
-        g4w_pair(c0, c1, fa[S][i], fb[S][2 * jp], fb[S][2 * jp + 1]);
-      }
-      if (READ && s < 16) rd(std::integral_constant<int, S ^ 1>{}, s, rbuf, S ^ 1);
-    }
-  };
-  auto sync = [&](auto vm_c) __attribute__((always_inline)) {
-    if constexpr (decltype(vm_c)::value) wait_vm<0>();
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (builtin: hipcc's waitcnt pass sees it)
-    bar();
-  };
-  // K-tile t in slot P: slice 0 (reads slice 1 of the same slot), slice 1 (reads slice 0 of slot P ^ 1,
-  // i.e. tile t + 1 -- the next item's tile 0 after an item's last K-tile; DMA of tile t + 2)
-  auto ktile = [&](int t, auto par_c, auto zero_c, auto next_c) __attribute__((always_inline)) {
-    constexpr int P = decltype(par_c)::value;
-    phase(K_<0>{}, zero_c, std::false_type{}, std::false_type{}, std::true_type{}, smem + P * BUF, t);
-    sync(std::true_type{});
-    phase(K_<1>{}, std::false_type{}, std::true_type{}, next_c, std::true_type{}, smem + (P ^ 1) * BUF, t);
-    sync(std::false_type{});
-  };
-
-  // prologue (first item): K-tiles 0 and 1 in flight, retire tile 0, read its slice-0 set
-  {
-    const i32x4_t rr[4] = {c_ra, c_ra, c_rb, c_rbh};
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int kind = 0; kind < 4; ++kind) {
-        const unsigned so = __builtin_amdgcn_readfirstlane((c_kt0 + (unsigned)tt) * (kind <= A_HI ? a_kstep : b_kstep));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bdma16(rr[kind], vo[kind][i], so, lds0 + tt * BUF + kind * HALF + i * 4096);
-      }
-    wait_vm<16>();
-    bar();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) rd(K_<0>{}, k, smem, 0);
-  }
-
-  while (true) {
-    ktile(0, K_<0>{}, std::true_type{}, std::false_type{});
-    ktile(1, K_<1>{}, std::false_type{}, std::false_type{});
-    for (int t = 2; t < c_KT - 2; t += 2) {
-      ktile(t, K_<0>{}, std::false_type{}, std::false_type{});
-      ktile(t + 1, K_<1>{}, std::false_type{}, std::false_type{});
-    }
-    const bool has_next = g + (int)gridDim.x < n_items;
-    decode(has_next ? g + (int)gridDim.x : g, n_tm, n_tn, n_sp, n_u, n_KT, n_kt0, n_ra, n_rb, n_rbh);
-    if (!has_next) n_ra[2] = n_rb[2] = n_rbh[2] = 0;  // the stream's tail: out of range, nothing moves
-    ktile(c_KT - 2, K_<0>{}, std::false_type{}, std::true_type{});
-    ktile(c_KT - 1, K_<1>{}, std::false_type{}, std::true_type{});
-    g2p_fence(acc);
-    g4w_epilogue<EPI>(args, acc, c_tm, c_tn, wr, wc, lane, c_sp, c_u);
-    if (!has_next) break;
-    g += (int)gridDim.x;
-    c_tm = n_tm, c_tn = n_tn, c_sp = n_sp, c_u = n_u, c_KT = n_KT, c_kt0 = n_kt0;
-    c_ra = n_ra, c_rb = n_rb, c_rbh = n_rbh;
-  }
-  wait_vm<0>();  // out-of-range tail pieces (nothing moves; retire before the workgroup ends)
-}
-
 // sum of the split partials of tail tile u (grouped-order position n_main + u) + epilogue;
 // thread = 8 consecutive columns of one row
 template <int EPI, int GROUP>
@@ -1785,27 +1610,9 @@ void launch_g(const G64Args& g, int variant) {
   const dim3 grid(n_items);
   bool launched = false;
   if constexpr (EPI != EPI_SWIGLU_BWD) {
-    if (variant == 5 && g.K >= 4 * TK) {  // 2-phase persistent kernel
-      hipLaunchKernelGGL((gemm2p_kernel<AT, BT, EPI, GROUP>), dim3(min(n_items, num_cus())), dim3(NT4), 0, stream(), g,
+    if (variant == 3 && g.K >= 4 * TK) {  // the persistent kernel peels two K-tiles per item
+      hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP>), dim3(min(n_items, num_cus())), dim3(NT4), 0, stream(), g,
                          n_items);
-      launched = true;
-    } else if (variant == 3 && g.K >= 4 * TK) {  // the persistent kernel peels two K-tiles per item
-      const dim3 pg(min(n_items, num_cus()));
-      if constexpr (EPI == EPI_STORE && GROUP == 4) {
-        const int ex = g.stamp_ptr ? (int)knob("gemm_exp", 0) : 0;
-        if (g.stamp_ptr && ex == 1)
-          hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP, 1, 1>), pg, dim3(NT4), 0, stream(), g, n_items);
-        else if (g.stamp_ptr && ex == 2)
-          hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP, 1, 2>), pg, dim3(NT4), 0, stream(), g, n_items);
-        else if (g.stamp_ptr && ex == 3)
-          hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP, 1, 3>), pg, dim3(NT4), 0, stream(), g, n_items);
-        else if (g.stamp_ptr)
-          hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP, 1>), pg, dim3(NT4), 0, stream(), g, n_items);
-        else
-          hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP>), pg, dim3(NT4), 0, stream(), g, n_items);
-      } else {
-        hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP>), pg, dim3(NT4), 0, stream(), g, n_items);
-      }
       launched = true;
     } else if (variant >= 3) {
       hipLaunchKernelGGL((gemm4w_kernel<AT, BT, EPI, GROUP>), grid, dim3(NT4), 0, stream(), g);

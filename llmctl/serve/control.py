@@ -193,21 +193,50 @@ class TensorChannel:
         pass
 
 
+class PeerLostError(RuntimeError):
+    """A TP control-plane peer died, closed its end or stopped heart-beating past the deadline."""
+
+
+def _pid_alive(pid: int) -> bool:
+    if pid <= 0:
+        return True  # not registered yet
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return True
+
+
 class ShmChannel:
     """Single-writer ring in a ``/dev/shm`` file (one node).  Layout (bytes):
 
-    ``[0, 64 * 32)``        per-reader ack words (u64, one 64-B line each; index = group rank)
+    ``[0, 64 * 32)``        one 64-B line per rank (index = group rank), u64 words:
+                            [0] ack (last seq read; readers), [1] pid, [2] heartbeat
+                            (CLOCK_MONOTONIC ns, node-wide), [3] closed flag
     ``[2048, ...)``         SLOTS slots of ``slot_bytes``: [u64 seq][u64 nbytes][u64 spill][pad
                             to 64][record]
 
     A plan that does not fit a slot is published with ``spill = 1`` and its bytes follow through
-    the gloo :class:`TensorChannel` (same order on every rank)."""
+    the gloo :class:`TensorChannel` (same order on every rank).
+
+    Liveness (the gloo path it replaced raised on the process-group timeout): every
+    rank writes its pid at setup and a heartbeat word from a daemon thread every
+    ``timeout_s / 8`` (at most 1 s).  A reader waiting for a plan and rank 0 waiting for a reader's
+    ack check the peer they wait on about every 50 ms and raise :class:`PeerLostError` when its
+    process is gone, it closed the channel, or its heartbeat is older than ``timeout_s`` (a frozen
+    process).  An idle server is not a failure: rank 0's heartbeat keeps its readers waiting.  The
+    TP worker then exits non-zero and torchrun tears the group down
+    (``/root/reference/llmctl/runtime/launcher.py:283-312`` watches exit codes the same way)."""
 
     SLOTS = 4
     HDR = 2048
     SLOT_HDR = 64
+    CHECK_S = 0.05  # liveness check period while blocked
 
-    def __init__(self, group, slot_bytes: int = 8 << 20, path: Optional[str] = None, poll_spin_s: float = 2e-3):
+    def __init__(self, group, slot_bytes: int = 8 << 20, path: Optional[str] = None, poll_spin_s: float = 2e-3,
+                 timeout_s: float = 600.0):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -215,6 +244,7 @@ class ShmChannel:
             raise ValueError("ShmChannel: at most 32 ranks")
         self.slot_bytes = slot_bytes
         self.poll_spin_s = poll_spin_s
+        self.timeout_s = float(timeout_s)
         self.fallback = TensorChannel(group)
         box = [None]
         if self.rank == 0:
@@ -233,10 +263,43 @@ class ShmChannel:
         self.u64 = self.mm.view(np.uint64)
         self._ack_idx = np.arange(1, self.world, dtype=np.int64) * 8
         self.seq = 0
-        dist.barrier(group=group)  # every rank mapped the file before rank 0 may unlink it
+        me = 8 * self.rank
+        self.u64[me + 1] = os.getpid()
+        self.u64[me + 2] = time.monotonic_ns()
+        self._hb_stop = None
+        self._start_heartbeat()
+        dist.barrier(group=group)  # every rank mapped the file (and wrote its pid) before rank 0 unlinks it
         if self.rank == 0:
             os.unlink(self.path)  # the mappings keep it alive; nothing leaks if a rank dies
         self.stats = {"published": 0, "spilled": 0}
+
+    # ------------------------------------------------------------------ liveness
+    def _start_heartbeat(self) -> None:
+        import threading
+
+        stop = threading.Event()
+        period = min(1.0, max(0.01, self.timeout_s / 8))
+        u64, word = self.u64, 8 * self.rank + 2
+
+        def beat():
+            while not stop.wait(period):
+                u64[word] = time.monotonic_ns()
+
+        self._hb_stop = stop
+        self._hb_thread = threading.Thread(target=beat, name=f"llmctl-shm-hb{self.rank}", daemon=True)
+        self._hb_thread.start()
+
+    def _check_peer(self, r: int, waited_s: float) -> None:
+        line = 8 * r
+        pid = int(self.u64[line + 1])
+        if int(self.u64[line + 3]):
+            raise PeerLostError(f"TP control plane: rank {r} closed the channel while rank {self.rank} waited on it")
+        if not _pid_alive(pid):
+            raise PeerLostError(f"TP control plane: rank {r} (pid {pid}) is gone; rank {self.rank} gives up")
+        age = (time.monotonic_ns() - int(self.u64[line + 2])) / 1e9
+        if age > self.timeout_s:
+            raise PeerLostError(f"TP control plane: rank {r} (pid {pid}) has not heart-beaten for {age:.1f} s "
+                                f"(deadline {self.timeout_s:.1f} s; rank {self.rank} waited {waited_s:.1f} s)")
 
     def _slot(self, seq: int) -> int:
         return self.HDR + (seq % self.SLOTS) * self.slot_bytes
@@ -250,9 +313,18 @@ class ShmChannel:
         s = self.seq
         base = self._slot(s)
         t0 = time.perf_counter()
+        next_check = t0 + self.CHECK_S
         while s - self._ack_min() > self.SLOTS:  # slot still unread by some rank
-            if time.perf_counter() - t0 > self.poll_spin_s:
+            now = time.perf_counter()
+            if now - t0 > self.poll_spin_s:
                 time.sleep(1e-5)
+            if now > next_check:
+                next_check = now + self.CHECK_S
+                for r in range(1, self.world):
+                    if s - int(self.u64[8 * r]) > self.SLOTS:  # only the laggards
+                        self._check_peer(r, now - t0)
+                if now - t0 > self.timeout_s:
+                    raise PeerLostError(f"TP control plane: no ack within {self.timeout_s:.1f} s")
         spill = len(b) > self.slot_bytes - self.SLOT_HDR
         w = base // 8
         if not spill:
@@ -271,14 +343,21 @@ class ShmChannel:
         base = self._slot(s)
         w = base // 8
         t0 = time.perf_counter()
-        idle = 0
+        next_check = t0 + self.CHECK_S
         while int(self.u64[w]) != s:
-            el = time.perf_counter() - t0
+            now = time.perf_counter()
+            el = now - t0
             if el > self.poll_spin_s:  # idle server: back off (50 us, then 1 ms sleeps)
-                idle += 1
                 time.sleep(1e-3 if el > 0.5 else 5e-5)
             else:
                 os.sched_yield()  # spinning, but never starve the ranks that share this CPU
+            if now > next_check:
+                next_check = now + self.CHECK_S
+                try:
+                    self._check_peer(0, el)
+                except PeerLostError:
+                    if int(self.u64[w]) != s:  # rank 0 may publish its last plan (stop) and close at once
+                        raise
         n = int(self.u64[w + 1])
         if int(self.u64[w + 2]):
             plan = self.fallback.receive()
@@ -288,7 +367,12 @@ class ShmChannel:
         return plan
 
     def close(self) -> None:
+        if self._hb_stop is not None:
+            self._hb_stop.set()
+            self._hb_thread.join(timeout=2.0)  # it holds a view of the mapping
+            self._hb_stop = self._hb_thread = None
         if self.mm is not None:
+            self.u64[8 * self.rank + 3] = 1  # a clean close: peers still waiting on this rank raise
             del self.u64
             self.mm = None
             try:
@@ -297,9 +381,27 @@ class ShmChannel:
                 pass
 
 
-def make_channel(group, kind: str = "auto"):
-    """``shm`` when every rank of ``group`` is on this node (TP serving), else gloo tensors."""
+def _node_id() -> str:
+    import socket
+
+    boot = ""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        pass
+    return f"{socket.gethostname()}/{boot}"
+
+
+def make_channel(group, kind: str = "auto", timeout_s: float = 600.0):
+    """``shm`` when every rank of ``group`` is on this node (TP serving), else gloo tensors.
+
+    ``auto`` decides from the node ids (hostname + boot id) all-gathered over ``group``: every rank
+    sees the same list, so every rank picks the same channel -- a group that spans nodes (or ranks
+    with inconsistent ``LOCAL_WORLD_SIZE``) falls back to gloo instead of half the ranks opening a
+    file the other node holds."""
     if kind == "auto":
-        local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-        kind = "shm" if dist.get_world_size(group) <= local and os.path.isdir("/dev/shm") else "tensor"
-    return ShmChannel(group) if kind == "shm" else TensorChannel(group)
+        ids: List[Optional[str]] = [None] * dist.get_world_size(group)
+        dist.all_gather_object(ids, _node_id(), group=group)
+        kind = "shm" if len(set(ids)) == 1 and os.path.isdir("/dev/shm") else "tensor"
+    return ShmChannel(group, timeout_s=timeout_s) if kind == "shm" else TensorChannel(group)

@@ -17,12 +17,16 @@ from __future__ import annotations
 
 import asyncio
 import json
+import logging
+import os
 import threading
 import time
 import uuid
 from typing import Any, Dict, List, Optional, Union
 
 from pydantic import BaseModel, Field
+
+log = logging.getLogger("llmctl.serve.server")
 
 
 class GenerationRequest(BaseModel):
@@ -169,6 +173,14 @@ class InferenceServer:
                         if seq.on_finish:
                             seq.on_finish(seq)
                     e.scheduler.waiting.clear()
+                from .control import PeerLostError
+
+                if isinstance(ex, PeerLostError):
+                    # a TP rank is gone: the group cannot serve again.  Give the failed requests a
+                    # moment to be answered, then leave non-zero so the launcher tears down the job
+                    log.error("TP peer lost, server exiting: %s", ex)
+                    threading.Timer(0.5, os._exit, (70,)).start()
+                    return
 
     # ------------------------------------------------------------------ request handling
     def _make_params(self, req: GenerationRequest):

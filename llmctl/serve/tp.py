@@ -21,6 +21,7 @@ xGMI peer-memory kernel (:mod:`llmctl.comms.custom_ar`) unless knob ``custom_ar`
 from __future__ import annotations
 
 import logging
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -49,6 +50,8 @@ class TPInferenceEngine(InferenceEngine):
         # plan channel (created on first use by every rank in the same order): "auto" = shm ring
         # on one node, gloo tensors otherwise; "tensor" / "shm" force one
         self.control_kind = kw.pop("control", "auto")
+        # liveness deadline of the shm plan ring (a frozen peer; a dead one is seen within ~50 ms)
+        self.control_timeout_s = float(kw.pop("control_timeout_s", 600.0))
         self.channel = None
         pc = ParallelContext(tp_group=tp_group, tp_size=self.tp_size, tp_rank=self.tp_rank)
         # this engine's own knobs (perf_knobs + LLMCTL_KNOBS) decide, not whatever is active
@@ -138,7 +141,7 @@ class TPInferenceEngine(InferenceEngine):
         if self.channel is None:
             from llmctl.serve.control import make_channel
 
-            self.channel = make_channel(self.control, self.control_kind)
+            self.channel = make_channel(self.control, self.control_kind, timeout_s=self.control_timeout_s)
         if self.tp_rank == 0:
             self.channel.publish(plan)
             return plan
@@ -251,14 +254,26 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv-cache-dtype", default="auto")
     ap.add_argument("--weight-dtype", default="auto")
+    ap.add_argument("--control-timeout", type=float, default=600.0,
+                    help="seconds a frozen TP peer may stop heart-beating before the others exit")
     a = ap.parse_args(argv)
     group, dev = init_tp()
     eng = TPInferenceEngine(a.artifact, tp_group=group, device=dev, max_batch_size=a.max_batch_size,
                             max_batch_tokens=a.max_batch_tokens, kv_cache_fraction=a.kv_cache_fraction,
                             block_size=a.block_size, scheduler=a.scheduler, use_graphs=not a.no_graphs,
-                            kv_cache_dtype=a.kv_cache_dtype, weight_dtype=a.weight_dtype)
+                            kv_cache_dtype=a.kv_cache_dtype, weight_dtype=a.weight_dtype,
+                            control_timeout_s=a.control_timeout)
+    from .control import PeerLostError
+
     if eng.tp_rank != 0:
-        eng.worker_loop()
+        try:
+            eng.worker_loop()
+        except PeerLostError as e:
+            # a peer is gone: leave non-zero at once (a teardown through the broken group could
+            # hang) so torchrun sees the failure and stops the rest of the group
+            log.error("%s", e)
+            logging.shutdown()
+            os._exit(70)
         eng.close()
         dist.destroy_process_group()
         return 0

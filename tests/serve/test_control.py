@@ -31,3 +31,51 @@ def test_control_channel_multirank(kind, slot):
         assert torch.equal(out[r]["digest"], out[0]["digest"])
     if kind == "shm" and slot == 4096:
         assert int(out[0]["spilled"]) > 0  # big prefill plans went through the gloo fallback
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("victim,mode", [(0, "kill"), (2, "kill"), (0, "stop")])
+def test_shm_channel_peer_loss(victim, mode):
+    """A dead (or frozen) rank 0 / a dead reader: every survivor raises PeerLostError and exits
+    non-zero within the deadline (2 s heartbeat deadline here) instead of spinning forever, and no
+    /dev/shm ring file is left behind."""
+    import glob
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    before = set(glob.glob("/dev/shm/llmctl-tp-*"))
+    port, world = _free_port(), 3
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    procs = [subprocess.Popen([sys.executable, "-m", "llmctl.testing.shm_liveness", "--rank", str(r), "--world",
+                               str(world), "--port", str(port), "--victim", str(victim), "--mode", mode],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True)
+             for r in range(world)]
+    t0 = time.monotonic()
+    try:
+        survivors = [p for r, p in enumerate(procs) if r != victim]
+        for p in survivors:
+            p.wait(timeout=90)
+        elapsed = time.monotonic() - t0
+        logs = [p.stdout.read() for p in survivors]
+        for p, log in zip(survivors, logs):
+            assert p.returncode == 3, log
+            assert "PeerLostError" in log, log
+        assert elapsed < 60, elapsed  # setup (~imports) + detection, not an unbounded spin
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGKILL)
+                p.wait(timeout=30)
+    if mode == "kill":
+        assert procs[victim].returncode == -signal.SIGKILL
+    assert set(glob.glob("/dev/shm/llmctl-tp-*")) <= before

@@ -6,7 +6,11 @@ ablation (--exps: 0 full kernel, 1 no DMA pieces, 2 no barriers, 3 no fragment r
 garbage under 1-3), the median cycles of each phase slot (P0-P3), the item's loop and epilogue
 cycles and the ideal MFMA cycles of a phase (32 x v_mfma_f32_16x16x32_bf16 = 512).
 
-    python tools/gemm_stamps.py [--shapes o up] [--layouts fwd dgrad] [--exps 0 1 2 3]
+    LLMCTL_BUILD_DEFINES="LLMCTL_STAMP LLMCTL_STAMP_EXP=<n>" python -m llmctl.ops.build --force
+    python tools/gemm_stamps.py [--shapes o up] [--layouts fwd dgrad]
+
+The stamps and the ablations (EXP) exist only in a library built with those defines (one
+ablation per build); rebuild without them afterwards.
 """
 import argparse
 import json
