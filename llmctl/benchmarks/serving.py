@@ -68,7 +68,7 @@ def run_serving_benchmark(model: str = "gpt-7b", prompt_length: int = 2048, gen_
     ttft = np.array([s.first_token_time - s.arrival_time for s in seqs])
     tpot = np.array([(s.finish_time - s.first_token_time) / max(len(s.output_ids) - 1, 1) for s in seqs])
     out_tokens = sum(len(s.output_ids) for s in seqs)
-    return {
+    res = {
         "model": eng.cfg.name, "device": str(eng.device), "num_requests": num_requests,
         "prompt_length": prompt_length, "gen_length": gen_length, "qps": qps, "max_batch_size": max_batch_size, "scheduler": scheduler,
         "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""), "decode_weight_dtype": eng.weight_dtype,
@@ -82,6 +82,8 @@ def run_serving_benchmark(model: str = "gpt-7b", prompt_length: int = 2048, gen_
         "wall_s": round(wall, 3), "graph_replays": eng.stats["graph_replays"],
         "kv_blocks": eng.kv.num_blocks, "data": "synthetic prompts, random-init weights",
     }
+    eng.close()
+    return res
 
 
 def single_request_ttft(model: str = "gpt-7b", prompt_length: int = 2048, repeats: int = 5, device: str = "auto"
@@ -101,5 +103,7 @@ def single_request_ttft(model: str = "gpt-7b", prompt_length: int = 2048, repeat
             eng.step()
         if r > 0:
             ts.append(s.first_token_time - s.arrival_time)
-    return {"model": eng.cfg.name, "prompt_length": prompt_length, "ttft_p50_ms": round(float(np.median(ts)) * 1e3, 2),
+    name = eng.cfg.name
+    eng.close()
+    return {"model": name, "prompt_length": prompt_length, "ttft_p50_ms": round(float(np.median(ts)) * 1e3, 2),
             "ttft_min_ms": round(min(ts) * 1e3, 2)}

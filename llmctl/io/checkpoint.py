@@ -31,8 +31,12 @@ import time
 from pathlib import Path
 from typing import Any, Dict, List, Optional
 
+import logging
+
 import torch
 import torch.distributed as dist
+
+log = logging.getLogger("llmctl.io.checkpoint")
 
 # ----------------------------------------------------------------------------- TP (re)sharding
 # how each parameter is split across tensor-parallel ranks
@@ -134,12 +138,15 @@ class CheckpointManager:
         # mid-write, then an elastic restart that saves this step again) carry another id and are
         # never counted toward this save's commit
         save_id = f"{e.global_step}:{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}:{os.environ.get('TORCHELASTIC_RUN_ID', '')}"
+        # every rank writes into a sibling staging directory; rank 0's commit renames it over
+        # ``path`` once complete, so re-saving an existing name never leaves it half-overwritten
+        final_path = path
+        path = self.root / f".{name}.staging"
         if e.is_main:
+            # before the barrier, so no rank of this save has written into it yet: the leftovers of
+            # an interrupted save (stale shards, markers) must not survive into this one
+            shutil.rmtree(path, ignore_errors=True)
             path.mkdir(parents=True, exist_ok=True)
-            # before the barrier, so no rank of this save has written a marker yet: a stale
-            # marker set and a stale commit record must not survive into this save
-            shutil.rmtree(path / ".done", ignore_errors=True)
-            (path / "training_state.json").unlink(missing_ok=True)
         if dist.is_initialized():
             dist.barrier()
         path.mkdir(parents=True, exist_ok=True)
@@ -190,7 +197,7 @@ class CheckpointManager:
                 (path / ".done").mkdir(exist_ok=True)
                 (path / ".done" / f"rank_{rank:05d}").write_text(save_id)
                 if e.is_main:
-                    self._commit(path, state, n_shards, world, timeout, save_id)
+                    self._commit(path, state, n_shards, world, timeout, save_id, final_path)
             except BaseException as ex:  # surfaced by wait()
                 self._error = ex
 
@@ -200,10 +207,10 @@ class CheckpointManager:
         else:
             _write()
             self.wait()
-        return path
+        return final_path
 
     def _commit(self, path: Path, state: Dict[str, Any], n_shards: int, world: int, timeout: float,
-                save_id: str = "") -> None:
+                save_id: str = "", final_path: Optional[Path] = None) -> None:
         """Rank 0, off the training thread: once every rank's done-marker exists (each rank
         writes its marker after its own shards), write the metadata and move ``latest``.
 
@@ -246,6 +253,16 @@ class CheckpointManager:
         tmp.write_text(json.dumps(state, indent=2, default=str))
         os.replace(tmp, path / "training_state.json")
         shutil.rmtree(done, ignore_errors=True)
+        if final_path is not None and final_path != path:
+            # swap the complete staging directory in: the old copy (a re-save of this name) is
+            # renamed aside first and deleted only after the new one is in place
+            old = self.root / f".{final_path.name}.old"
+            shutil.rmtree(old, ignore_errors=True)
+            if final_path.exists():
+                os.replace(final_path, old)
+            os.replace(path, final_path)
+            shutil.rmtree(old, ignore_errors=True)
+            path = final_path
         lt = self.root / "latest.tmp"
         lt.write_text(path.name)
         os.replace(lt, self.root / "latest")
@@ -279,10 +296,14 @@ class CheckpointManager:
             if not (p / "training_state.json").exists():
                 # ``latest`` names a checkpoint whose re-save was interrupted (its commit record is
                 # removed before the rewrite): fall back to the newest complete one
-                done = [d for d in root.iterdir() if d.is_dir() and (d / "training_state.json").exists()]
+                done = [d for d in root.iterdir() if d.is_dir() and not d.name.startswith(".")
+                        and (d / "training_state.json").exists()]
                 if not done:
                     raise FileNotFoundError(f"{root}: no complete checkpoint")
+                skipped = p.name
                 p = max(done, key=lambda d: json.loads((d / "training_state.json").read_text()).get("global_step", -1))
+                log.warning("checkpoint: 'latest' names %s, which is incomplete (an interrupted save); "
+                            "resuming from %s instead", skipped, p.name)
         state = json.loads((p / "training_state.json").read_text())
         e.optimizer.wait_params()
         full = load_full_state_dict(p, e.model_config)

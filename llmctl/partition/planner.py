@@ -142,10 +142,17 @@ class HardwareModel:
     intra_bw_gbps: float = MI355X["xgmi_links"] * MI355X["xgmi_link_gbps"]  # per-GPU aggregate
     inter_bw_gbps: float = 50.0
     hbm_bw_gbps: float = 8000.0
-    # model-FLOP efficiency of forward+backward, calibrated on MI355X: GPT-7B mb=12 single GPU
-    # measured 28.1k tok/s (46 % MFU, profiles/bench_r2_gemm64_ab.jsonl) including the AdamW
-    # term below
-    gemm_efficiency: float = 0.465
+    # Per-op rates measured on MI355X (round 5 step kernel stats, GPT-7B mb 16 seq 2048, one GPU:
+    # profiles/bench_r5_kernel_stats_default.txt; profiles/planner_calibration_r6.txt):
+    #   projection GEMMs 1.51 PF at 32k tokens per GEMM (861 ms of GEMM kernels for 1.30 PFLOP),
+    #   flash attention forward 721 TF, backward 543 TF (model FLOPs = 2.5x the forward's; the
+    #   dK/dV + dQ kernels recompute S and dP), RMSNorm / SwiGLU / RoPE ~64 B per hidden element
+    #   per token per layer at 6.3 TB/s, fused AdamW 28 B per parameter at 6.0 TB/s.
+    gemm_efficiency: float = 0.604
+    attn_fwd_efficiency: float = 0.288
+    attn_bwd_efficiency: float = 0.217
+    elementwise_bytes_per_hidden: float = 64.0
+    hbm_efficiency: float = 0.79
     collective_efficiency: float = 0.6
 
     @classmethod
@@ -279,17 +286,27 @@ class ParallelismPlanner:
         shrinks from (pp-1)/M to (pp-1)/(vs*M) of the compute, the stage-boundary p2p volume
         grows vs-fold."""
         c = self.cfg
+        hw = self.hw
         tokens_per_rank = mb * self.seq_len * accum * pp  # pp: all micro-batches flow through every stage
-        flops_rank = c.flops_per_token(self.seq_len) * tokens_per_rank / (tp * pp)
+        S = self.seq_len
+        attn_fwd = 2 * 2 * c.layers * c.q_size * S / 2  # QK^T + PV per token, causal half
+        lin = c.flops_per_token(S) - 3 * attn_fwd       # 6 x (projection + LM-head) parameters
+        share = tokens_per_rank / (tp * pp)              # heads / features split over TP, layers over PP
+        # GEMM rate grows with the token count per GEMM (M dimension); calibrated at 32k tokens
+        T = mb * S / (tp if sp else 1)
+        eff = hw.gemm_efficiency * min((T / (T + 2048.0)) / (32768.0 / 34816.0), 1.02)
+        t_gemm = lin * share / (hw.peak_flops * eff)
+        t_attn_f = attn_fwd * share / (hw.peak_flops * hw.attn_fwd_efficiency)
+        t_attn_b = 2.5 * attn_fwd * share / (hw.peak_flops * hw.attn_bwd_efficiency)
         if ac == "full":
-            flops_rank *= 4 / 3
-        elif ac == "selective":
-            flops_rank *= 1.01
-        # GEMM efficiency grows with the token count per GEMM (M dimension): normalised so
-        # that 16k tokens/GEMM (measured GPT-7B mb=8) gets the calibrated efficiency
-        T = mb * self.seq_len / (tp if sp else 1)
-        eff = self.hw.gemm_efficiency * min((T / (T + 2048.0)) / (16384.0 / 18432.0), 1.05)
-        compute = flops_rank / (self.hw.peak_flops * eff)
+            t_gemm *= 4 / 3
+            t_attn_f *= 2
+        elif ac == "selective":  # the attention core and SwiGLU are recomputed in the backward
+            t_attn_f *= 2
+        elem_tokens = tokens_per_rank / ((tp if sp else 1) * pp)
+        t_elem = (hw.elementwise_bytes_per_hidden * c.hidden * c.layers * elem_tokens
+                  / (hw.hbm_bw_gbps * 1e9 * hw.hbm_efficiency))
+        compute = t_gemm + t_attn_f + t_attn_b + t_elem
         M = accum * pp if pp > 1 else accum
         vs = max(int(vs), 1) if pp > 1 else 1
         compute_total = compute * (1 + (pp - 1) / (vs * M)) if pp > 1 else compute
@@ -310,7 +327,9 @@ class ParallelismPlanner:
         dp_time = 2 * self._ring(grad_bytes, dp, dp_bw)
         if zs >= 3:
             dp_time *= 1.5  # params gathered in fwd and bwd
-        exposed_dp = max(dp_time - 0.8 * compute, 0.1 * dp_time)
+        # overlapped with the backward except the last bucket; the RCCL kernels share the CUs and
+        # HBM with the backward's (uncalibrated: no multi-GPU node measured, 15 % of their time)
+        exposed_dp = max(dp_time - 0.8 * compute, 0.1 * dp_time) + 0.15 * dp_time
         # MoE token all-to-all: dispatch + combine, forward and backward, per layer (exposed)
         ep_time = 0.0
         ep = self.expert_parallel(dp)
@@ -323,8 +342,8 @@ class ParallelismPlanner:
         opt_time = 28.0 * self._stage_params(tp, pp) / (self.hw.hbm_bw_gbps * 1e9 * 0.75)
         if zs >= 1:
             opt_time /= dp
-            if zs < 3:
-                dp_time += 0.1 * self._ring(grad_bytes, dp, dp_bw)
+            if zs < 3:  # the updated-parameter all-gather: the next forward's first buckets wait on it
+                exposed_dp += 0.25 * self._ring(grad_bytes, dp, dp_bw)
         total = compute_total + tp_time + pp_time + exposed_dp + ep_time + opt_time
         return dict(compute_s=compute_total, tp_s=tp_time, pp_s=pp_time, dp_s=dp_time, opt_s=opt_time, total_s=total,
                     comm_gb=(grad_bytes * 2 * (dp > 1) + (4 * act_bytes * c.layers if tp > 1 else 0)) / GiB)

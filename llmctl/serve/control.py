@@ -52,30 +52,51 @@ def _flatten(d: Dict[str, Any], prefix: str, out: List[Tuple[str, Any]]) -> None
             out.append((key, v))
 
 
-# decode steps (the per-token hot path) have a fixed layout: [magic, n, mb] then ids / positions /
-# slots / ctx as int64 rows and the [n, mb] int32 block table -- one conversion, one copy
+# decode steps (the per-token hot path) have a fixed layout: [magic, n, mb, stamp] then ids /
+# positions / slots / ctx as int64 rows and the [n, mb] int32 block table -- one conversion, one
+# copy.  Sampling decode steps (``decode_s``: the TP async pipeline) add [cont] to the head and the
+# uniforms, temperatures, top-k and top-p rows (fp32 / int32) after the block table.
 _DECODE_MAGIC = 0x0DEC0DE1
+_DECODE_S_MAGIC = 0x0DEC0DE2
 _DECODE_KEYS = {"op", "ids", "positions", "slots", "ctx", "bt"}
 _DECODE_KEYS_STAMPED = _DECODE_KEYS | {"stamp"}  # + a float timestamp (tools/tp_control_bench.py)
+_DECODE_S_KEYS = _DECODE_KEYS | {"cont", "u", "temp", "topk", "topp"}
 
 
 def _pack_decode(plan: Dict[str, Any]) -> bytes:
     bt = np.ascontiguousarray(plan["bt"], dtype=np.int32)
-    n = len(plan["ids"])
-    head = np.empty(4 + 4 * n, dtype=np.int64)
-    head[0], head[1], head[2] = _DECODE_MAGIC, n, bt.shape[1] if bt.ndim == 2 else 0
+    n = len(plan["positions"])
+    samp = plan["op"] == "decode_s"
+    head = np.empty(5 + 4 * n, dtype=np.int64)
+    head[0], head[1], head[2] = _DECODE_S_MAGIC if samp else _DECODE_MAGIC, n, bt.shape[1] if bt.ndim == 2 else 0
     head[3:4].view(np.float64)[0] = plan.get("stamp", float("nan"))
+    head[4] = int(plan.get("cont", 0))
     for i, k in enumerate(("ids", "positions", "slots", "ctx")):
-        head[4 + i * n: 4 + (i + 1) * n] = plan[k]
-    return head.tobytes() + bt.tobytes()
+        head[5 + i * n: 5 + (i + 1) * n] = plan[k]
+    parts = [head.tobytes(), bt.tobytes()]
+    if samp:
+        parts += [np.ascontiguousarray(plan["u"], dtype=np.float32).tobytes(),
+                  np.ascontiguousarray(plan["temp"], dtype=np.float32).tobytes(),
+                  np.ascontiguousarray(plan["topk"], dtype=np.int32).tobytes(),
+                  np.ascontiguousarray(plan["topp"], dtype=np.float32).tobytes()]
+    return b"".join(parts)
 
 
 def _unpack_decode(buf) -> Dict[str, Any]:
-    a = np.frombuffer(buf, dtype=np.int64, count=4)
+    a = np.frombuffer(buf, dtype=np.int64, count=5)
+    samp = int(a[0]) == _DECODE_S_MAGIC
     n, mb = int(a[1]), int(a[2])
-    rows = np.frombuffer(buf, dtype=np.int64, count=4 * n, offset=32).reshape(4, n).copy()
-    bt = np.frombuffer(buf, dtype=np.int32, count=n * mb, offset=32 + 32 * n).reshape(n, mb).copy()
-    out = {"op": "decode", "ids": rows[0], "positions": rows[1], "slots": rows[2], "ctx": rows[3], "bt": bt}
+    rows = np.frombuffer(buf, dtype=np.int64, count=4 * n, offset=40).reshape(4, n).copy()
+    off = 40 + 32 * n
+    bt = np.frombuffer(buf, dtype=np.int32, count=n * mb, offset=off).reshape(n, mb).copy()
+    off += 4 * n * mb
+    out = {"op": "decode_s" if samp else "decode", "ids": rows[0], "positions": rows[1], "slots": rows[2],
+           "ctx": rows[3], "bt": bt}
+    if samp:
+        out["cont"] = bool(a[4])
+        for k, dt in (("u", np.float32), ("temp", np.float32), ("topk", np.int32), ("topp", np.float32)):
+            out[k] = np.frombuffer(buf, dtype=dt, count=n, offset=off).copy()
+            off += 4 * n
     stamp = float(a[3:4].view(np.float64)[0])
     if stamp == stamp:
         out["stamp"] = stamp
@@ -86,7 +107,9 @@ def pack(plan: Dict[str, Any]) -> bytes:
     """Plan dict -> bytes.  Values: None, bool, int, float, str, list of ints (round-trips as a
     list), numpy arrays (int / bool / float dtypes, any shape), nested dicts.  Decode plans use a
     fixed layout (their lists come back as int64 arrays)."""
-    if plan.get("op") == "decode" and (plan.keys() == _DECODE_KEYS or plan.keys() == _DECODE_KEYS_STAMPED):
+    op = plan.get("op")
+    if ((op == "decode" and (plan.keys() == _DECODE_KEYS or plan.keys() == _DECODE_KEYS_STAMPED))
+            or (op == "decode_s" and plan.keys() - {"stamp"} == _DECODE_S_KEYS)):
         return _pack_decode(plan)
     items: List[Tuple[str, Any]] = []
     _flatten(plan, "", items)
@@ -120,7 +143,7 @@ def pack(plan: Dict[str, Any]) -> bytes:
 def unpack(buf) -> Dict[str, Any]:
     """bytes / uint8 view -> plan dict (arrays are copies, safe after the slot is reused)."""
     mv = memoryview(buf)
-    if len(mv) >= 24 and struct.unpack_from("<q", mv, 0)[0] == _DECODE_MAGIC:
+    if len(mv) >= 40 and struct.unpack_from("<q", mv, 0)[0] in (_DECODE_MAGIC, _DECODE_S_MAGIC):
         return _unpack_decode(mv)
     (n,) = struct.unpack_from("<I", mv, 0)
     off = 4

@@ -401,21 +401,28 @@ class InferenceEngine:
             d = {}
             for name in self._W8_NAMES:
                 w = getattr(layer, name, None)
-                if w is None or w.dim() != 2 or w.shape[0] % 64:
+                # only weights the fused fp8 kernels take (ops.decode_fused_ok: out % 64, in % 128)
+                if w is None or w.dim() != 2 or w.shape[0] % 64 or w.shape[1] % 128:
                     continue
                 qd = quantize_fp8(w.detach())
                 d[name] = (qd["qweight"].contiguous(), qd["scale"].float().contiguous())
             out.append(d)
         hw = self.model.head_weight()
-        if hw.dim() == 2 and hw.shape[0] % 64 == 0:  # the (local shard of the) vocabulary projection
+        if hw.dim() == 2 and hw.shape[0] % 64 == 0 and hw.shape[1] % 128 == 0:  # the (local shard of the) LM head
             qd = quantize_fp8(hw.detach())
             self._w8_head = (qd["qweight"].contiguous(), qd["scale"].float().contiguous())
         return out
 
-    def _dw(self, li: int, layer, name: str):
-        """(weight, row scales or None) the fused decode path streams for ``layer.name``."""
-        if self._w8 is not None and name in self._w8[li]:
-            return self._w8[li][name]
+    W8_MAX_ROWS = 16  # the fused fp8 decode kernels take at most 16 token rows (ops.decode_fused_ok)
+
+    def _dw(self, li: int, layer, name: str, n: int):
+        """(weight, row scales or None) the fused decode path streams for ``layer.name`` at ``n``
+        token rows: the fp8 copy only where the fused fp8 kernel takes it, else the bf16 weight
+        (which is kept) -- never a per-step dequantised fp32 image of the fp8 one."""
+        if self._w8 is not None and 1 <= n <= self.W8_MAX_ROWS and name in self._w8[li]:
+            q = self._w8[li][name]
+            if name not in ("wo", "w_down") or q[0].shape[0] <= 16384:  # add+RMSNorm finalize limit
+                return q
         return getattr(layer, name), None
 
     def _decode_body_fused(self, ids, positions, slots, block_tables, ctx_lens) -> torch.Tensor:
@@ -429,9 +436,10 @@ class InferenceEngine:
         def lin(x, w, s):  # a plain decode projection (TP row-parallel partial): bf16 or fp8 weights
             return ops.decode_linear(x, w) if s is None else ops.decode_linear_fp8(x, w, s)
 
+        n = ids.shape[0]
         for li, layer in enumerate(layers):
-            (wqkv, sqkv), (wo, so) = self._dw(li, layer, "wqkv"), self._dw(li, layer, "wo")
-            (wu, su), (wd, sd) = self._dw(li, layer, "w_up"), self._dw(li, layer, "w_down")
+            (wqkv, sqkv), (wo, so) = self._dw(li, layer, "wqkv", n), self._dw(li, layer, "wo", n)
+            (wu, su), (wd, sd) = self._dw(li, layer, "w_up", n), self._dw(li, layer, "w_down", n)
             o = ops.decode_attention_qkv(xn, wqkv, layer.bqkv, self.rope[0], self.rope[1], layer.nq,
                                          layer.nkv, positions, kc[li], vc[li], slots, block_tables, ctx_lens,
                                          w_scale=sqkv)
@@ -447,7 +455,7 @@ class InferenceEngine:
                 xn, res = self._reduce_add_rmsnorm(lin(act, wd, sd), layer.b_down, res, nw, eps)
             else:
                 xn, res = ops.decode_linear_add_rmsnorm(act, wd, layer.b_down, res, nw, eps, w_scale=sd)
-        if self._w8_head is not None:
+        if self._w8_head is not None and n <= self.W8_MAX_ROWS:
             return self._gather_vocab(ops.decode_linear_fp8(xn, *self._w8_head))
         return self._gather_vocab(ops.decode_linear(xn, m.head_weight()))
 
@@ -519,6 +527,34 @@ class InferenceEngine:
             g.reset()
         self._graphs.clear()
 
+    def close(self) -> None:
+        """Deterministic teardown, never left to garbage collection: drop an in-flight pipelined
+        step, release the captured decode graphs (their memory pool and any captured collectives),
+        drain the device and drop the KV cache / weights this engine holds.  Idempotent; the engine
+        is unusable afterwards.  Also the ``with InferenceEngine(...) as e:`` exit."""
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        self._release_resources()
+
+    def _release_resources(self) -> None:
+        self._pending = None
+        self._last_toks = None
+        self.release_graphs()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.kv_cache = None
+        self._w8 = self._w8_head = None
+        self.rope = None
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
     def decode_plan(self, seqs: List[Sequence]) -> Dict:
         return {"op": "decode", "ids": [s.last_id for s in seqs], "positions": [s.num_tokens - 1 for s in seqs],
                 "slots": [s._decode_slot for s in seqs], "ctx": [self.kv.num_tokens(s.seq_id) for s in seqs],
@@ -535,18 +571,21 @@ class InferenceEngine:
         n = len(ids)
         self.stats["decode_tokens"] += n
         if self.use_graphs:
-            g, b = self._stage_and_replay(plan, None, cont=False)
+            g, b = self._stage_and_replay(plan, cont=False)
             return b["logits"][:n]
         d = self.device
         return self._decode_body(torch.tensor(ids, device=d), torch.tensor(positions, dtype=torch.int32, device=d),
                                  torch.tensor(slots, device=d), torch.from_numpy(bt).to(d),
                                  torch.tensor(ctx, dtype=torch.int32, device=d))
 
-    def _stage_and_replay(self, plan: Dict, seqs: Optional[List[Sequence]], cont: bool):
+    def _stage_and_replay(self, plan: Dict, cont: bool):
         """Fill one host staging set with the step's inputs, copy them (asynchronously) into the
         graph's static buffers and replay it.  ``cont``: the input ids are already on the device
         (the previous replay of this graph sampled them), only positions / slots / block tables /
-        context lengths / uniforms are copied.  ``seqs``: rows whose sampling parameters to load."""
+        context lengths / uniforms are copied.  A sampling plan (``decode_s``) carries its uniforms
+        ``u`` and per-row ``temp`` / ``topk`` / ``topp``; a logits-only plan draws nothing (the
+        in-graph sampling result is unused then, and the host RNG stream stays the one every
+        engine configuration consumes: one uniform per sampled row)."""
         n = len(plan["positions"])
         nb = self._bucket(n)
         if nb not in self._graphs:
@@ -563,18 +602,18 @@ class InferenceEngine:
         hn["block_tables"][:n] = plan["bt"]
         hn["ctx_lens"][:] = 1
         hn["ctx_lens"][:n] = plan["ctx"]
-        hn["u"][:n] = plan["u"] if "u" in plan else self._np_rng.random(n, dtype=np.float32)
-        if seqs is not None:
-            key = tuple((s.params.temperature, s.params.top_k if s.params.top_k and s.params.top_k > 0 else 0,
-                         s.params.top_p) for s in seqs)
+        hn["u"][:n] = plan["u"] if "u" in plan else 0.0
+        if "temp" in plan:
+            key = (np.asarray(plan["temp"], dtype=np.float32).tobytes(), np.asarray(plan["topk"], dtype=np.int32).tobytes(),
+                   np.asarray(plan["topp"], dtype=np.float32).tobytes())
             if b["params_key"] != key:
                 d = self.device
                 b["temp"].zero_()
                 b["topk"].zero_()
                 b["topp"].fill_(1.0)
-                b["temp"][:n].copy_(torch.tensor([k[0] for k in key], dtype=torch.float32, device=d))
-                b["topk"][:n].copy_(torch.tensor([k[1] for k in key], dtype=torch.int32, device=d))
-                b["topp"][:n].copy_(torch.tensor([k[2] for k in key], dtype=torch.float32, device=d))
+                b["temp"][:n].copy_(torch.from_numpy(np.frombuffer(key[0], dtype=np.float32).copy()).to(d))
+                b["topk"][:n].copy_(torch.from_numpy(np.frombuffer(key[1], dtype=np.int32).copy()).to(d))
+                b["topp"][:n].copy_(torch.from_numpy(np.frombuffer(key[2], dtype=np.float32).copy()).to(d))
                 b["params_key"] = key
         for k in self._STAGED:
             if cont and k == "ids":
@@ -585,32 +624,73 @@ class InferenceEngine:
         return g, b
 
     # ------------------------------------------------------------------ asynchronous decode
+    @staticmethod
+    def _sampling_fields(seqs: List[Sequence]) -> Dict[str, np.ndarray]:
+        return {"temp": np.asarray([s.params.temperature for s in seqs], dtype=np.float32),
+                "topk": np.asarray([s.params.top_k if s.params.top_k and s.params.top_k > 0 else 0 for s in seqs],
+                                   dtype=np.int32),
+                "topp": np.asarray([s.params.top_p for s in seqs], dtype=np.float32)}
+
+    def _publish(self, plan: Dict) -> Dict:
+        """TP hook: rank 0's plan to the other ranks (identity at TP = 1)."""
+        return plan
+
     @torch.inference_mode()
     def _launch_decode(self, seqs: List[Sequence], plan: Dict, cont: bool) -> Dict:
         """Run a decode step with sampling (the graph replay, or the eager layer stack) and queue
         the D2H copy of its tokens; the tokens are read by :meth:`_finalize`.  ``cont``: the
-        input ids are the previous step's sampled tokens, already on the device."""
-        self.stats["decode_tokens"] += len(seqs)
+        input ids are the previous step's sampled tokens, already on the device.
+
+        TP > 1: the plan -- with the step's uniforms and sampling parameters -- goes to every rank
+        first; every rank runs the same step and the same in-graph sampling on the same gathered
+        logits and uniforms, so all ranks hold identical sampled ids on the device without a
+        broadcast of the tokens, and a continued step (``cont``) feeds them back as its input on
+        every rank.  Only rank 0 reads the tokens back."""
         n = len(seqs)
+        self.stats["decode_tokens"] += n
+        plan = dict(plan, op="decode_s", cont=bool(cont), u=self._np_rng.random(n, dtype=np.float32),
+                    **self._sampling_fields(seqs))
+        if cont:
+            plan.setdefault("ids", np.zeros(n, dtype=np.int64))
+        toks = self._decode_sample_exec(self._publish(plan))
+        d = self.device
         if self.use_graphs:
-            g, b = self._stage_and_replay(plan, seqs, cont)
+            b = self._graphs[self._bucket(n)][1]
             out = b["host_toks"][b["tflip"]]
             b["tflip"] ^= 1
-            out.copy_(b["toks"], non_blocking=True)
+            out.copy_(toks, non_blocking=True)
         else:
-            d = self.device
-            ids = self._last_toks if cont else torch.tensor(plan["ids"], device=d)
-            logits = self._decode_body(ids, torch.tensor(plan["positions"], dtype=torch.int32, device=d),
-                                       torch.tensor(plan["slots"], device=d), torch.from_numpy(np.asarray(plan["bt"])).to(d),
-                                       torch.tensor(plan["ctx"], dtype=torch.int32, device=d))
-            toks = self._sample_rows(logits, seqs)
-            self._last_toks = toks
             out = toks.to("cpu", non_blocking=True) if d.type == "cuda" else toks
         ev = None
-        if self.device.type == "cuda":
+        if d.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
         return {"seqs": list(seqs), "host": out, "event": ev, "n": n}
+
+    @torch.inference_mode()
+    def _decode_sample_exec(self, plan: Dict) -> torch.Tensor:
+        """Every rank's half of :meth:`_launch_decode`: the decode step + sampling of a
+        ``decode_s`` plan; returns the device tensor of sampled ids (graph: the static ``toks``
+        buffer, all bucket rows)."""
+        use_knobs(self.knobs)
+        cont = bool(plan["cont"])
+        if self.use_graphs:
+            _, b = self._stage_and_replay(plan, cont)
+            return b["toks"]
+        d = self.device
+        n = len(plan["positions"])
+        ids = self._last_toks if cont else torch.as_tensor(np.asarray(plan["ids"], dtype=np.int64)).to(d)
+        logits = self._decode_body(ids, torch.as_tensor(np.asarray(plan["positions"], dtype=np.int32)).to(d),
+                                   torch.as_tensor(np.asarray(plan["slots"], dtype=np.int64)).to(d),
+                                   torch.from_numpy(np.asarray(plan["bt"])).to(d),
+                                   torch.as_tensor(np.asarray(plan["ctx"], dtype=np.int32)).to(d))
+        temp = torch.from_numpy(np.asarray(plan["temp"], dtype=np.float32)).to(d)
+        topk = torch.from_numpy(np.asarray(plan["topk"], dtype=np.int32)).to(d)
+        topp = torch.from_numpy(np.asarray(plan["topp"], dtype=np.float32)).to(d)
+        u = torch.from_numpy(np.asarray(plan["u"], dtype=np.float32)).to(d)
+        toks = ops.sample(logits[:n].contiguous(), temp, topk, topp, u)
+        self._last_toks = toks
+        return toks
 
     def _finalize(self, p: Dict) -> int:
         """Read an in-flight step's tokens (the one host sync of the pipeline) and append them."""
@@ -654,7 +734,7 @@ class InferenceEngine:
         return self._launch_decode(seqs, plan, cont=True)
 
     def _async_ok(self) -> bool:
-        return self.knobs.async_decode and self.tp == 1
+        return self.knobs.async_decode
 
     # ------------------------------------------------------------------ sampling
     def sample(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[int]:
@@ -738,7 +818,7 @@ class InferenceEngine:
                 produced += 1
             self.stats["steps"] += 1
             return produced
-        if out.decode and not out.prefill and self.tp == 1 and "sample" not in self.__dict__:
+        if out.decode and not out.prefill and "sample" not in self.__dict__:
             # sampling in the decode step (inside the graph); asynchronous: tokens read next call.
             # (an instance-level ``sample`` override -- teacher forcing, logit capture -- keeps
             # the host-sampling path below)

@@ -98,6 +98,9 @@ class InferenceServer:
         @app.on_event("shutdown")
         async def _shutdown():
             self.stop_engine()
+            if getattr(self, "_own_engine", False) and self.engine is not None:
+                self.engine.close()
+                self.engine = None
 
         @app.post("/v1/completions")
         async def completions(req: GenerationRequest):
@@ -140,6 +143,7 @@ class InferenceServer:
             from .engine import InferenceEngine
 
             self.engine = InferenceEngine(**self.engine_kwargs)
+            self._own_engine = True  # closed by this server's shutdown (a passed-in engine is the caller's)
         if self._thread is None:
             self._stop = False
             self._thread = threading.Thread(target=self._engine_loop, name="llmctl-engine", daemon=True)

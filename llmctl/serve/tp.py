@@ -163,6 +163,17 @@ class TPInferenceEngine(InferenceEngine):
 
     CAR_CHECK_EVERY = 64  # decode steps between reads of the custom all-reduce's error word (one D2H copy)
 
+    def _publish(self, plan: Dict) -> Dict:
+        return self._bcast(plan)
+
+    @torch.inference_mode()
+    def _decode_sample_exec(self, plan: Dict) -> torch.Tensor:
+        toks = super()._decode_sample_exec(plan)
+        self._car_checks += 1
+        if self.car is not None and self._car_checks % self.CAR_CHECK_EVERY == 0:
+            self.car.check()
+        return toks
+
     @torch.inference_mode()
     def mixed(self, chunks, seqs: List[Sequence]) -> torch.Tensor:
         return self.mixed_exec(self._bcast(self.mixed_plan(chunks, seqs)))
@@ -200,6 +211,7 @@ class TPInferenceEngine(InferenceEngine):
         if self._own_control and self.control is not None:
             dist.destroy_process_group(self.control)
         self.control = None
+        self._release_resources()
         if err is not None:
             raise err
 
@@ -214,6 +226,8 @@ class TPInferenceEngine(InferenceEngine):
                 return
             if op == "prefill":
                 self.prefill_exec(plan)
+            elif op == "decode_s":  # async pipeline: decode + in-graph sampling, ids stay on the device
+                self._decode_sample_exec(plan)
             elif op == "decode":
                 self.decode_exec(plan)
             elif op == "mixed":

@@ -158,10 +158,11 @@ def serve_generate(rank: int, world: int, max_tokens: int = 8, model: str = "tin
     logits = eng.prefill(probe).float().cpu()
     for s in probe:
         eng.kv.free_sequence(s.seq_id)
+    kv_heads_local = eng.kv_cache.k.shape[-2]
     if world > 1:
         eng.stop_workers()
         eng.close()
-    return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": eng.kv_cache.k.shape[-2],
+    return {"tokens": [s.output_ids for s in seqs], "kv_heads_local": kv_heads_local,
             "prefill_logits": logits}
 
 
@@ -571,3 +572,124 @@ def control_channel_worker(rank, world, kind, slot_bytes=8 << 20):
             assert p["x"] == 1.5 and p["flag"] is True and (p["doc"] is None) == bool(it % 2)
     ch.close()
     return {"digest": torch.stack(digests), "spilled": torch.tensor(getattr(ch, "stats", {}).get("spilled", 0))}
+
+
+def serve_sampled(rank: int, world: int, async_decode: bool = True, temperature: float = 0.9,
+                  max_tokens: int = 8) -> dict:
+    """Seeded sampled generation (temperature > 0, top-k / top-p) through the serving engine at
+    TP = world (gloo) or world 1; rank 0 returns the tokens, how many decode steps ran pipelined
+    (step N + 1 launched from step N's device-side ids) and the engine's host-RNG draw count (one
+    uniform per sampled row, whatever the TP degree or pipelining)."""
+    import os
+
+    import torch.distributed as dist
+
+    from llmctl.serve.scheduler import SamplingParams
+
+    kw = dict(device="cpu", max_batch_size=4, num_kv_blocks=48, block_size=8, max_model_len=256,
+              max_batch_tokens=512, seed=3, perf_knobs={"async_decode": async_decode}, prefix_caching=False)
+    if world == 1:
+        from llmctl.serve.engine import InferenceEngine
+
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            os.environ.pop(k, None)
+        eng = InferenceEngine("tiny", **kw)
+    else:
+        from llmctl.serve.tp import TPInferenceEngine
+
+        dist.init_process_group("gloo")
+        eng = TPInferenceEngine("tiny", **kw)
+        if eng.tp_rank != 0:
+            eng.worker_loop()
+            eng.close()
+            return {}
+    p = SamplingParams(max_tokens=max_tokens, temperature=temperature, top_k=40, top_p=0.95, ignore_eos=True)
+    seqs = eng.generate(PROMPTS, p)
+    res = {"tokens": [s.output_ids for s in seqs], "continued": eng.stats.get("async_continued", 0),
+           "rng_next": float(eng._np_rng.random())}
+    if world > 1:
+        eng.stop_workers()
+        eng.close()
+    return res
+
+
+def serve_async_gpu(rank: int, world: int, model: str = "tiny", env=None, engine_kw=None, prompts=None,
+                    max_tokens: int = 16) -> dict:
+    """TP = world serving on cuda:0 (world processes sharing the GPU: gloo default group, custom
+    IPC all-reduces, decode hipGraphs with in-graph sampling), greedy, with the pipelined decode
+    loop on and then off on the same engine.  Rank 0 returns both runs' tokens, the pipelined
+    steps, and per decode step of the pipelined run: host wall ms (``step()`` loop) and device ms
+    (CUDA events around each decode launch on rank 0's stream; with the pipeline full the next
+    launch's start event fires when the previous replay ends, so the sum is the busy time)."""
+    import dataclasses
+    import os
+    import time
+
+    import torch.distributed as dist
+
+    from llmctl.serve.scheduler import SamplingParams
+
+    os.environ.update(env or {})
+    torch.cuda.set_device(0)
+    kw = dict(device="cuda", max_batch_size=4, num_kv_blocks=64, block_size=16, max_model_len=256,
+              max_batch_tokens=512, seed=0, use_graphs=True, prefix_caching=False)
+    kw.update(engine_kw or {})
+    prompts = prompts or PROMPTS
+    if world == 1:
+        from llmctl.serve.engine import InferenceEngine
+
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            os.environ.pop(k, None)
+        eng = InferenceEngine(model, **kw)
+    else:
+        from llmctl.serve.tp import TPInferenceEngine
+
+        dist.init_process_group("gloo")
+        eng = TPInferenceEngine(model, **kw)
+        if eng.tp_rank != 0:
+            eng.worker_loop()
+            eng.close()
+            return {}
+    p = SamplingParams(max_tokens=max_tokens, temperature=0.0, ignore_eos=True)
+    base = eng.knobs
+    res = {}
+    inner = eng._decode_sample_exec
+    evs = []
+
+    def timed(plan):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = inner(plan)
+        b.record()
+        evs.append((a, b))
+        return out
+
+    for mode in (True, False):
+        eng.knobs = dataclasses.replace(base, async_decode=mode)
+        c0 = eng.stats.get("async_continued", 0)
+        seqs = [eng.add_request(list(pr), p) for pr in prompts]
+        while any(s.first_token_time is None for s in seqs):  # prefills (+ first tokens)
+            eng.step()
+        torch.cuda.synchronize()
+        start = [len(s.output_ids) for s in seqs]
+        evs.clear()
+        eng._decode_sample_exec = timed
+        t0 = time.perf_counter()
+        while any(s.status != "finished" for s in seqs):
+            eng.step()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
+        eng._decode_sample_exec = inner
+        steps = max(len(s.output_ids) - s0 for s, s0 in zip(seqs, start))
+        gpu = sum(a.elapsed_time(b) for a, b in evs)
+        res[f"tokens_{int(mode)}"] = [s.output_ids for s in seqs]
+        res[f"continued_{int(mode)}"] = eng.stats.get("async_continued", 0) - c0
+        res[f"host_ms_{int(mode)}"] = wall / max(steps, 1)
+        res[f"gpu_ms_{int(mode)}"] = gpu / max(len(evs), 1)
+    res["graph_replays"] = eng.stats["graph_replays"]
+    if world > 1:
+        eng.stop_workers()
+        eng.close()
+    else:
+        eng.release_graphs()
+    return res

@@ -437,3 +437,68 @@ def test_engine_fp8_kv_cache_cpu():
     assert [o[0] for o in outs["fp8"]] == [o[0] for o in outs["auto"]]
     with pytest.raises(ValueError):
         InferenceEngine("tiny", device="cpu", kv_cache_dtype="int4")
+
+
+@pytest.mark.parametrize("temp", [0.0, 0.9])
+def test_tp_async_decode_matches_tp1(temp):
+    """TP = 2 (gloo) with the pipelined decode loop: every rank samples in the decode step from the
+    same gathered logits and the uniforms rank 0 publishes with the plan, and a continued step
+    feeds the device-side ids back on every rank.  Tokens equal the TP = 2 synchronous loop and the
+    TP = 1 engine, greedy and seeded-sampled, and the host RNG advanced by the same number of draws
+    (no second draw per step on the TP path)."""
+    from llmctl.testing.harness import run_ranks
+    from llmctl.testing.workers import serve_sampled
+
+    one = run_ranks(serve_sampled, 1, True, temp)[0]
+    tp_async = run_ranks(serve_sampled, 2, True, temp)[0]
+    tp_sync = run_ranks(serve_sampled, 2, False, temp)[0]
+    assert tp_async["continued"] >= 3 and tp_sync["continued"] == 0
+    assert tp_async["tokens"] == tp_sync["tokens"] == one["tokens"]
+    assert tp_async["rng_next"] == tp_sync["rng_next"] == one["rng_next"]
+
+
+@pytest.mark.parametrize("async_decode", [True, False])
+def test_async_decode_early_stop_with_prefix_cache(async_decode):
+    """Sequences that stop on EOS (or a stop string) while a speculative step N + 1 for them is in
+    flight, with prefix caching on: outputs and finish reasons equal the synchronous loop, and
+    every KV block comes back (free, or held only by the prefix cache)."""
+    from llmctl.serve.scheduler import SamplingParams
+
+    prompts = [[1, 2, 3, 4, 5, 6, 7, 8, 9], [9] * 11, [1, 2, 3, 4, 5, 6, 7, 8, 9, 10], [3] * 17]
+    mk = lambda a: InferenceEngine("tiny", device="cpu", max_batch_size=4, num_kv_blocks=64, block_size=4,
+                                   max_model_len=128, seed=5, perf_knobs={"async_decode": a}, prefix_caching=True)
+    probe = mk(False)
+    free = [s.output_ids for s in probe.generate(prompts, SamplingParams(max_tokens=12, temperature=0.0,
+                                                                          ignore_eos=True))]
+    # a token some sequence first produces mid-stream: that row (and any other hitting it) stops there
+    si, pos = next((i, j) for i, o in enumerate(free) for j in range(2, len(o)) if o[j] not in o[:j])
+    eos = free[si][pos]
+    outs = {}
+    for a in (async_decode, False):
+        e = mk(a)
+        e.tokenizer.eos_token_id = eos
+        seqs = e.generate(prompts, SamplingParams(max_tokens=12, temperature=0.0))
+        stop = e.add_request([2, 2, 2, 2, 2], SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True,
+                                                             stop=[e.tokenizer.decode(free[0][2:3])]))
+        while stop.status != "finished":
+            e.step()
+        outs[a] = ([s.output_ids for s in seqs], [s.finish_reason for s in seqs], stop.output_ids,
+                   stop.finish_reason)
+        assert e.kv.num_free_blocks + e.prefix_cache.num_evictable() == 64
+        e.prefix_cache.clear()
+        assert e.kv.num_free_blocks == 64
+    assert outs[async_decode] == outs[False]
+    assert outs[False][1][si] == "stop" and len(outs[False][0][si]) == pos + 1
+
+
+def test_engine_close_is_deterministic_and_idempotent():
+    """``close()`` (and the context-manager exit) drops the pipelined step, the graphs, the KV
+    cache and the fp8 copies without waiting for garbage collection; a second close is a no-op."""
+    from llmctl.serve.scheduler import SamplingParams
+
+    with InferenceEngine("tiny", device="cpu", max_batch_size=2, num_kv_blocks=16, block_size=8,
+                         max_model_len=64) as e:
+        e.generate([[1, 2, 3]], SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
+        assert e.kv_cache is not None
+    assert e.kv_cache is None and e._pending is None and not e._graphs
+    e.close()

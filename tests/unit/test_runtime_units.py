@@ -422,3 +422,39 @@ def test_checkpoint_commit_ignores_stale_done_markers(tmp_path):
     (ck / ".done" / "rank_00001").write_text("stale")
     with pytest.raises(TimeoutError):
         mgr._commit(ck, st, 1, 2, 0.2, "this-save")
+
+
+def test_checkpoint_resave_is_staged_and_swapped(tmp_path, caplog):
+    """Re-saving an existing checkpoint name writes a sibling staging directory and renames it over
+    the target only once complete: an interrupted re-save (a staging directory left behind) never
+    touches the committed copy, the next save clears it, and a ``latest`` that names an incomplete
+    checkpoint is skipped with a warning."""
+    import logging
+
+    from llmctl.io.checkpoint import CheckpointManager
+    from llmctl.runtime.engine import TrainingEngine
+    from llmctl.testing.workers import _config
+
+    eng = TrainingEngine(_config(output_dir=str(tmp_path)))
+    g = torch.Generator().manual_seed(0)
+    batch = [(torch.randint(1, 500, (2, 32), generator=g), torch.randint(1, 500, (2, 32), generator=g))]
+    eng.train_step(batch)
+    mgr = CheckpointManager(eng, str(tmp_path))
+    ck = mgr.save("checkpoint-1", final=True)
+    assert ck == tmp_path / "checkpoint-1" and (ck / "training_state.json").exists()
+    # an interrupted re-save: its staging directory holds partial shards, the committed copy is intact
+    st = tmp_path / ".checkpoint-1.staging"
+    st.mkdir()
+    (st / "model.safetensors").write_bytes(b"partial")
+    assert json.loads((ck / "training_state.json").read_text())["global_step"] == 1
+    eng.train_step(batch)
+    mgr.save("checkpoint-1", final=True)  # the re-save proper
+    assert json.loads((ck / "training_state.json").read_text())["global_step"] == 2
+    assert not st.exists() and not (tmp_path / ".checkpoint-1.old").exists()
+    # ``latest`` naming an incomplete checkpoint: fall back to the newest complete one, with a warning
+    (tmp_path / "checkpoint-9").mkdir()
+    (tmp_path / "latest").write_text("checkpoint-9")
+    eng2 = TrainingEngine(_config(output_dir=str(tmp_path)))
+    with caplog.at_level(logging.WARNING, logger="llmctl.io.checkpoint"):
+        CheckpointManager(eng2, str(tmp_path)).load(str(tmp_path))
+    assert eng2.global_step == 2 and "incomplete" in caplog.text

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--layouts", nargs="+", default=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--knob", action="append", default=[], help="native knob name=value (repeatable)")
+    ap.add_argument("--knob-sets", nargs="+", default=[],
+                    help="extra cases per config: 'name=value,name=value' native knob sets, timed interleaved "
+                         "with the base case (e.g. gemm_stagger=400)")
     a = ap.parse_args()
     assert _lib.load(), _lib._error
     print("tuned hipBLASLt solutions:", enable_tuned_gemms(), flush=True)
@@ -73,11 +76,29 @@ def main():
             want = ref().float()
             r = {"shape": name, "layout": lay, "tokens": T}
             cases = {"hipblaslt": ref}
+            base = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.knob}
+
+            def with_knobs(ks, c):
+                def f():
+                    for k, v in ks.items():
+                        ops.set_knob(k, v)
+                    run(c)
+                    for k in ks:
+                        ops.set_knob(k, base.get(k, 0))
+                return f
+
             for c in a.configs:
                 run(c)
                 torch.cuda.synchronize()
                 r[f"err{c}"] = round(row_err(res, want), 5)
                 cases[f"g{c}"] = lambda c=c: run(c)
+                for ksv in a.knob_sets:
+                    ks = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in ksv.split(",")}
+                    f = with_knobs(ks, c)
+                    f()
+                    torch.cuda.synchronize()
+                    r[f"err{c}[{ksv}]"] = round(row_err(res, want), 5)
+                    cases[f"g{c}[{ksv}]"] = f
             times = {k: [] for k in cases}
             for _ in range(a.rounds):
                 for k, f in cases.items():
