@@ -42,12 +42,11 @@ def test_gemm64_ex(native_lib, M, N, K, at, bt, acc, split, variant):
 
 
 @pytest.mark.parametrize("config", [4, 8, 104, 108, 1104, 2104, 4008, 8104, 904, 908, 1904, 2904, 8904,
-                                    304, 308, 1304, 2304, 8304, 504, 508, 1504, 2504, 8504])
+                                    304, 308, 1304, 2304, 8304])
 def test_gemm64_configs(native_lib, config):
     """Every tile-order group / schedule variant / tail split computes the same product (fwd
     and wgrad); 1xxx = no split, Sxxx = S K-ranges (24 tiles < one round: all of them split).
-    x0xx-x2xx: 8-wave kernel, x3xx: persistent 4-wave, x5xx: 2-phase persistent 4-wave, x4xx /
-    x6xx-x9xx: one-shot 4-wave."""
+    x0xx-x2xx: 8-wave kernel, x3xx: persistent 4-wave, x4xx-x9xx: one-shot 4-wave."""
     M, N, K = 1536, 1024, 2048  # 24 tiles: more tiles than one group, several K-tile pairs
     A, B = _bf(M, K, seed=3), _bf(N, K, seed=4)
     want = A.float() @ B.float().t()
@@ -66,7 +65,7 @@ def test_gemm64_split_tail_multi_round(native_lib):
     A, B = _bf(K, M, seed=91), _bf(K, N, seed=92)
     c0 = _bf(M, N, seed=93)
     want = A.float().t() @ B.float()
-    for cfg in (104, 8104, 904, 8904, 304, 1304, 8304, 504, 1504, 8504):
+    for cfg in (104, 8104, 904, 8904, 304, 1304, 8304):
         # x1xx: 8-wave; x3xx: 4-wave persistent; x9xx: 4-wave
         out = c0.clone()
         native_lib.gemm64_ex(A, B, out, True, True, True, cfg)
@@ -90,7 +89,7 @@ def test_gemm64_persistent_many_rounds(native_lib, at, bt, rounds):
     a = A.t().contiguous() if at else A
     b = B.t().contiguous() if bt else B
     want = A.float() @ B.float().t()
-    for cfg in (304, 1304, 308, 504, 1504, 508):
+    for cfg in (304, 1304, 308):
         out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
         native_lib.gemm64_ex(a, b, out, at, bt, False, cfg)
         assert torch.isfinite(out.float()).all(), cfg
@@ -181,7 +180,7 @@ def test_swiglu_down_autograd_fused_matches_unfused(native_lib):
         assert row_err(gu.grad, g32.grad) < 2e-2 and row_err(w.grad, w32.grad) < 2e-2
 
 
-@pytest.mark.parametrize("cfg", [104, 2104, 904, 2904, 1904, 304, 1304, 2304, 504, 1504, 2504])
+@pytest.mark.parametrize("cfg", [104, 2104, 904, 2904, 1904, 304, 1304, 2304])
 def test_gemm64_wgrad_fp32_output(native_lib, cfg):
     """fp32 main gradients: the wgrad layout stores / accumulates an fp32 C (no bf16 rounding of
     the running sum); one-shot and persistent schedules, with and without the split tail."""
