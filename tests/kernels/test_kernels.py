@@ -819,6 +819,14 @@ def test_decode_fused_ops_fp8_weights(native_lib):
     q2 = native_lib.decode_qkv_rope_cache(x, wd.to(torch.bfloat16), None, cos, sin, nq, nkv, pos, kc2, vc2, slots)
     errs = (_row_err(q, q2.float()), _row_err(kc, kc2.float()), _row_err(vc, vc2.float()))
     assert max(errs) < 2e-2, errs
+    # and against the fp32 oracle: x @ dequant(w)^T in fp32, RoPE in fp32 (ops.ref), the K / V rows
+    # at their cache slots
+    qo, ko, vo = ref.rope_qkv_fwd(x.float() @ wd.t(), cos, sin, nq, nkv, 256, pos)
+    qo, ko, vo = qo.float(), ko.float(), vo.float()
+    kflat, vflat = kc.view(nb * bs, nkv, D), vc.view(nb * bs, nkv, D)
+    errs = (_row_err(q.reshape(M, -1), qo.reshape(M, -1)), _row_err(kflat[slots].reshape(M, -1), ko.reshape(M, -1)),
+            _row_err(vflat[slots].reshape(M, -1), vo.reshape(M, -1)))
+    assert max(errs) < 2e-2, errs
     # up + SwiGLU
     F = 1024
     w8, sc, wd = _w8(2 * F, K, 113)
