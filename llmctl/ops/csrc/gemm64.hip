@@ -844,6 +844,14 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
   constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;
   const int g = lane >> 4, i16 = lane & 15;
   if constexpr (EPI == EPI_ROPE_QKV) {
+    if (sp >= 0) {  // a split tail item: fp32 partials; gemm64_split_reduce applies the RoPE epilogue
+      float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 128 + 4 * g;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + 16 * j) = acc[i][j];
+      return;
+    }
     // a 256-column tile = 2 heads of D = 128: wave wc owns head 2 tn + wc whole; n-tile j (< 4)
     // holds dims d = 16 j + 4 g + r, n-tile j + 4 the rotation partners d + 64
     const int h = 2 * tn + wc;
@@ -1567,6 +1575,56 @@ __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
       v[4 + j] += x1[j];
     }
   }
+  if constexpr (EPI == EPI_ROPE_QKV) {
+    // the main epilogue's RoPE / head split: a thread of the first half of a head (d < 64) also sums
+    // its rotation partners d + 64 and writes both halves
+    const int hh = col >> 7, d = col & 127;
+    if (d >= 64) return;
+    float w2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < args.splits; ++sp) {
+      const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(W + 64 + (long)sp * (TM * TN));
+      const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(W + 64 + (long)sp * (TM * TN) + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w2[j] += x0[j];
+        w2[4 + j] += x1[j];
+      }
+    }
+    const int h = 2 * tn + hh, nrot = args.nq + args.nkv;
+    unsigned short* dst0;
+    long dst_ld;
+    if (h < args.nq) {
+      dst0 = args.c + (long)h * 128;
+      dst_ld = (long)args.nq * 128;
+    } else if (h < nrot) {
+      dst0 = args.out2 + (long)(h - args.nq) * 128;
+      dst_ld = (long)args.nkv * 128;
+    } else {
+      dst0 = args.out3 + (long)(h - nrot) * 128;
+      dst_ld = (long)args.nkv * 128;
+    }
+    const long t = (long)tm * TM + row;
+    float o1[8], o2[8];
+    if (h < nrot) {  // as rope_fwd_kernel on the bf16-stored projection
+      const long p = args.pos ? (long)args.pos[t] : (long)(t % args.seq);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = bf2f(f2bf(v[j])), b = bf2f(f2bf(w2[j]));
+        const float cs = args.cosT[p * 64 + d + j], sn = args.sinT[p * 64 + d + j];
+        o1[j] = a * cs - b * sn;
+        o2[j] = b * cs + a * sn;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o1[j] = v[j];
+        o2[j] = w2[j];
+      }
+    }
+    store8(dst0 + t * dst_ld + d, o1);
+    store8(dst0 + t * dst_ld + 64 + d, o2);
+    return;
+  }
   if constexpr (epi_f32(EPI)) {
     f32x4_t* pf = reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(args.c) + (long)(tm * TM + row) * args.ldc + tn * TN + col);
     f32x4_t lo = {v[0], v[1], v[2], v[3]}, hi = {v[4], v[5], v[6], v[7]};
@@ -1927,7 +1985,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm64_qkv_rope(const at::Tensor&
   g.nq = (int)nq;
   g.nkv = (int)nkv;
   g.seq = (int)std::max<int64_t>(seq, 1);
-  plan_split(g, 1);  // whole tiles (the epilogue needs the full K sum)
+  // tail split (config / 1000, as gemm64_ex) on the 4-wave kernels, whose split items store fp32
+  // partials that gemm64_split_reduce rotates; the 8-wave kernel takes whole tiles only
+  plan_split(g, (config / 100) % 10 >= 3 ? (int)(config / 1000) : 1);
+  at::Tensor ws;
+  if (g.splits > 1) {
+    ws = at::empty({(long)(g.tiles_m * g.tiles_n - g.n_main) * g.splits * TM * TN}, x.options().dtype(at::kFloat));
+    g.ws = ws.data_ptr<float>();
+  }
   launch<false, false, EPI_ROPE_QKV>(g, (int)(config % 1000));
   return {q, k, v};
 }

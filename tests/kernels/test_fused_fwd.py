@@ -46,6 +46,24 @@ def test_gemm64_qkv_rope_matches_fp32(native_lib, T, K, nq, nkv, with_pos, confi
         assert row_err(got.reshape(T, -1), want.reshape(T, -1)) < 8e-3
 
 
+@pytest.mark.parametrize("T,K,nq,nkv", [(2048, 4096, 32, 32), (512, 1024, 8, 4)])
+def test_gemm64_qkv_rope_tail_split(native_lib, T, K, nq, nkv):
+    """Prefill-sized QKV + RoPE with the tail split (partial last round cut into K-ranges, the
+    RoPE / head split applied by gemm64_split_reduce) == the same GEMM on whole tiles (config
+    1304) up to the order of the split sums, and == the fp32 oracle."""
+    D = 128
+    x = _bf(T, K, seed=11)
+    w = _bf((nq + 2 * nkv) * D, K, seed=12, scale=K ** -0.5)
+    cos, sin = ref.rope_tables(4096, D, device=DEV)
+    pos = torch.randint(0, 4096, (T,), device=DEV, dtype=torch.int32)
+    q, k, v = native_lib.gemm64_qkv_rope(x, w, cos, sin, pos, nq, nkv, T, 304)
+    q1, k1, v1 = native_lib.gemm64_qkv_rope(x, w, cos, sin, pos, nq, nkv, T, 1304)
+    rq, rk, rv = ref.rope_qkv_fwd(x.float() @ w.float().t(), cos, sin, nq, nkv, T, pos)
+    for got, whole, want in ((q, q1, rq), (k, k1, rk), (v, v1, rv)):
+        assert row_err(got.reshape(T, -1), whole.reshape(T, -1).float()) < 8e-3  # one bf16 ulp
+        assert row_err(got.reshape(T, -1), want.reshape(T, -1)) < TOL
+
+
 @pytest.mark.parametrize("T,K,F", [(256, 256, 128), (512, 384, 384), (1024, 512, 1024)])
 @pytest.mark.parametrize("config", [104, 304, 904])
 def test_gemm64_up_swiglu_matches_fp32(native_lib, T, K, F, config):

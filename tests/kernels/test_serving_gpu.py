@@ -343,13 +343,15 @@ def test_fresh_prefill_flash_attention_matches_paged(native_lib, monkeypatch):
         assert e.kv.add_sequence_shared(s.seq_id, s.num_tokens, [])
     plan = e.prefill_plan([PrefillChunk(s, 0, s.num_tokens) for s in seqs])
     assert plan["doc"] is not None
-    from llmctl.config.knobs import configure
+    import dataclasses
 
-    configure({"prefill_fa": True})
+    base = e.knobs  # the engine routes by its own knobs (prefill_exec re-activates them)
+    e.knobs = dataclasses.replace(base, prefill_fa=True)
     la = e.prefill_exec(plan).float()
     kc_a = [t.clone() for t in e.kv_cache.k]
-    configure({"prefill_fa": False})
+    e.knobs = dataclasses.replace(base, prefill_fa=False)
     lb = e.prefill_exec(plan).float()
+    e.knobs = base
     assert la.shape == lb.shape == (4, e.cfg.vocab_size)
     assert (la - lb).norm() / lb.norm() < 1e-2
     assert torch.equal(kc_a[0], e.kv_cache.k[0])  # layer 0: the same RoPE'd K rows written

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Single-request TTFT A/B (GPT-7B, 2048-token prompt): one engine, native knob sets timed in
-interleaved rounds (same process, same box: CDNA guide §5.4 rule 24); p50 / min TTFT per set.
+"""Single-request TTFT A/B (GPT-7B, 2048-token prompt): one engine, knob sets timed in interleaved
+rounds (same process, same box: CDNA guide §5.4 rule 24); p50 / min TTFT per set.  A knob that is
+a PerfKnobs field is set on the engine's own knobs, any other name is a native knob.
 
     python tools/ttft_ab.py --knob-sets gemm_fused_split=0 gemm_fused_split=1 [--rounds 5 --repeats 4]
 """
@@ -36,10 +37,17 @@ def main():
     eng.generate([[1] * 32], p)
     times = {i: [] for i in range(len(sets))}
     n = 0
+    import dataclasses
+
+    base = eng.knobs
     for rnd in range(a.rounds + 1):
         for i, ks in enumerate(sets):
+            eng.knobs = base
             for k, v in ks.items():
-                ops.set_knob(k, v)
+                if hasattr(base, k):
+                    eng.knobs = dataclasses.replace(eng.knobs, **{k: type(getattr(base, k))(v)})
+                else:
+                    ops.set_knob(k, v)
             for _ in range(a.repeats):
                 n += 1
                 s = eng.add_request([(7 * j + n) % V for j in range(a.prompt_length)], p)
