@@ -307,9 +307,9 @@ def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
     assert fus["fused_decode"] and not ref["fused_decode"]
     err = row_err(_logit_rows(fus), _logit_rows(ref))
     assert err < 2e-2, err
-    # one decode step from identical cache state: fused vs unfused logits (the engine re-activates
-    # its own knobs on every step, so the unfused body runs under an explicit override)
-    from llmctl.config.knobs import override
+    # one decode step from identical cache state: fused vs unfused logits (the engine routes by its
+    # own knobs, so the unfused body runs with them switched)
+    import dataclasses
     for pr in prompts:
         ef.add_request(pr, SamplingParams(max_tokens=4, temperature=0.0))
     while ef.scheduler.waiting or any(s.first_token_time is None for s in ef.scheduler.running):
@@ -322,8 +322,11 @@ def test_fused_decode_layer_matches_unfused(native_lib, monkeypatch):
         args = (torch.tensor(plan["ids"], device=d), torch.tensor(plan["positions"], dtype=torch.int32, device=d),
                 torch.tensor(plan["slots"], device=d), torch.from_numpy(plan["bt"]).to(d),
                 torch.tensor(plan["ctx"], dtype=torch.int32, device=d))
-        with override(decode_fused=False):
-            lu = ef._decode_body(*args).float()
+        base = ef.knobs
+        ef.knobs = dataclasses.replace(base, decode_fused=False)
+        assert not ef._fused_decode()
+        lu = ef._decode_body(*args).float()
+        ef.knobs = base
         lf = ef._decode_body_fused(*args).float()
     assert torch.isfinite(lf).all() and (lf - lu).norm() / lu.norm() < 2e-2
 
