@@ -132,7 +132,8 @@ def pack(plan: Dict[str, Any]) -> bytes:
             parts += [_HDR.pack(len(kb), _KIND_STR, 0, 0), kb, struct.pack("<q", len(sb)), sb]
         else:
             kind = _KIND_ARRAY if isinstance(v, np.ndarray) else _KIND_LIST
-            a = np.ascontiguousarray(v if kind == _KIND_ARRAY else np.asarray(v, dtype=np.int64))
+            a = v if kind == _KIND_ARRAY else np.asarray(v, dtype=np.int64)
+            a = np.ascontiguousarray(a).reshape(a.shape)  # (ascontiguousarray alone turns 0-d into 1-d)
             if a.dtype not in _DT_CODE:
                 raise TypeError(f"plan field {key!r}: unsupported dtype {a.dtype}")
             parts += [_HDR.pack(len(kb), kind, _DT_CODE[a.dtype], a.ndim), kb,

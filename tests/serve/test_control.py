@@ -79,3 +79,59 @@ def test_shm_channel_peer_loss(victim, mode):
     if mode == "kill":
         assert procs[victim].returncode == -signal.SIGKILL
     assert set(glob.glob("/dev/shm/llmctl-tp-*")) <= before
+
+
+def test_pack_roundtrip_property():
+    """Property test (hypothesis): any plan of the supported value kinds -- None / bool / int /
+    float / str / int lists / numpy arrays of any shape and int / bool / float dtype / nested
+    dicts, plus the fixed-layout decode and sampling-decode records -- survives pack -> unpack."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    from hypothesis.extra import numpy as hnp
+
+    dtypes = st.sampled_from([np.int32, np.int64, np.float32, np.float64, np.bool_, np.uint8])
+    arrays = dtypes.flatmap(lambda dt: hnp.arrays(dt, hnp.array_shapes(min_dims=0, max_dims=3, max_side=5)))
+    leaves = st.one_of(st.none(), st.booleans(), st.integers(-2**62, 2**62), st.floats(allow_nan=False),
+                       st.text(max_size=12), st.lists(st.integers(-2**31, 2**31), max_size=6), arrays)
+    keys = st.text(alphabet="abcdefghij_", min_size=1, max_size=6)
+    plans = st.recursive(st.dictionaries(keys, leaves, max_size=5),
+                         lambda inner: st.dictionaries(keys, st.one_of(leaves, inner), max_size=4), max_leaves=12)
+
+    def same(a, b):
+        if isinstance(a, dict):
+            return isinstance(b, dict) and a.keys() == b.keys() and all(same(a[k], b[k]) for k in a)
+        if isinstance(a, np.ndarray):
+            return (isinstance(b, np.ndarray) and a.dtype == b.dtype and a.shape == b.shape
+                    and np.ascontiguousarray(a).tobytes() == b.tobytes())  # bitwise (NaN payloads too)
+        if isinstance(a, list):
+            return list(b) == a
+        return type(a) is type(b) and a == b
+
+    @settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+    @given(plans)
+    def generic(plan):
+        plan = dict(plan, op="prefill")
+        assert same(plan, unpack(pack(plan)))
+
+    @settings(max_examples=60, deadline=None)
+    @given(st.integers(1, 17), st.integers(1, 9), st.booleans(), st.booleans())
+    def decode(n, mb, sampling, cont):
+        rng = np.random.default_rng(n * 31 + mb)
+        plan = {"op": "decode_s" if sampling else "decode", "ids": rng.integers(0, 32000, n).tolist(),
+                "positions": rng.integers(0, 4096, n).tolist(), "slots": rng.integers(-1, 1 << 20, n).tolist(),
+                "ctx": rng.integers(1, 4096, n).tolist(), "bt": rng.integers(0, 999, (n, mb)).astype(np.int32)}
+        if sampling:
+            plan.update(cont=cont, u=rng.random(n, dtype=np.float32), temp=rng.random(n, dtype=np.float32),
+                        topk=rng.integers(0, 50, n).astype(np.int32), topp=rng.random(n, dtype=np.float32))
+        got = unpack(pack(plan))
+        assert got["op"] == plan["op"]
+        for k in ("ids", "positions", "slots", "ctx"):
+            assert np.array_equal(got[k], np.asarray(plan[k]))
+        assert np.array_equal(got["bt"], plan["bt"])
+        if sampling:
+            assert got["cont"] == cont
+            for k in ("u", "temp", "topk", "topp"):
+                assert np.array_equal(got[k], plan[k])
+
+    generic()
+    decode()
