@@ -102,7 +102,7 @@ class KVManager {
   bool add_sequence(int64_t seq, int64_t tokens) {
     if (tables_.count(seq)) throw std::runtime_error("sequence already registered");
     auto blocks = alloc_.allocate_n(blocks_needed(std::max<int64_t>(tokens, 1)));
-    if (blocks.empty() && tokens > 0) return false;
+    if (blocks.empty()) return false;  // (a 0-token sequence reserves one block too)
     tables_[seq] = {std::move(blocks), tokens};
     return true;
   }
@@ -152,6 +152,7 @@ class KVManager {
 
   // share all full blocks of `src` with a new sequence `dst` (copy-on-write prefix sharing)
   void fork(int64_t src, int64_t dst) {
+    if (tables_.count(dst)) throw std::runtime_error("sequence already registered");
     auto& s = get(src);
     Table t;
     t.tokens = s.tokens;

@@ -38,7 +38,12 @@ class PyKVManager:
         self.ref[b] = 1
         return b
 
+    def _new(self, seq: int) -> None:
+        if seq in self.tables:
+            raise RuntimeError("sequence already registered")
+
     def add_sequence(self, seq: int, tokens: int) -> bool:
+        self._new(seq)
         n = self.blocks_needed(max(tokens, 1))
         if n > len(self.free_list):
             return False
@@ -47,6 +52,7 @@ class PyKVManager:
         return True
 
     def add_sequence_shared(self, seq: int, tokens: int, prefix: List[int]) -> bool:
+        self._new(seq)
         need = self.blocks_needed(max(tokens, 1))
         if len(prefix) > need:
             raise ValueError("prefix longer than the sequence")
@@ -90,6 +96,7 @@ class PyKVManager:
         return self.tables[seq][pos // self.bs] * self.bs + pos % self.bs
 
     def fork(self, src: int, dst: int) -> None:
+        self._new(dst)
         for b in self.tables[src]:
             self.ref[b] += 1
         self.tables[dst] = list(self.tables[src])

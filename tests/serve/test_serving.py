@@ -502,3 +502,106 @@ def test_engine_close_is_deterministic_and_idempotent():
         assert e.kv_cache is not None
     assert e.kv_cache is None and e._pending is None and not e._graphs
     e.close()
+
+
+def test_kv_manager_native_matches_python_model():
+    """Model-based property test (hypothesis state machine): the native C++ KVManager and the
+    Python PyKVManager, driven by the same random operation sequence (add / add with a shared
+    prefix / append / fork / free / external prefix-cache references, OOM included), return the
+    same results and hold the same block tables, token counts, slots and reference counts; every
+    block's count equals its table occurrences plus the external references."""
+    from hypothesis import settings
+    from hypothesis import strategies as st
+    from hypothesis.stateful import RuleBasedStateMachine, initialize, invariant, precondition, rule
+
+    native = make_kv_manager(1, 1)
+    if isinstance(native, PyKVManager):
+        pytest.skip("native runtime not built")
+
+    class Machine(RuleBasedStateMachine):
+        @initialize(nb=st.integers(1, 24), bs=st.sampled_from([1, 2, 4, 16]))
+        def setup(self, nb, bs):
+            self.n, self.p = make_kv_manager(nb, bs), PyKVManager(nb, bs)
+            self.nb, self.bs, self.next_id, self.ext = nb, bs, 0, []
+
+        def _both(self, name, *args):
+            outs = []
+            for m in (self.n, self.p):
+                try:
+                    outs.append(("ok", getattr(m, name)(*args)))
+                except Exception as e:  # the same failure on both sides
+                    outs.append(("err", type(e).__name__ in ("RuntimeError", "ValueError", "IndexError")))
+            assert outs[0] == outs[1] or (outs[0][0] == outs[1][0] == "err"), (name, args, outs)
+            return outs[0]
+
+        @property
+        def seqs(self):
+            return sorted(self.p.tables)
+
+        @rule(tokens=st.integers(0, 40))
+        def add(self, tokens):
+            self._both("add_sequence", self.next_id, tokens)
+            self.next_id += 1
+
+        @precondition(lambda self: self.p.tables)
+        @rule(data=st.data(), tokens=st.integers(1, 40))
+        def add_shared(self, data, tokens):
+            src = data.draw(st.sampled_from(self.seqs))
+            full = self.p.num_tokens(src) // self.bs
+            k = data.draw(st.integers(0, min(full, self.p.blocks_needed(tokens))))
+            self._both("add_sequence_shared", self.next_id, tokens, self.p.block_table(src)[:k])
+            self.next_id += 1
+
+        @precondition(lambda self: self.p.tables)
+        @rule(data=st.data())
+        def append(self, data):
+            self._both("append_token", data.draw(st.sampled_from(self.seqs)))
+
+        @precondition(lambda self: self.p.tables)
+        @rule(data=st.data())
+        def fork(self, data):
+            self._both("fork", data.draw(st.sampled_from(self.seqs)), self.next_id)
+            self.next_id += 1
+
+        @precondition(lambda self: self.p.tables)
+        @rule(data=st.data())
+        def free(self, data):
+            self._both("free_sequence", data.draw(st.sampled_from(self.seqs)))
+
+        @precondition(lambda self: any(self.p.tables.values()))
+        @rule(data=st.data())
+        def cache_ref(self, data):  # the prefix cache takes a reference on a live block
+            s = data.draw(st.sampled_from([s for s in self.seqs if self.p.tables[s]]))
+            b = data.draw(st.sampled_from(self.p.block_table(s)))
+            self._both("incref_block", b)
+            self.ext.append(b)
+
+        @precondition(lambda self: self.ext)
+        @rule(data=st.data())
+        def cache_release(self, data):
+            b = self.ext.pop(data.draw(st.integers(0, len(self.ext) - 1)))
+            self._both("decref_block", b)
+
+        @invariant()
+        def same_state(self):
+            if not hasattr(self, "p"):
+                return
+            assert self.n.num_free_blocks == self.p.num_free_blocks
+            assert self.n.num_sequences == self.p.num_sequences
+            occ = [0] * self.nb
+            for s in self.seqs:
+                t = self.p.block_table(s)
+                assert list(self.n.block_table(s)) == t and self.n.num_tokens(s) == self.p.num_tokens(s)
+                for b in t:
+                    occ[b] += 1
+                if t:
+                    n_slots = min(self.p.num_tokens(s), len(t) * self.bs)
+                    assert list(self.n.slots(s, 0, n_slots)) == list(self.p.slots(s, 0, n_slots))
+            for b in self.ext:
+                occ[b] += 1
+            for b in range(self.nb):
+                assert self.n.refcount(b) == self.p.refcount(b) == occ[b], (b, occ[b])
+            assert self.p.num_free_blocks == occ.count(0)
+
+    Machine.TestCase.settings = settings(max_examples=120, stateful_step_count=40, deadline=None)
+    Machine.TestCase().runTest()
