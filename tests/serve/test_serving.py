@@ -605,3 +605,71 @@ def test_kv_manager_native_matches_python_model():
 
     Machine.TestCase.settings = settings(max_examples=120, stateful_step_count=40, deadline=None)
     Machine.TestCase().runTest()
+
+
+def test_scheduler_simulation_property():
+    """Property test (hypothesis): the continuous-batching scheduler driven by a fake engine
+    (the engine's synchronous step: decode rows then prefill chunks, ``computed`` then token
+    append, finish at max_tokens) over random request mixes -- shared prompt prefixes, every
+    policy, tight KV pools that force preemption, small token budgets, prefix cache on / off.
+    Every step respects the token budget and batch size, every chunk continues exactly where its
+    sequence stopped and addresses reserved KV slots, every request finishes with its max_tokens,
+    the run makes progress (no livelock), and at the end every KV block is free or held only by
+    the prefix cache with consistent reference counts."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    from llmctl.serve.prefix_cache import PrefixCache
+    from llmctl.serve.scheduler import ContinuousBatchScheduler, SamplingParams, Sequence
+
+    requests = st.lists(st.tuples(st.integers(0, 3), st.integers(1, 40), st.integers(1, 12)), min_size=1, max_size=9)
+
+    @settings(max_examples=120, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+    @given(requests, st.sampled_from(["dynamic", "prefill_first", "static"]), st.sampled_from([1, 4, 16]),
+           st.integers(1, 6), st.integers(8, 96), st.booleans(), st.booleans())
+    def run(reqs, policy, bs, max_bs, budget, use_pc, native):
+        max_len = 64
+        nb = (max_len + 2 * bs) // bs + 3  # any single sequence fits: preemption always makes progress
+        kv = make_kv_manager(nb, bs, prefer_native=native)
+        pc = PrefixCache(kv, bs) if use_pc else None
+        sched = ContinuousBatchScheduler(kv, max_bs, budget, max_len, policy, bs, pc)
+        bases = [[(7 * j + 3 * k) % 50 + 1 for k in range(40)] for j in range(4)]
+        seqs = []
+        for base, n, mt in reqs:
+            s = Sequence(prompt_ids=bases[base][:n], params=SamplingParams(max_tokens=mt, ignore_eos=True))
+            sched.add(s)
+            seqs.append(s)
+        idle = steps = 0
+        while sched.has_work():
+            out = sched.schedule()
+            steps += 1
+            assert steps < 2000
+            assert sum(c.count for c in out.prefill) + len(out.decode) <= budget
+            assert len(out.decode) <= max_bs and len(sched.running) <= max_bs
+            idle = idle + 1 if not (out.prefill or out.decode) else 0
+            assert idle < 3, "scheduler made no progress"
+            for seq in out.decode:
+                assert seq.num_computed == seq.num_tokens - 1 and seq.kv_len == seq.num_tokens
+                assert seq._decode_slot == kv.slot(seq.seq_id, seq.num_tokens - 1)
+            for c in out.prefill:
+                assert c.start == c.seq.num_computed and c.count > 0
+                assert c.start + c.count <= c.seq.kv_len == c.seq.num_tokens
+                kv.slots(c.seq.seq_id, c.start, c.count)  # reserved positions (raises otherwise)
+            for seq in out.decode:
+                sched.computed(seq, 1)
+            for c in out.prefill:
+                sched.computed(c.seq, c.count)
+            for seq in list(out.decode) + [c.seq for c in out.prefill if c.final]:
+                seq.output_ids.append((seq.seq_id * 31 + len(seq.output_ids)) % 50 + 1)
+                if len(seq.output_ids) >= seq.params.max_tokens or seq.num_tokens >= max_len:
+                    sched.finish(seq, "length")
+        for s in seqs:
+            assert s.status == "finished"
+            assert len(s.output_ids) == min(s.params.max_tokens, max_len - len(s.prompt_ids)), s
+        held = set(pc._owner) if pc is not None else set()
+        assert kv.num_free_blocks == nb - len(held)
+        assert kv.num_sequences == 0
+        for b in range(nb):
+            assert kv.refcount(b) == (1 if b in held else 0)
+
+    run()
