@@ -391,7 +391,7 @@ class ParallelismPlanner:
                     global_batch_size=gbs, grad_accum=accum, num_microbatches=M,
                     virtual_stages=vs if pp > 1 else 1,
                     estimated_memory_gb=round(mem, 3), estimated_comm_gb=round(t["comm_gb"], 3),
-                    estimated_flops=self.estimate_flops(gbs), estimated_step_time_s=round(t["total_s"], 4),
+                    estimated_flops=self.estimate_flops(gbs), estimated_step_time_s=float(f"{t['total_s']:.5g}"),
                     estimated_tokens_per_sec=round(tps, 1),
                     estimated_mfu=round(tps * self.cfg.flops_per_token(self.seq_len) /
                                         (self.hw.peak_flops * self.hw.gpus), 4))
@@ -421,9 +421,8 @@ class ParallelismPlanner:
         if best is None:
             # nothing fits: most-sharded configuration, flagged by the memory estimate
             n = self.hw.gpus
-            tp = min(8, n, self.hw.gpus_per_node)
-            while tp > 1 and (self.cfg.heads % tp or self.cfg.kv_heads % tp):
-                tp //= 2
+            tp = max(t for t in (1, 2, 4, 8) if t <= min(n, self.hw.gpus_per_node) and n % t == 0
+                     and self.cfg.heads % t == 0 and self.cfg.kv_heads % t == 0)  # every GPU used: tp | n
             best = self.evaluate(tp, 1, n // tp, 3 if n // tp > 1 else 0, tp > 1, "full", 1, global_batch)
         return best
 

@@ -145,3 +145,39 @@ def test_planner_virtual_stages_shrink_the_bubble():
     assert sm["virtual_stages"] == 2 and len(sm["stages"]) == 8
     r0 = [r for r in sm["ranks"] if r["pp_rank"] == 0][0]
     assert r0["layers"] == [sm["stages"][0], sm["stages"][4]]
+
+
+def test_planner_plan_properties():
+    """Property test (hypothesis) of the MI355X planner over model templates, node sizes (including
+    non-powers of two), sequence lengths and fixed micro-batches: the chosen layout uses every GPU
+    exactly (tp x pp x dp = gpus), divides the heads / KV heads, never has more stages than layers,
+    fits the HBM budget whenever any layout does, and reports finite positive estimates."""
+    import dataclasses
+    import math
+
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from llmctl.partition.planner import HardwareModel
+
+    models = st.sampled_from(["gpt-7b", "llama-13b", "llama-70b", "tiny", "tiny-wide", "gpt2"])
+
+    @settings(max_examples=60, deadline=None)
+    @given(models, st.sampled_from([1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64]), st.sampled_from([512, 2048, 8192, 32768]),
+           st.sampled_from([None, 1, 4, 16]))
+    def check(name, gpus, seq, mb):
+        cfg = get_model_config(name)
+        pl = ParallelismPlanner(dataclasses.asdict(cfg), {}, seq, hw=HardwareModel(gpus=gpus))
+        plan = pl.search_optimal_plan(fixed={"mb": mb} if mb else None)
+        tp, pp, dp = plan["tensor_parallel"], plan["pipeline_parallel"], plan["data_parallel"]
+        assert tp * pp * dp == gpus, plan
+        assert cfg.heads % tp == 0 and cfg.kv_heads % tp == 0
+        assert 1 <= pp <= cfg.layers
+        for k in ("estimated_tokens_per_sec", "estimated_step_time_s", "estimated_memory_gb"):
+            assert math.isfinite(plan[k]) and plan[k] > 0, (k, plan)
+        feasible = any(pl.evaluate(**c)["estimated_memory_gb"] <= 0.9 * pl.hw.hbm_gb
+                       for c in pl.candidates((mb,) if mb else (1, 2, 4, 8, 16)))
+        if feasible:
+            assert plan["estimated_memory_gb"] <= 0.9 * pl.hw.hbm_gb, plan
+
+    check()
