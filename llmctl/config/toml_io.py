@@ -66,8 +66,27 @@ def load_any(path) -> Dict[str, Any]:
 _BARE = re.compile(r"^[A-Za-z0-9_-]+$")
 
 
+_ESC = {'"': '\\"', "\\": "\\\\", "\b": "\\b", "\t": "\\t", "\n": "\\n", "\f": "\\f", "\r": "\\r"}
+
+
+def _basic_str(s: str) -> str:
+    """A TOML basic string: every character literal (UTF-8) except the quote, the backslash and
+    the control characters, which are escaped (JSON's encoder would emit surrogate-pair escapes
+    for astral characters and leave U+007F raw, both invalid TOML)."""
+    out = []
+    for ch in s:
+        e = _ESC.get(ch)
+        if e is not None:
+            out.append(e)
+        elif ord(ch) < 0x20 or ord(ch) == 0x7F:
+            out.append(f"\\u{ord(ch):04x}")
+        else:
+            out.append(ch)
+    return '"' + "".join(out) + '"'
+
+
 def _key(k: str) -> str:
-    return k if _BARE.match(k) else json.dumps(k)
+    return k if _BARE.match(k) else _basic_str(k)
 
 
 def _scalar(v: Any) -> str:
@@ -88,14 +107,14 @@ def _scalar(v: Any) -> str:
             return f"{m}e{int(e)}"
         return r
     if isinstance(v, str):
-        return json.dumps(v, ensure_ascii=False)
+        return _basic_str(v)
     if isinstance(v, (_dt.datetime, _dt.date)):
         return v.isoformat()
     if isinstance(v, (list, tuple)):
         return "[" + ", ".join(_scalar(x) for x in v if x is not None) + "]"
     if isinstance(v, dict):
         return "{ " + ", ".join(f"{_key(k)} = {_scalar(x)}" for k, x in v.items() if x is not None) + " }"
-    return json.dumps(str(v))
+    return _basic_str(str(v))
 
 
 def _is_table_list(v: Any) -> bool:

@@ -181,3 +181,48 @@ def test_planner_plan_properties():
             assert plan["estimated_memory_gb"] <= 0.9 * pl.hw.hbm_gb, plan
 
     check()
+
+
+def test_toml_writer_roundtrip_property():
+    """Property test (hypothesis): the own TOML emitter round-trips through tomli for nested
+    tables of the value kinds the schemas use -- arbitrary unicode keys and strings (quotes,
+    backslashes, control characters, newlines), ints, finite / infinite floats, bools, lists of
+    scalars, lists of tables; None values are omitted."""
+    import math
+
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    keys = st.text(min_size=1, max_size=8)
+    scal = st.one_of(st.integers(-2**63, 2**63 - 1), st.booleans(), st.text(max_size=12),
+                     st.floats(allow_nan=False))
+    lists = st.lists(st.integers(-10**6, 10**6), max_size=4) | st.lists(st.text(max_size=5), max_size=4)
+    tables = st.recursive(st.dictionaries(keys, st.one_of(scal, lists, st.none()), max_size=4),
+                          lambda inner: st.dictionaries(keys, st.one_of(scal, lists, inner,
+                                                                        st.lists(inner, min_size=1, max_size=2)),
+                                                        max_size=4), max_leaves=10)
+
+    def strip_none(d):
+        if isinstance(d, dict):
+            return {k: strip_none(v) for k, v in d.items() if v is not None}
+        if isinstance(d, list):
+            return [strip_none(x) for x in d]
+        return d
+
+    def same(a, b):
+        if isinstance(a, dict):
+            return isinstance(b, dict) and a.keys() == b.keys() and all(same(a[k], b[k]) for k in a)
+        if isinstance(a, list):
+            return isinstance(b, list) and len(a) == len(b) and all(same(x, y) for x, y in zip(a, b))
+        if isinstance(a, float):
+            return isinstance(b, float) and (a == b or (math.isinf(a) and a == b))
+        return type(a) is type(b) and a == b
+
+    @settings(max_examples=300, deadline=None)
+    @given(tables)
+    def check(d):
+        text = dumps_toml(d)
+        got = loads_toml(text)
+        assert same(strip_none(d), got), text
+
+    check()
