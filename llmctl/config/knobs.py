@@ -67,6 +67,7 @@ class PerfKnobs:
     skinny_gemm: str = "auto"      # decode-size GEMMs on the skinny kernel: auto | all | off
     prefill_swiglu: bool = True    # serving prefill gate/up GEMM with the SwiGLU epilogue
     prefill_fa: bool = True        # fresh prompts through the packed flash-attention kernel
+    prefill_norm_fold: bool = True  # prefill RMSNorms folded into the QKV / gate-up GEMMs (row-scaled epilogue)
     mixed_steps: bool = True       # decode rows ride on prefill chunk steps
     custom_ar: bool = True         # TP all-reduces through the xGMI peer-memory kernel
     tp_graphs: bool = True         # TP decode steps captured in hipGraphs

@@ -24,10 +24,13 @@ from .functional import (
     kv_cache_write,
     l2norm_sq,
     layernorm,
+    linear_acc_,
+    linear_rowscale,
     paged_attention_decode,
     paged_prefill_attention,
     attn_merge_,
     prefill_work_list,
+    rms_rstd,
     rmsnorm,
     rope_qkv,
     rope_flash_attention,
@@ -36,6 +39,7 @@ from .functional import (
     swiglu,
     transpose_,
     up_swiglu,
+    up_swiglu_rowscale,
 )
 
 __all__ = [
@@ -44,4 +48,5 @@ __all__ = [
     "flash_attention", "gelu", "kv_cache_write", "l2norm_sq", "layernorm", "paged_attention_decode",
     "paged_prefill_attention", "prefill_work_list", "attn_merge_",
     "rmsnorm", "rope_qkv", "rope_flash_attention", "rope_qkv_cache", "sample", "swiglu", "transpose_", "up_swiglu",
+    "rms_rstd", "linear_rowscale", "up_swiglu_rowscale", "linear_acc_",
 ]

@@ -73,7 +73,9 @@ TORCH_LIBRARY(llmctl, m) {
   m.def("gemm_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int variant=-1) -> ()");
   m.def("hbm_copy(Tensor src, Tensor(a!) dst) -> ()");
   m.def("gemm64_ex(Tensor a, Tensor b, Tensor(a!) out, bool at, bool bt, bool accumulate, int config=4) -> ()");
-  m.def("gemm64_swiglu_fwd(Tensor x, Tensor w, int config) -> Tensor");
+  m.def("gemm64_swiglu_fwd(Tensor x, Tensor w, int config, Tensor? rstd=None) -> Tensor");
+  m.def("gemm64_rs(Tensor x, Tensor w, Tensor rstd, int config=304) -> Tensor");
+  m.def("rms_rstd(Tensor x, float eps) -> Tensor");
   m.def("gemm64_swiglu_dgrad(Tensor dy, Tensor w, Tensor gu, int config=104) -> Tensor");
   m.def("gemm64_qkv_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, Tensor? pos, int nq, int nkv, int seq, int config=104) -> (Tensor, Tensor, Tensor)");
   m.def("gemm64_up_swiglu(Tensor x, Tensor w, int config=104) -> (Tensor, Tensor)");

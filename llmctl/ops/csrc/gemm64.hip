@@ -112,6 +112,9 @@ struct G64Args {
   const float* sinT = nullptr;
   const int* pos = nullptr;        // EPI_ROPE_QKV: int32 position per token (nullptr: t % seq)
   int nq = 0, nkv = 0, seq = 1;
+  // RS (row-scaled forward, serving prefill with the RMSNorm folded in): C[m, :] *= rs[m] before the
+  // bf16 rounding -- rs = the rows' RMSNorm rstd, the norm weight folded into B's K columns
+  const float* rs = nullptr;
   // side job (SIDE > 0, wgrad of the down projection): dgu = swiglu_bwd(dact, gu), dact [T, F],
   // gu / dgu [T, 2F], E = T * F elements spread over the K-tiles of the whole grid
   const unsigned short* s_dact = nullptr;
@@ -838,11 +841,15 @@ __device__ __forceinline__ void g2p_fence(f32x4_t (&acc)[8][8]) {
 
 // 4-wave epilogues (lane holds C[wr*128 + 16 i + (l & 15)][wc*128 + 16 j + 4 (l >> 4) + r]): split
 // partial, fp32 store / accumulate, bf16 store / accumulate, fused RoPE-QKV / SwiGLU forward
-template <int EPI>
+template <int EPI, bool RS = false>
 __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)[8][8], int tm, int tn, int wr, int wc,
-                                             int lane, int sp, int u) {
+                                             int lane, int sp, int u, const float* rsl = nullptr) {
   constexpr bool PAIRED_B = EPI == EPI_UP_SWIGLU || EPI == EPI_SWIGLU_FWD;
   const int g = lane >> 4, i16 = lane & 15;
+  // RS: the lane's row 16 i + i16 of the wave's 128 is scaled by rs[row], read per row block from
+  // the tile's 256 rs values staged in LDS (rsl; split partials stay unscaled: gemm64_split_reduce
+  // scales their sum)
+  auto row_scale = [&](int i) __attribute__((always_inline)) { return RS ? rsl[wr * 128 + 16 * i + i16] : 1.f; };
   if constexpr (EPI == EPI_ROPE_QKV) {
     if (sp >= 0) {  // a split tail item: fp32 partials; gemm64_split_reduce applies the RoPE epilogue
       float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 128 + 4 * g;
@@ -911,6 +918,7 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const long t = (long)tm * TM + wr * 128 + 16 * i + i16;
+      const float ri = row_scale(i);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = tn * 128 + wc * 64 + 16 * j + 4 * g;
@@ -918,8 +926,8 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
         unsigned short gb[4], ub[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {  // as swiglu_fwd_kernel on the bf16-stored g / u
-          gb[e] = f2bf(acc[i][j][e]);
-          ub[e] = f2bf(acc[i][j + 4][e]);
+          gb[e] = f2bf(RS ? acc[i][j][e] * ri : acc[i][j][e]);
+          ub[e] = f2bf(RS ? acc[i][j + 4][e] * ri : acc[i][j + 4][e]);
           const float gg = bf2f(gb[e]), uu = bf2f(ub[e]);
           o[e] = gg * (1.f / (1.f + __expf(-gg))) * uu;
         }
@@ -978,6 +986,7 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     uint4 old[4];
+    const float ri = row_scale(i);
     if constexpr (EPI == EPI_ACC) {
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) old[jp] = *reinterpret_cast<const uint4*>(Cb + (long)(16 * i) * args.ldc + 32 * jp);
@@ -1002,10 +1011,15 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
           pk[e] = (unsigned)f2bf(v[2 * e] + bf2f(ow[e] & 0xffff)) | ((unsigned)f2bf(v[2 * e + 1] + bf2f(ow[e] >> 16)) << 16);
         o = make_uint4(pk[0], pk[1], pk[2], pk[3]);
       } else {
-        const unsigned x0 = (unsigned)f2bf(acc[i][j][0]) | ((unsigned)f2bf(acc[i][j][1]) << 16);
-        const unsigned x1 = (unsigned)f2bf(acc[i][j][2]) | ((unsigned)f2bf(acc[i][j][3]) << 16);
-        const unsigned y0 = (unsigned)f2bf(acc[i][j + 1][0]) | ((unsigned)f2bf(acc[i][j + 1][1]) << 16);
-        const unsigned y1 = (unsigned)f2bf(acc[i][j + 1][2]) | ((unsigned)f2bf(acc[i][j + 1][3]) << 16);
+        f32x4_t c0 = acc[i][j], c1 = acc[i][j + 1];
+        if constexpr (RS) {
+          c0 *= ri;
+          c1 *= ri;
+        }
+        const unsigned x0 = (unsigned)f2bf(c0[0]) | ((unsigned)f2bf(c0[1]) << 16);
+        const unsigned x1 = (unsigned)f2bf(c0[2]) | ((unsigned)f2bf(c0[3]) << 16);
+        const unsigned y0 = (unsigned)f2bf(c1[0]) | ((unsigned)f2bf(c1[1]) << 16);
+        const unsigned y1 = (unsigned)f2bf(c1[2]) | ((unsigned)f2bf(c1[3]) << 16);
         const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
         const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
         o = make_uint4(r0[0], r1[0], r0[1], r1[1]);
@@ -1318,10 +1332,12 @@ constexpr int EXP = 0;
 #else
 constexpr int STAMP = 0, EXP = 0;
 #endif
-template <bool AT, bool BT, int EPI, int GROUP>
+template <bool AT, bool BT, int EPI, int GROUP, bool RS = false>
 __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4wp_kernel(G64Args args,
                                                                                                   int n_items) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF + (STAMP ? 4 * STAMPS * 4 : 0)];
+  // RS: two 1 KB slots (item parity) of the tile rows' rs values behind the operand buffers
+  constexpr int RSB = RS ? 2048 : 0;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF + RSB + (STAMP ? 4 * STAMPS * 4 : 0)];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // lane-constant addressing (DMA voffsets, fragment LDS offsets) is recomputed per item from a
@@ -1418,7 +1434,7 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     if constexpr (STAMP) {
       const unsigned tt = (unsigned)__builtin_amdgcn_s_memtime();
       if ((tid & 63) == 0 && sidx < STAMPS)
-        *reinterpret_cast<unsigned*>(smem + 2 * BUF + (wave * STAMPS + sidx) * 4) = tt;
+        *reinterpret_cast<unsigned*>(smem + 2 * BUF + RSB + (wave * STAMPS + sidx) * 4) = tt;
       ++sidx;
     }
   };
@@ -1489,6 +1505,21 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       for (int ks = 0; ks < 2; ++ks) b03[0][j][ks] = frag<BT>(smem + bo03, p03 + 16 * j, ks, lane);
     sync(K_<-1>{});
   };
+  // RS: wave 0 stages the item's 256 rs values into LDS slot (item parity) with one LDS-DMA piece,
+  // issued where no load is outstanding (kernel entry / behind the item-boundary drain): it is then
+  // the OLDEST load, retired by the first counted wait that also retires younger pieces (loads
+  // retire in order), so every count in the loop still holds; the K-loop's barriers publish it to
+  // the other waves long before the epilogue.  A slot is rewritten two items later, after the
+  // barriers of the item in between (no wave still reads it).
+  int it = 0;
+  auto rs_issue = [&]() __attribute__((always_inline)) {
+    if constexpr (RS) {
+      if (wave == 0)
+        bdma16(make_rsrc(args.rs + (long)c_tm * TM), (unsigned)(tid & 63) * 16u, 0u,
+               lds_addr(smem) + 2 * BUF + (it & 1) * 1024);
+    }
+  };
+  rs_issue();
   // prologue (first item only): K-tiles 0 and 1 in flight; retire A_lo(0) / B(0)
   issue(K_<A_LO>{}, 0);
   issue(K_<B_H0>{}, 0);
@@ -1521,7 +1552,8 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     g4w_fence(acc);
     if (!has_next) wait_vm<0>();  // the re-loads of the last item's K-tiles 0 / 1 are still landing
     stamp();
-    g4w_epilogue<EPI>(args, acc, c_tm, c_tn, wr, wc, lane, c_sp, c_u);
+    g4w_epilogue<EPI, RS>(args, acc, c_tm, c_tn, wr, wc, lane, c_sp, c_u,
+                          reinterpret_cast<const float*>(smem + 2 * BUF + (it & 1) * 1024));
     if constexpr (STAMP) {
       wait_vm<0>();
       stamp();
@@ -1531,7 +1563,7 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       if (out != nullptr && blockIdx.x < 32 && it < 4)
         for (int e = (tid & 63); e < STAMPS; e += 64)
           out[((blockIdx.x * 4 + wave) * 4 + it) * STAMPS + e] =
-              *reinterpret_cast<const unsigned*>(smem + 2 * BUF + (wave * STAMPS + e) * 4);
+              *reinterpret_cast<const unsigned*>(smem + 2 * BUF + RSB + (wave * STAMPS + e) * 4);
       wait_vm<0>();
       sidx = 0;
     }
@@ -1548,12 +1580,14 @@ __global__ __launch_bounds__(NT4, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     g += (int)gridDim.x;
     c_tm = n_tm, c_tn = n_tn, c_sp = n_sp, c_u = n_u, c_KT = n_KT, c_kt0 = n_kt0;
     c_ra = n_ra, c_rb = n_rb, c_rbh = n_rbh;
+    ++it;
+    rs_issue();
   }
 }
 
 // sum of the split partials of tail tile u (grouped-order position n_main + u) + epilogue;
 // thread = 8 consecutive columns of one row
-template <int EPI, int GROUP>
+template <int EPI, int GROUP, bool RS = false>
 __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
   const int u = blockIdx.x / (TM * TN / 8 / 256);
   const int e = (blockIdx.x % (TM * TN / 8 / 256)) * 256 + threadIdx.x;  // 8-column chunk in the tile
@@ -1574,6 +1608,11 @@ __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
       v[j] += x0[j];
       v[4 + j] += x1[j];
     }
+  }
+  if constexpr (RS) {
+    const float r = args.rs[(long)tm * TM + row];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= r;
   }
   if constexpr (EPI == EPI_ROPE_QKV) {
     // the main epilogue's RoPE / head split: a thread of the first half of a head (d < 64) also sums
@@ -1662,12 +1701,17 @@ __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
 // (measured slower, aliased here): the 8-wave schedules 0 / 2 / 3 and persistent 8-wave kernel (5;
 // profiles/gemm_persistent_r3.txt), the 4-wave K-step-major kernel (4) and the 4-wave phase
 // orderings 6-8 (profiles/ab_gemm64_config_r4.log), register-staged B (profiles/gemm_regstage_ab_r4.txt)
-template <bool AT, bool BT, int EPI, int GROUP>
+template <bool AT, bool BT, int EPI, int GROUP, bool RS = false>
 void launch_g(const G64Args& g, int variant) {
   const int n_items = g.n_main + (g.tiles_m * g.tiles_n - g.n_main) * g.splits;
   const dim3 grid(n_items);
   bool launched = false;
-  if constexpr (EPI != EPI_SWIGLU_BWD) {
+  if constexpr (RS) {  // row-scaled epilogue: the persistent kernel only
+    LLMCTL_CHECK(variant == 3 && g.K >= 4 * TK, "gemm64 row-scaled epilogue: persistent schedule (variant 3), K >= 256");
+    hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP, true>), dim3(min(n_items, num_cus())), dim3(NT4), 0, stream(),
+                       g, n_items);
+    launched = true;
+  } else if constexpr (EPI != EPI_SWIGLU_BWD) {
     if (variant == 3 && g.K >= 4 * TK) {  // the persistent kernel peels two K-tiles per item
       hipLaunchKernelGGL((gemm4wp_kernel<AT, BT, EPI, GROUP>), dim3(min(n_items, num_cus())), dim3(NT4), 0, stream(), g,
                          n_items);
@@ -1677,20 +1721,21 @@ void launch_g(const G64Args& g, int variant) {
       launched = true;
     }
   }
-  if (!launched) hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP>), grid, dim3(NTHR), 0, stream(), g);
+  if constexpr (!RS)
+    if (!launched) hipLaunchKernelGGL((gemm64_kernel<AT, BT, EPI, GROUP>), grid, dim3(NTHR), 0, stream(), g);
   const int n_tail = g.tiles_m * g.tiles_n - g.n_main;
   if (n_tail > 0)
-    hipLaunchKernelGGL((gemm64_split_reduce<EPI, GROUP>), dim3(n_tail * (TM * TN / 8 / 256)), dim3(256), 0, stream(),
-                       g);
+    hipLaunchKernelGGL((gemm64_split_reduce<EPI, GROUP, RS>), dim3(n_tail * (TM * TN / 8 / 256)), dim3(256), 0,
+                       stream(), g);
 }
 
 // config = group (tile-rows per tile-order group: 4 / 8) + 100 * schedule variant
 //          + 1000 * split (0: automatic tail split, 1: none, S >= 2: S K-ranges when legal)
-template <bool AT, bool BT, int EPI>
+template <bool AT, bool BT, int EPI, bool RS = false>
 void launch(const G64Args& g, int config) {
   const int group = config % 100, variant = (config / 100) % 10;
-  if (group == 8) launch_g<AT, BT, EPI, 8>(g, variant);
-  else launch_g<AT, BT, EPI, 4>(g, variant);
+  if (group == 8) launch_g<AT, BT, EPI, 8, RS>(g, variant);
+  else launch_g<AT, BT, EPI, 4, RS>(g, variant);
 }
 
 // Tail split plan: tiles of the last, partial round (when it is at most half full) are cut into
@@ -1921,7 +1966,17 @@ at::Tensor gemm64_wgrad_swiglu(const at::Tensor& dy, const at::Tensor& act, at::
 
 // Gate/up projection fused with SwiGLU (serving prefill): act [M, F] = silu(x Wg^T) * (x Wu^T) with
 // W_up = [Wg; Wu] [2F, K] (forward layout, both operands K-contiguous); M % 256, F % 128, K % 128.
-at::Tensor gemm64_swiglu_fwd(const at::Tensor& x, const at::Tensor& w, int64_t config) {
+void check_rstd(const c10::optional<at::Tensor>& rstd, long M, const char* who) {
+  if (!rstd.has_value() || !rstd->defined()) return;
+  LLMCTL_CHECK(rstd->is_cuda() && rstd->scalar_type() == at::kFloat && rstd->is_contiguous() && rstd->numel() == M, who,
+               ": rstd must be a contiguous fp32 GPU tensor [M]");
+}
+
+// persistent schedule (variant 3) of a config, keeping its group and split fields
+int persistent_config(int64_t config) { return (int)((config / 1000) * 1000 + 300 + config % 100); }
+
+at::Tensor gemm64_swiglu_fwd(const at::Tensor& x, const at::Tensor& w, int64_t config,
+                             const c10::optional<at::Tensor>& rstd) {
   LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                    x.is_cuda() && w.is_cuda() && x.stride(1) == 1 && w.is_contiguous(),
                "gemm64_swiglu_fwd: bf16 GPU x [M, K] (unit inner stride), contiguous W_up [2F, K]");
@@ -1940,7 +1995,14 @@ at::Tensor gemm64_swiglu_fwd(const at::Tensor& x, const at::Tensor& w, int64_t c
             reinterpret_cast<unsigned short*>(act.data_ptr()), x.stride(0), K, F,
             (int)M, (int)F, (int)K, (int)(M / TM), (int)(F / (TN / 2)), 0, 1, 0, nullptr, nullptr};
   plan_split(g, 1);  // whole tiles only (the pairing epilogue has no split-K reduction)
-  launch<false, false, EPI_SWIGLU_FWD>(g, (int)(config % 1000));
+  check_rstd(rstd, M, "gemm64_swiglu_fwd");
+  if (rstd.has_value() && rstd->defined()) {
+    LLMCTL_CHECK(K >= 4 * TK, "gemm64_swiglu_fwd: row-scaled form needs K >= 256");
+    g.rs = rstd->data_ptr<float>();
+    launch<false, false, EPI_SWIGLU_FWD, true>(g, persistent_config(config) % 1000);
+  } else {
+    launch<false, false, EPI_SWIGLU_FWD>(g, (int)(config % 1000));
+  }
   return act;
 }
 
@@ -2022,7 +2084,39 @@ std::tuple<at::Tensor, at::Tensor> gemm64_up_swiglu(const at::Tensor& x, const a
   return {gu, act};
 }
 
+// Row-scaled projection (serving prefill, RMSNorm folded in): y = (x · w^T) * rstd[:, None] in bf16,
+// x [M, K] (M % 256), w [N, K] (N % 256) with the norm weight folded into its K columns.
+at::Tensor gemm64_rs(const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd, int64_t config) {
+  LLMCTL_CHECK(x.dim() == 2 && w.dim() == 2 && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                   x.is_cuda() && w.is_cuda() && x.stride(1) == 1 && w.is_contiguous(),
+               "gemm64_rs: bf16 GPU x [M, K] (unit inner stride), contiguous w [N, K]");
+  const long M = x.size(0), K = x.size(1), N = w.size(0);
+  LLMCTL_CHECK(w.size(1) == K && gemm64_supported(M, N, K) && K >= 4 * TK,
+               "gemm64_rs: M, N multiples of 256, K of 128 and >= 256 (got ", M, "x", N, "x", K, ")");
+  LLMCTL_CHECK(x.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0 && (long)TM * x.stride(0) * 2 < (1L << 31) &&
+                   (long)TN * K * 2 < (1L << 31),
+               "gemm64_rs: 16-byte aligned rows / 32-bit offsets");
+  check_rstd(rstd, M, "gemm64_rs");
+  const c10::DeviceGuard dg(x.device());
+  auto y = at::empty({M, N}, x.options());
+  G64Args g{reinterpret_cast<const unsigned short*>(x.data_ptr()), reinterpret_cast<const unsigned short*>(w.data_ptr()),
+            reinterpret_cast<unsigned short*>(y.data_ptr()), x.stride(0), K, N,
+            (int)M, (int)N, (int)K, (int)(M / TM), (int)(N / TN), 0, 1, 0, nullptr, nullptr};
+  g.rs = rstd.data_ptr<float>();
+  const int cfg = persistent_config(config);
+  plan_split(g, cfg / 1000);
+  at::Tensor ws;
+  if (g.splits > 1) {
+    ws = at::empty({(long)(g.tiles_m * g.tiles_n - g.n_main) * g.splits * TM * TN}, x.options().dtype(at::kFloat));
+    g.ws = ws.data_ptr<float>();
+  }
+  launch<false, false, EPI_STORE, true>(g, cfg % 1000);
+  return y;
+}
+
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("gemm64_rs", &gemm64_rs);
   m.impl("gemm64_qkv_rope", &gemm64_qkv_rope);
   m.impl("gemm64_up_swiglu", &gemm64_up_swiglu);
   m.impl("gemm64_swiglu_fwd", &gemm64_swiglu_fwd);

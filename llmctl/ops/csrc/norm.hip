@@ -100,6 +100,33 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const unsigned short* __r
   }
 }
 
+// RMSNorm statistics only: rstd[row] = rsqrt(mean(x[row]^2) + eps), one wave per row (serving
+// prefill with the norm folded into the next projection: the GEMM scales its output rows by rstd
+// and the norm weight lives in its K columns, so no normalised copy of x is written)
+template <int NV>
+__global__ __launch_bounds__(256) void rstd_kernel(const unsigned short* __restrict__ x, float* __restrict__ rstd_out,
+                                                   int T, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * kWaves;
+  for (int row = wave; row < T; row += nwaves) {
+    const size_t base = (size_t)row * H;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = i * 512 + lane * 8;
+      if (col < H) {
+        float v[8];
+        load8(x + base + col, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+      }
+    }
+    s = wave_sum(s);
+    if (lane == 0) rstd_out[row] = rsqrtf(s / (float)H + eps);
+  }
+}
+
 template <int NV, bool LN, bool DRES>
 __global__ __launch_bounds__(256, LN ? 1 : 2) void norm_bwd_kernel(const unsigned short* __restrict__ dy,
                                                                     const unsigned short* __restrict__ x,
@@ -512,7 +539,31 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layernorm_bwd(const at::Tensor& d
   return {dx, dw, db};
 }
 
+at::Tensor rms_rstd(const at::Tensor& x, double eps) {
+  check2d(x, "x");
+  const int T = x.size(0), H = x.size(1);
+  LLMCTL_CHECK(H % 8 == 0 && H <= 16384, "rms_rstd: hidden size must be a multiple of 8 and <= 16384, got ", H);
+  const c10::DeviceGuard g(x.device());
+  auto rstd = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+  if (T == 0) return rstd;
+  const int nv = (H + 511) / 512;
+  dim3 grid(fwd_grid(T)), block(256);
+  auto s = stream();
+#define LAUNCH(NV) \
+  hipLaunchKernelGGL((rstd_kernel<NV>), grid, block, 0, s, bf_ptr(x), rstd.data_ptr<float>(), T, H, (float)eps)
+  switch (nv) {
+    case 1: LAUNCH(1); break;
+    case 2: LAUNCH(2); break;
+    case 3: case 4: LAUNCH(4); break;
+    case 5: case 6: case 7: case 8: LAUNCH(8); break;
+    default: LAUNCH(32); break;
+  }
+#undef LAUNCH
+  return rstd;
+}
+
 TORCH_LIBRARY_IMPL(llmctl, CUDA, m) {
+  m.impl("rms_rstd", &rms_rstd);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);

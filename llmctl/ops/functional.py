@@ -524,6 +524,60 @@ def decode_up_swiglu(x, w, b=None, w_scale=None):
     return swiglu(decode_linear(x, _dequant(w, w_scale, x.dtype), b))
 
 
+# ----------------------------------------------------------- prefill with the RMSNorm folded in
+# Serving prefill (llmctl/serve/engine.py ``_prefill_layers_folded``): rmsnorm(h) * w_n @ W^T equals
+# rstd(h)[:, None] * (h @ (W * w_n)^T), so with the norm weight folded into the projection's K
+# columns (once, at engine start) the norm reduces to a per-row statistic that the GEMM applies in its
+# epilogue, and no normalised copy of h is written or read.
+
+def rms_rstd(x, eps: float):
+    """``rsqrt(mean(x^2, -1) + eps)`` per row of a 2-D bf16 ``x`` (fp32 [T])."""
+    if use_native(x):
+        return native().rms_rstd(x.contiguous(), eps)
+    return torch.rsqrt(x.float().pow(2).mean(-1) + eps)
+
+
+def rowscale_ok(x, w) -> bool:
+    """Shapes the row-scaled gemm64 forms take: x [T, K], w [N, K], T and N multiples of 256, K of
+    128 and >= 256, bf16 GPU operands, 16-byte aligned rows."""
+    return (use_native(x) and x.dim() == 2 and w.dim() == 2 and x.dtype == w.dtype == torch.bfloat16
+            and x.shape[0] % 256 == 0 and x.shape[0] > 0 and w.shape[0] % 256 == 0 and x.shape[1] == w.shape[1]
+            and x.shape[1] % 128 == 0 and x.shape[1] >= 256 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0 and w.is_contiguous() and w.data_ptr() % 16 == 0)
+
+
+def linear_rowscale(x, w, rstd):
+    """``(x @ w^T) * rstd[:, None]`` rounded once to bf16 (gemm64 persistent kernel, row scale in
+    its epilogue)."""
+    if rowscale_ok(x, w):
+        from llmctl.exec.linear import gemm64_config
+
+        return native().gemm64_rs(x, w, rstd, gemm64_config("fwd", x.shape[0], w.shape[0], x.shape[1]))
+    return ((x.float() @ w.float().t()) * rstd.float()[:, None]).to(x.dtype)
+
+
+def up_swiglu_rowscale(x, w, rstd):
+    """``silu(g) * u`` of ``(x @ w^T) * rstd[:, None]`` (w = [W_gate; W_up]): the SwiGLU and the row
+    scale in the gate/up GEMM's epilogue."""
+    F = w.shape[0] // 2
+    if rowscale_ok(x, w) and F % 128 == 0:
+        from llmctl.exec.linear import gemm64_config
+
+        return native().gemm64_swiglu_fwd(x, w, gemm64_config("fwd", x.shape[0], w.shape[0], x.shape[1]) % 1000, rstd)
+    gu = ((x.float() @ w.float().t()) * rstd.float()[:, None]).to(x.dtype)
+    return swiglu(gu)
+
+
+def linear_acc_(x, w, out):
+    """``out += x @ w^T`` in place (the residual add riding on the projection's epilogue)."""
+    if rowscale_ok(x, w) and out.is_contiguous() and out.shape == (x.shape[0], w.shape[0]):
+        from llmctl.exec.linear import gemm64_config
+
+        native().gemm64_ex(x, w, out, False, False, True, gemm64_config("fwd", x.shape[0], w.shape[0], x.shape[1]))
+        return out
+    return out.addmm_(x, w.t())
+
+
 def decode_linear_add_rmsnorm(x, w, b, residual, norm_w, eps: float, w_scale=None):
     """Decode row projection + residual add + RMSNorm in one finalize pass:
     ``(rmsnorm(y + residual) * norm_w, y + residual)`` with ``y = x @ w^T (+ b)``."""
@@ -546,4 +600,5 @@ __all__ = [
     "gelu", "cross_entropy", "adamw_step_", "l2norm_sq", "kv_cache_write", "paged_attention_decode",
     "sample", "decode_linear", "decode_linear_fp8", "decode_fused_ok", "decode_qkv_rope_cache", "decode_up_swiglu", "decode_attention_qkv", "up_swiglu",
     "decode_linear_add_rmsnorm", "rope_qkv_cache", "paged_prefill_attention", "prefill_work_list", "attn_merge_",
+    "rms_rstd", "rowscale_ok", "linear_rowscale", "up_swiglu_rowscale", "linear_acc_",
 ]

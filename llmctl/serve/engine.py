@@ -95,6 +95,11 @@ class InferenceEngine:
         elif weight_dtype not in ("auto", "model", "bf16", "bfloat16"):
             raise ValueError(f"weight_dtype must be auto / bf16 / fp8, got {weight_dtype!r}")
         self.weight_dtype = "fp8" if self._w8 is not None else "auto"
+        # prefill with the RMSNorms folded into the QKV / gate-up projections (knob
+        # prefill_norm_fold): copies of those weights with the norm weight multiplied into their K
+        # columns ((H + 2 kv) D + 2 F) H bf16 per layer, made before the KV cache is sized
+        self._nf: Optional[List[Tuple[torch.Tensor, torch.Tensor]]] = (
+            self._fold_norm_weights() if self.knobs.prefill_norm_fold else None)
         # KV cache element: the model dtype ("auto"), or OCP fp8 e4m3fn ("fp8": half the bytes per
         # token, so twice the blocks and half the decode attention's HBM stream; saturating at +-448)
         if kv_cache_dtype in ("auto", "model", "bf16", "bfloat16"):
@@ -134,6 +139,52 @@ class InferenceEngine:
         self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "graph_replays": 0}
         log.info("engine: %s on %s, %d KV blocks x %d tokens (%.1f GB)", cfg.name, self.device, num_kv_blocks,
                  block_size, self.kv_cache.nbytes / 1e9)
+
+    def _fold_norm_weights(self) -> Optional[List[Tuple[torch.Tensor, torch.Tensor]]]:
+        """(W_qkv * w_attn_norm, W_up * w_mlp_norm) per layer, or None when the model does not fit
+        the folded prefill (GPU, TP=1, RMSNorm, RoPE, dense SwiGLU MLP without biases, gemm64 shapes)."""
+        cfg, m = self.cfg, self.model
+        if (self.device.type != "cuda" or self.tp != 1 or cfg.is_moe or not cfg.gated_mlp or cfg.norm != "rmsnorm"
+                or cfg.position != "rope" or cfg.hidden % 128 or cfg.hidden < 256):
+            return None
+        out = []
+        for layer in m.layers:
+            if (layer.moe is not None or layer.bqkv is not None or layer.bo is not None or layer.b_up is not None
+                    or layer.b_down is not None or layer.wqkv.shape[0] % 256 or layer.w_up.shape[0] % 256
+                    or layer.w_down.shape[0] % 256):
+                return None
+            out.append(((layer.wqkv.float() * layer.attn_norm_w.float()).to(layer.wqkv.dtype).contiguous(),
+                        (layer.w_up.float() * layer.mlp_norm_w.float()).to(layer.w_up.dtype).contiguous()))
+        return out
+
+    def _norm_fold_ok(self, T: int) -> bool:
+        return self._nf is not None and self.knobs.prefill_norm_fold and T > 0 and T % 256 == 0
+
+    def _prefill_layers_folded(self, x, pos, slots, fa, doc, bt, cu, ctx, work):
+        """The prefill layers with each RMSNorm folded into the projection that consumes it: per layer
+        rstd(h) -> QKV GEMM scaling its rows by rstd -> RoPE + cache write -> attention -> h += o W_o^T
+        (hipBLASLt beta = 1) -> rstd(h) -> gate/up GEMM with row scale and SwiGLU -> h += act W_down^T
+        (gemm64 accumulate epilogue).  Returns the residual stream h [T, H] after the last layer (the
+        final norm is applied to the selected rows only)."""
+        T = x.shape[0]
+        eps = self.cfg.layer_norm_eps
+        kc, vc = self.kv_cache.k, self.kv_cache.v
+        h = x.contiguous()
+        for li, layer in enumerate(self.model.layers):
+            wqkv_f, wup_f = self._nf[li]
+            qkv = ops.linear_rowscale(h, wqkv_f, ops.rms_rstd(h, eps))
+            q, k, v = ops.rope_qkv_cache(qkv, self.rope[0], self.rope[1], layer.nq, layer.nkv, self.max_model_len,
+                                         pos, kc[li], vc[li], slots)
+            if fa:
+                o = ops.flash_attention(q.view(1, T, layer.nq, layer.D), k.view(1, T, layer.nkv, layer.D),
+                                        v.view(1, T, layer.nkv, layer.D), causal=True, doc_start=doc)
+            else:
+                o = ops.paged_prefill_attention(q.view(T, layer.nq, layer.D), kc[li], vc[li], bt, cu, ctx,
+                                                work=work)
+            h.addmm_(o.reshape(T, -1), layer.wo.t())
+            act = ops.up_swiglu_rowscale(h, wup_f, ops.rms_rstd(h, eps))
+            ops.linear_acc_(act, layer.w_down, h)
+        return h
 
     # ------------------------------------------------------------------ TP hooks (identity at tp=1)
     def _load(self, model_path: str, dtype, seed: int):
@@ -269,6 +320,14 @@ class InferenceEngine:
         # (one prompt: plain causal attention, which also lets the kernel split the K/V range of
         # its few q-blocks over two workgroups — the split is off for packed documents)
         x = self._embed(ids, pos.long())
+        if self._norm_fold_ok(T):
+            h = self._prefill_layers_folded(x, pos, slots, fa, doc, bt, cu, ctx, work)
+            self.stats["prefill_tokens"] += T
+            if not plan["last"]:
+                return torch.empty(0, self.cfg.vocab_size, device=d, dtype=h.dtype)
+            hl = h.index_select(0, torch.tensor(plan["last"], device=d))
+            xn = ops.rmsnorm(hl, self.model.final_norm_w, self.cfg.layer_norm_eps)
+            return self._gather_vocab(ops.decode_linear(xn, self.model.head_weight()))
         res = None
         kc, vc = self.kv_cache.k, self.kv_cache.v
         for li, layer in enumerate(self.model.layers):

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--knob-sets", nargs="+", required=True, help="'name=value,name=value' native knob sets")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--repeats", type=int, default=4)
+    ap.add_argument("--init-knobs", default="", help="'name=value,...' PerfKnobs given to the engine at construction")
     a = ap.parse_args()
     import torch
 
@@ -31,7 +32,9 @@ def main():
     assert _lib.load(), _lib._error
     ops = torch.ops.llmctl
     sets = [{kv.split("=")[0]: int(kv.split("=")[1]) for kv in ks.split(",")} for ks in a.knob_sets]
-    eng = InferenceEngine(a.model, device="cuda", max_batch_size=1, max_model_len=a.prompt_length + 32)
+    init = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.init_knobs.split(",") if kv}
+    eng = InferenceEngine(a.model, device="cuda", max_batch_size=1, max_model_len=a.prompt_length + 32,
+                          perf_knobs=init or None)
     p = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
     V = eng.cfg.vocab_size
     eng.generate([[1] * 32], p)
