@@ -604,6 +604,7 @@ class InferenceEngine:
             torch.cuda.synchronize(self.device)
         self.kv_cache = None
         self._w8 = self._w8_head = None
+        self._nf = None
         self.rope = None
         if self.device.type == "cuda":
             torch.cuda.empty_cache()

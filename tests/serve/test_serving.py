@@ -500,7 +500,7 @@ def test_engine_close_is_deterministic_and_idempotent():
                          max_model_len=64) as e:
         e.generate([[1, 2, 3]], SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
         assert e.kv_cache is not None
-    assert e.kv_cache is None and e._pending is None and not e._graphs
+    assert e.kv_cache is None and e._pending is None and not e._graphs and e._nf is None
     e.close()
 
 
