@@ -673,3 +673,52 @@ def test_scheduler_simulation_property():
             assert kv.refcount(b) == (1 if b in held else 0)
 
     run()
+
+
+def test_sampling_oracle_property():
+    """Property test (hypothesis) of the sampling oracle (``llmctl.ops.ref.sample``, the semantics
+    ``csrc/sampling.hip`` is tested against): temperature <= 0 is the argmax; otherwise the token
+    is in the kept set {x >= max(k-th largest, top-p threshold)} with a nonzero weight, the argmax
+    is always drawable, the draw is monotone in the uniform (inverse CDF in vocabulary order) and
+    u = 0 picks the first drawable token."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from llmctl.ops import ref
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.integers(1, 64), st.integers(0, 2**31 - 1), st.one_of(st.just(0.0), st.floats(0.05, 3.0)),
+           st.integers(0, 70),
+           st.floats(0.05, 1.0), st.floats(0.0, 0.999999), st.floats(0.0, 0.999999))
+    def check(V, seed, temp, k, p, u1, u2):
+        g = torch.Generator().manual_seed(seed)
+        logits = torch.randn(1, V, generator=g) * 3
+        if seed % 3 == 0:
+            logits = logits.round()  # ties
+        T, K, P = torch.tensor([temp]), torch.tensor([k]), torch.tensor([p])
+        lo, hi = min(u1, u2), max(u1, u2)
+        a = int(ref.sample(logits, T, K, P, torch.tensor([lo]))[0])
+        b = int(ref.sample(logits, T, K, P, torch.tensor([hi]))[0])
+        if temp <= 0:
+            assert a == b == int(torch.argmax(logits[0]))
+            return
+        x = logits[0].float() / temp
+        thr = -float("inf")
+        if 0 < k < V:
+            thr = float(torch.topk(x, k).values[-1])
+        if p < 1.0:
+            e = torch.exp(x - x.max())
+            sx, si = torch.sort(x, descending=True)
+            cum = torch.cumsum(e[si], 0)
+            n = int((cum < p * float(e.sum())).sum())
+            thr = max(thr, float(sx[min(n, V - 1)]))
+        keep = x >= thr
+        # drawable: kept with a nonzero weight (a kept token whose exp underflows is never drawn)
+        drawable = keep & (torch.exp(x - x.max()) > 0)
+        assert bool(drawable[int(torch.argmax(x))])
+        assert bool(drawable[a]) and bool(drawable[b])
+        assert a <= b
+        first = int(torch.nonzero(drawable)[0])
+        assert int(ref.sample(logits, T, K, P, torch.tensor([0.0]))[0]) == first
+
+    check()

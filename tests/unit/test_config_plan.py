@@ -226,3 +226,58 @@ def test_toml_writer_roundtrip_property():
         assert same(strip_none(d), got), text
 
     check()
+
+
+def test_shard_map_properties():
+    """Property test (hypothesis) of the shard map: pipeline stages are contiguous, cover every
+    layer once and differ by at most one layer (the first / last stages never above a middle one);
+    every rank has unique (tp, dp, pp) coordinates, the pipeline ranks of each (tp, dp) slice own
+    every layer exactly once (virtual chunks included), the TP ranks partition the heads / FFN /
+    vocabulary ranges, and only the first / last pipeline rank holds the embedding / LM head."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    @settings(max_examples=400, deadline=None)
+    @given(st.integers(1, 96), st.integers(1, 8))
+    def stages(L, pp):
+        s = split_layers(L, pp)
+        assert len(s) == pp and s[0][0] == 0 and s[-1][1] == L
+        assert all(a[1] == b[0] for a, b in zip(s, s[1:]))
+        sizes = [e - b for b, e in s]
+        assert max(sizes) - min(sizes) <= 1
+        if pp > 2:
+            assert max(sizes[0], sizes[-1]) <= min(sizes[1:-1])
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.integers(1, 80), st.sampled_from([1, 2, 4, 8]), st.sampled_from([1, 2, 3, 4]), st.integers(1, 3),
+           st.integers(0, 3), st.integers(1, 3), st.integers(1, 64), st.integers(1, 8))
+    def shard(L, tp, pp, dp, zero, V, heads, kvdiv):
+        kv = max(1, heads // kvdiv)
+        model = {"layers": L, "heads": heads, "kv_heads": kv, "hidden": 64 * heads, "ffn": 11008, "vocab_size": 32000}
+        sm = build_shard_map(model, tp, pp, dp, zero, virtual_stages=V)
+        ranks = sm["ranks"]
+        assert len(ranks) == tp * pp * dp
+        assert len({(r["tp_rank"], r["dp_rank"], r["pp_rank"]) for r in ranks}) == len(ranks)
+        Vr = sm["virtual_stages"]
+        assert Vr == (V if pp > 1 else 1)
+        for t in range(tp):
+            for d in range(dp):
+                owned = []
+                for r in ranks:
+                    if r["tp_rank"] == t and r["dp_rank"] == d:
+                        chunks = [r["layers"]] if Vr == 1 else r["layers"]
+                        assert len(chunks) == Vr
+                        for b, e in chunks:
+                            owned.extend(range(b, e))
+                        assert r["embedding"] == (r["pp_rank"] == 0) and r["lm_head"] == (r["pp_rank"] == pp - 1)
+                        assert r["zero_partition"] == ([d, dp] if zero >= 1 else None)
+                assert sorted(owned) == list(range(L))
+        for key, total in (("q_heads", heads), ("kv_heads", kv), ("ffn", 11008), ("vocab", 32000)):
+            for p in range(pp):
+                for d in range(dp):
+                    parts = sorted(r[key] for r in ranks if r["pp_rank"] == p and r["dp_rank"] == d)
+                    assert parts[0][0] == 0 and parts[-1][1] == total
+                    assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+
+    stages()
+    shard()
