@@ -674,6 +674,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm64_kernel(G64Args args) {
     return;
   }
   if constexpr (EPI == EPI_SWIGLU_FWD) {
+    if (sp >= 0) {  // split item (uniform per workgroup): the generic partial tile, gate cols [0, 128), up 128 +
+      float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 64 + 4 * g;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + 16 * j) = acc[i][j];
+      return;
+    }
     // up waves (wc 2, 3) hand their tiles to the gate waves (wc 0, 1) with the same (wr, i, j, lane)
     // through the now idle 128-KB LDS image: [wr][wc & 1][i][j][lane] f32x4
     __syncthreads();
@@ -912,6 +920,18 @@ __device__ __forceinline__ void g4w_epilogue(const G64Args& args, f32x4_t (&acc)
     return;
   }
   if constexpr (PAIRED_B) {
+    if constexpr (EPI == EPI_SWIGLU_FWD) {
+      if (sp >= 0) {  // a split tail item: fp32 partials, gate cols at [0, 128) and up cols at 128 + [0, 128)
+        // of the workspace tile; gemm64_split_reduce applies the row scale and the SwiGLU
+        float* W = args.ws + ((long)u * args.splits + sp) * (TM * TN) + (wr * 128 + i16) * TN + wc * 64 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            *reinterpret_cast<f32x4_t*>(W + (16 * i) * TN + (j < 4 ? 16 * j : 128 + 16 * (j - 4))) = acc[i][j];
+        return;
+      }
+    }
     // n-tile j (< 4): gate cols 128 tn + wc * 64 + 16 j + 4 g + r; n-tile j + 4: the same up cols.
     // EPI_UP_SWIGLU stores gu [T, 2F] and act [T, F]; EPI_SWIGLU_FWD only act (into C, ldc = F)
     const long F = args.N;
@@ -1614,6 +1634,34 @@ __global__ __launch_bounds__(256) void gemm64_split_reduce(G64Args args) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] *= r;
   }
+  if constexpr (EPI == EPI_SWIGLU_FWD) {
+    // the paired tile's gate cols [0, 128) and their up partners 128 + [0, 128): a thread of the gate
+    // half sums its partners too and writes act = silu(g) * u (as the main epilogue, on bf16 g / u)
+    if (col >= TN / 2) return;
+    float w2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < args.splits; ++sp) {
+      const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(W + TN / 2 + (long)sp * (TM * TN));
+      const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(W + TN / 2 + (long)sp * (TM * TN) + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w2[j] += x0[j];
+        w2[4 + j] += x1[j];
+      }
+    }
+    if constexpr (RS) {
+      const float r = args.rs[(long)tm * TM + row];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w2[j] *= r;
+    }
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gg = bf2f(f2bf(v[j])), uu = bf2f(f2bf(w2[j]));
+      o[j] = gg * (1.f / (1.f + __expf(-gg))) * uu;
+    }
+    store8(args.c + ((long)tm * TM + row) * args.ldc + (long)tn * (TN / 2) + col, o);
+    return;
+  }
   if constexpr (EPI == EPI_ROPE_QKV) {
     // the main epilogue's RoPE / head split: a thread of the first half of a head (d < 64) also sums
     // its rotation partners d + 64 and writes both halves
@@ -1994,7 +2042,15 @@ at::Tensor gemm64_swiglu_fwd(const at::Tensor& x, const at::Tensor& w, int64_t c
   G64Args g{reinterpret_cast<const unsigned short*>(x.data_ptr()), reinterpret_cast<const unsigned short*>(w.data_ptr()),
             reinterpret_cast<unsigned short*>(act.data_ptr()), x.stride(0), K, F,
             (int)M, (int)F, (int)K, (int)(M / TM), (int)(F / (TN / 2)), 0, 1, 0, nullptr, nullptr};
-  plan_split(g, 1);  // whole tiles only (the pairing epilogue has no split-K reduction)
+  // tail split (config / 1000, 0 = automatic): split items store the paired tile's fp32 partials and
+  // gemm64_split_reduce applies the SwiGLU (e.g. 4,096 tokens of GPT-7B: 1,376 tiles = 5.375 rounds).
+  // Native knob swiglu_fwd_split = 0: whole tiles only (A/B)
+  plan_split(g, knob("swiglu_fwd_split", 1) ? (int)(config / 1000) : 1);
+  at::Tensor ws;
+  if (g.splits > 1) {
+    ws = at::empty({(long)(g.tiles_m * g.tiles_n - g.n_main) * g.splits * TM * TN}, x.options().dtype(at::kFloat));
+    g.ws = ws.data_ptr<float>();
+  }
   check_rstd(rstd, M, "gemm64_swiglu_fwd");
   if (rstd.has_value() && rstd->defined()) {
     LLMCTL_CHECK(K >= 4 * TK, "gemm64_swiglu_fwd: row-scaled form needs K >= 256");

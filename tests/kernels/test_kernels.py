@@ -851,13 +851,17 @@ def test_gemm64_swiglu_fwd(native_lib, M, F, K):
     tiles) + swiglu_fwd bit for bit, and vs the fp32 oracle."""
     x = _bf(M, K, seed=211)
     w = _bf(2 * F, K, scale=0.05, seed=212)
-    act = native_lib.gemm64_swiglu_fwd(x, w, 104)
+    act = native_lib.gemm64_swiglu_fwd(x, w, 1104)  # whole tiles (the tail split sums fp32 partials)
     gu = torch.empty(M, 2 * F, dtype=torch.bfloat16, device=DEV)
     native_lib.gemm64_ex(x, w, gu, False, False, False, 1104)
     assert act.shape == (M, F) and torch.equal(act, native_lib.swiglu_fwd(gu))
     g = x.float() @ w.float().t()
     ref_act = torch.nn.functional.silu(g[:, :F]) * g[:, F:]
     assert _row_err(act, ref_act) < 2e-2
+    # automatic tail split (8-wave, one-shot and persistent schedules): split items store the paired
+    # tile's fp32 partials, gemm64_split_reduce applies the SwiGLU
+    for cfg in (104, 404, 304):
+        assert _row_err(native_lib.gemm64_swiglu_fwd(x, w, cfg), ref_act) < 2e-2
 
 
 @pytest.mark.parametrize("V", [32000, 50257, 1003])

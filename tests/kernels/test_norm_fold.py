@@ -120,3 +120,23 @@ def test_engine_prefill_norm_fold_matches_unfused(native_lib):
             assert (a.float() - b.float()).norm() / b.float().norm() < 2e-2
     e.knobs = base
     e.close()
+
+
+@pytest.mark.parametrize("rs", [False, True])
+@pytest.mark.parametrize("config", [304, 404, 104])
+def test_swiglu_fwd_tail_split(native_lib, rs, config):
+    """4,096 tokens of GPT-7B's gate/up projection: 1,376 paired tiles = 5.375 rounds, so the automatic
+    plan splits the last round's K range (fp32 partials, SwiGLU and row scale in gemm64_split_reduce):
+    within a bf16 ulp of the whole-tile kernel and vs the fp32 oracle."""
+    M, F, K = 4096, 11008, 4096
+    x = _bf(M, K, seed=11)
+    w = _bf(2 * F, K, seed=12, scale=K ** -0.5)
+    r = (0.5 + torch.rand(M, device=DEV)).float() if rs else None
+    split = native_lib.gemm64_swiglu_fwd(x, w, config, r)
+    whole = native_lib.gemm64_swiglu_fwd(x, w, 1000 + config, r)
+    gu = x.float() @ w.float().t()
+    if rs:
+        gu = gu * r[:, None]
+    want = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    assert row_err(split, want) < 2e-2 and row_err(whole, want) < 2e-2
+    assert (split.float() - whole.float()).abs().max() <= 1.6e-2 * whole.float().abs().max()
