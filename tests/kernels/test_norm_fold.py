@@ -140,3 +140,36 @@ def test_swiglu_fwd_tail_split(native_lib, rs, config):
     want = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
     assert row_err(split, want) < 2e-2 and row_err(whole, want) < 2e-2
     assert (split.float() - whole.float()).abs().max() <= 1.6e-2 * whole.float().abs().max()
+
+
+def test_engine_prefill_norm_fold_gpt7b_layer_dims(native_lib, tmp_path):
+    """One decoder layer at GPT-7B's dimensions (hidden 4096, 32 heads, ffn 11008), one 2,048-token
+    prompt: the folded prefill (QKV GEMM with the row scale and a tail split, gate/up + SwiGLU with the
+    row scale, residual adds in the o / down epilogues) matches the norm-kernel prefill."""
+    import json
+
+    from llmctl.serve.engine import InferenceEngine
+    from llmctl.serve.scheduler import PrefillChunk, SamplingParams, Sequence
+
+    cfg = {"name": "gpt7b-1l", "arch": "decoder-only", "layers": 1, "hidden": 4096, "ffn": 11008, "heads": 32,
+           "vocab_size": 512, "max_position_embeddings": 4096, "rope": {"base": 10000, "scaling": "linear"}}
+    path = tmp_path / "gpt7b-1l.json"
+    path.write_text(json.dumps(cfg))
+    e = InferenceEngine(str(path), device="cuda", max_batch_size=1, num_kv_blocks=160, block_size=16,
+                        max_model_len=2560, use_graphs=False, perf_knobs={"prefill_norm_fold": True})
+    assert e._nf is not None
+    g = torch.Generator().manual_seed(9)
+    seq = Sequence(prompt_ids=torch.randint(0, 512, (2048,), generator=g).tolist(), params=SamplingParams(max_tokens=1))
+    assert e.kv.add_sequence_shared(seq.seq_id, seq.num_tokens, [])
+    plan = e.prefill_plan([PrefillChunk(seq, 0, seq.num_tokens)])
+    base = e.knobs
+    e.knobs = dataclasses.replace(base, prefill_norm_fold=True)
+    la = e.prefill_exec(plan).float()
+    ka, va = e.kv_cache.k[0].clone(), e.kv_cache.v[0].clone()
+    e.knobs = dataclasses.replace(base, prefill_norm_fold=False)
+    lb = e.prefill_exec(plan).float()
+    e.knobs = base
+    assert (la - lb).norm() / lb.norm() < 2e-2
+    for a, b in ((ka, e.kv_cache.k[0]), (va, e.kv_cache.v[0])):
+        assert (a.float() - b.float()).norm() / b.float().norm() < 2e-2
+    e.close()
