@@ -63,7 +63,7 @@ def load_any(path) -> Dict[str, Any]:
 
 
 # ----------------------------------------------------------------------------- writer
-_BARE = re.compile(r"^[A-Za-z0-9_-]+$")
+_BARE = re.compile(r"[A-Za-z0-9_-]+")
 
 
 _ESC = {'"': '\\"', "\\": "\\\\", "\b": "\\b", "\t": "\\t", "\n": "\\n", "\f": "\\f", "\r": "\\r"}
@@ -86,7 +86,7 @@ def _basic_str(s: str) -> str:
 
 
 def _key(k: str) -> str:
-    return k if _BARE.match(k) else _basic_str(k)
+    return k if _BARE.fullmatch(k) else _basic_str(k)  # fullmatch: "$" would accept a trailing newline
 
 
 def _scalar(v: Any) -> str:
