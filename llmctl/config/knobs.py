@@ -48,6 +48,7 @@ class PerfKnobs:
     fused_fwd: bool = False        # QKV+RoPE / up+SwiGLU epilogues in the forward GEMMs
     rope_inplace: bool = True      # RoPE applied in place on the q / k views
     fused_rope_attn: bool = True   # RoPE folded into the attention kernels' Q/K loads
+    moe_pad: bool = True           # MoE expert rows padded to multiples of 256 (gemm64 expert GEMMs)
     overlap_optimizer: bool = False  # ZeRO-0: per-bucket AdamW under the backward (measured neutral)
     gemm_tuning: bool = True       # hipBLASLt TunableOp solutions (configs/gemm_tuning/*.csv)
     # ---- attention kernels (native: flash_attn_fwd.hip / flash_attn_bwd.hip)

@@ -358,11 +358,17 @@ class _Linear(torch.autograd.Function):
             sink: Optional[GradSink] = getattr(ctx.wparam, "_llmctl_grad_sink", None)
             if sink is not None:
                 sink.write(ctx.wparam, dy2, x2)  # weight grad first: lets its bucket's comm start earlier
-            else:
-                dw = dy2.t().matmul(x2)
+            else:  # an ordinary gradient (AccumulateGrad adds it), still on the MFMA kernels when they fit
+                dw = torch.empty_like(w)
+                wgrad_into(dw, dy2, x2, accumulate=False)
         dx = None
         if ctx.needs_input_grad[0]:
-            if dgrad64_ok(dy2, w):
+            # an unsinked weight keeps no W^T copy, so its alternative is hipBLASLt's slower "NN"
+            # layout: gemm64 (W read K-major) whenever the shape fits, unless knob dgrad64 is off
+            free = getattr(ctx.wparam, "_llmctl_grad_sink", None) is None and knobs().dgrad64 != "off"
+            if dgrad64_ok(dy2, w) or (free and dy2.is_cuda and dy2.dtype == torch.bfloat16 and _rows_ok(dy2)
+                                      and _gemm64_ok(dy2.shape[0], w.shape[1], w.shape[0], w)
+                                      and w.shape[0] * w.stride(0) * 2 < 2**31):
                 dx = dgrad64(dy2, w).view(*dy.shape[:-1], w.shape[1])
             elif ctx.wt is not None:
                 GradSink.wait_weight_t(ctx.wparam)
@@ -374,8 +380,13 @@ class _Linear(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``x @ w^T (+ b)`` on hipBLASLt; weight grads go through the parameter's sink if any."""
-    if getattr(w, "_llmctl_grad_sink", None) is None or not torch.is_grad_enabled():
+    """``x @ w^T (+ b)`` (``forward_linear``: gemm64 or hipBLASLt); weight grads go through the
+    parameter's sink if any.  Whenever a gradient is needed the call goes through ``_Linear`` — the
+    gemm64 forward is a plain kernel call that autograd cannot see, so an unsinked weight (MoE
+    experts, tied heads) taking that route from ``forward_linear`` directly would get no gradient."""
+    needs_grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad
+                                              or (b is not None and b.requires_grad))
+    if not needs_grad:
         return forward_linear(x, w, b)
     return _Linear.apply(x, w, b)
 

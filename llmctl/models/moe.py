@@ -124,15 +124,29 @@ class MoEMLP(nn.Module):
         else:
             xe = xs
             local_counts = counts.tolist()
-        outs = []
-        o = 0
-        for e, n in enumerate(local_counts):
-            if n == 0:
-                continue
-            seg = xe[o:o + n]
-            o += n
-            outs.append(linear(ops.swiglu(linear(seg, self.experts_up[e])), self.experts_down[e]))
-        ye = torch.cat(outs, 0) if outs else xe.new_zeros((0, h))
+        pad = self._pad_rows(xe, local_counts)
+        if pad is not None:
+            # every expert's rows padded with zero rows to a multiple of 256: all expert GEMMs -- the
+            # token-deep weight gradients included -- then take gemm64's shapes (hipBLASLt's
+            # weight-gradient layout runs ~1.0 PF); zero rows contribute zero outputs and gradients
+            dst, padded = pad
+            xp = xe.new_zeros((sum(padded), h)).index_copy(0, dst, xe)
+            outs, o = [], 0
+            for e, n in enumerate(padded):
+                if n:
+                    outs.append(linear(ops.swiglu(linear(xp[o:o + n], self.experts_up[e])), self.experts_down[e]))
+                    o += n
+            ye = torch.cat(outs, 0).index_select(0, dst) if outs else xe.new_zeros((0, h))
+        else:
+            outs = []
+            o = 0
+            for e, n in enumerate(local_counts):
+                if n == 0:
+                    continue
+                seg = xe[o:o + n]
+                o += n
+                outs.append(linear(ops.swiglu(linear(seg, self.experts_up[e])), self.experts_down[e]))
+            ye = torch.cat(outs, 0) if outs else xe.new_zeros((0, h))
         if self.ep > 1:
             inv = torch.empty_like(perm_t)
             inv[perm_t] = torch.arange(perm_t.numel(), device=x.device)
@@ -141,6 +155,25 @@ class MoEMLP(nn.Module):
             ys = ye
         w = topw.reshape(-1).index_select(0, order).to(ys.dtype).unsqueeze(-1)
         return torch.zeros_like(x).index_add(0, tok, ys * w)
+
+
+    def _pad_rows(self, xe: torch.Tensor, counts: List[int]):
+        """(destination row of every expert row in the padded buffer, padded count per expert), or
+        None: GPU only (gemm64 shapes), knob ``moe_pad``."""
+        from llmctl.config.knobs import knobs
+
+        if not (knobs().moe_pad and xe.is_cuda and xe.dtype == torch.bfloat16 and xe.shape[1] % 128 == 0
+                and self.experts_up[0].shape[0] % 256 == 0 and self.experts_down[0].shape[0] % 256 == 0
+                and self.experts_down[0].shape[1] % 128 == 0):
+            return None
+        padded = [(n + 255) // 256 * 256 for n in counts]
+        idx, o = [], 0
+        for n, npad in zip(counts, padded):
+            idx.append(torch.arange(o, o + n))
+            o += npad
+        dst = torch.cat(idx).to(xe.device, non_blocking=True) if idx else torch.zeros(0, dtype=torch.long,
+                                                                                       device=xe.device)
+        return dst, padded
 
 
 def expert_param_global_name(name: str, module_e0: int) -> str:
