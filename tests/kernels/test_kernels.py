@@ -907,3 +907,20 @@ def test_rope_flash_attention_inplace_matches(native_lib, with_pos):
         outs.append((o.detach(), leaf.grad))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_linear_unsinked_weight_gets_gradient_on_gemm64_route(native_lib):
+    """An unsinked weight whose forward shape takes the gemm64 route (N >= 16384, M <= 8192) still
+    gets its gradient through ``linear`` (the kernel call is invisible to autograd, so ``linear``
+    wraps it in ``_Linear``), and its data gradient (gemm64, W read K-major) matches fp32."""
+    from llmctl.exec.linear import linear
+
+    x = _bf(512, 256, seed=31).requires_grad_(True)
+    w = torch.nn.Parameter(_bf(16384, 256, seed=32, scale=0.05))
+    dy = _bf(512, 16384, seed=33)
+    y = linear(x, w)
+    assert y.grad_fn is not None
+    y.backward(dy)
+    assert w.grad is not None and x.grad is not None
+    assert _row_err(w.grad, dy.float().t() @ x.detach().float()) < 1.5e-2
+    assert _row_err(x.grad, dy.float() @ w.detach().float()) < 1.5e-2
