@@ -722,3 +722,26 @@ def test_sampling_oracle_property():
         assert int(ref.sample(logits, T, K, P, torch.tensor([0.0]))[0]) == first
 
     check()
+
+
+def test_prefill_work_list_property():
+    """Property test (hypothesis): the paged-prefill work list holds every (chunk, 128-row q-block)
+    exactly once, decodable from ``(chunk << 16) | block``, ordered by non-increasing causal span."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from llmctl.ops.functional import prefill_work_list
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.lists(st.integers(0, 3000), min_size=1, max_size=40))
+    def check(lens):
+        cu = [0]
+        for n in lens:
+            cu.append(cu[-1] + n)
+        work = prefill_work_list(cu)
+        got = [(w >> 16, w & 0xFFFF) for w in work]
+        want = {(i, b) for i, n in enumerate(lens) for b in range((n + 127) // 128)}
+        assert len(got) == len(want) and set(got) == want
+        assert all(a[1] >= b[1] for a, b in zip(got, got[1:]))
+
+    check()
